@@ -1,0 +1,198 @@
+/* ltx_hip.h -- C ABI of libltxhip.so, the MI355X (gfx950) kernels behind the LTX-Video 2B
+ * LoRA training step of lusinlu/Video-Generation-for-Human-Avatars.
+ *
+ * The reference has no native layer: every entry point below replaces a torch / diffusers /
+ * peft eager op sequence on the path ltx_video/training.py:94-166 drives. Each declaration
+ * cites the reference call site it stands in for. The Python host mirror
+ * (video-generation-for-human-avatars_amd/ltx_amd) binds these with ctypes; INTEGRATION.md shows
+ * the binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *  - Plain pointers to DEVICE memory, int64 sizes / leading dims in ELEMENTS, row-major.
+ *  - "bf16" buffers hold raw bfloat16 bits; "f32" buffers IEEE float.
+ *  - Caller owns every buffer (inputs, outputs, saved-for-backward, workspaces); nothing is
+ *    retained or freed across calls.
+ *  - `stream` is a hipStream_t; every call is asynchronous and stream-ordered, no host sync.
+ *  - Return 0 (LTX_OK) or an error code (a hipError_t value, or LTX_ERR_*); shape / alignment
+ *    checks run on the host before any launch. ltx_last_error() gives a thread-local message.
+ */
+#ifndef LTX_HIP_H_
+#define LTX_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  LTX_OK = 0,
+  LTX_ERR_BAD_ARG = 1000,
+  LTX_ERR_UNSUPPORTED = 1001,
+};
+
+/* GEMM epilogues (ltx_gemm_bf16_nt `epilogue`). y = bf16(acc + bias) first, then: */
+enum {
+  LTX_EPI_STORE = 0,            /* C = y                                        nn.Linear */
+  LTX_EPI_GELU = 1,             /* aux0 <- y (pre-act, optional); C = bf16(gelu_tanh(y))
+                                   attention.py:1237-1238 (diffusers GELU tanh), PixArt proj */
+  LTX_EPI_GATED_RESIDUAL = 2,   /* C = bf16(R + bf16(gate[b] * y)); R = aux0, gate = aux1 row b =
+                                   m / rows_per_batch (row stride ld1)    attention.py:265-268,305-308 */
+  LTX_EPI_LORA = 3,             /* C = bf16(y + alpha * U[m,:].Lb[n,:]); U = aux1 f32 [M,rank],
+                                   Lb = aux2 f32 [N,rank]      peft lora.Linear, training.py:50-68 */
+  LTX_EPI_LORA_RESIDUAL = 4,    /* C = bf16(R + bf16(LORA)); R = aux0        attention.py:285 */
+  LTX_EPI_GELU_BWD = 5,         /* C = bf16(bf16(acc) * gelu_tanh'(F)); F = aux0 (pre-act) */
+  LTX_EPI_ACCUM = 6,            /* C = bf16(R + bf16(acc)); R = aux0 (may alias C) */
+  LTX_EPI_LORA_DGRAD_ACCUM = 7, /* C = [R +] bf16(bf16(acc) + bf16(alpha * Wd[m,:].A[:,n]));
+                                   Wd = aux1 f32 [M,rank], A = aux2 f32 [rank,N], R = aux0 opt. */
+};
+
+int ltx_abi_version(void);
+const char* ltx_last_error(void);
+/* Device properties the host mirror checks before running (gfx arch number, CU count). */
+int ltx_device_info(int* gfx_arch, int* num_cus);
+
+/* ---- K1: SymmetricPatchifier (symmetric_patchifier.py:33-84), bit exact ---------------------- */
+/* latents [B,C,F,H,W] bf16 -> tokens [B,F*H*W,C] bf16                    (patchify :55-65) */
+int ltx_patchify_bf16(const void* latents, void* tokens, int64_t B, int64_t C, int64_t F,
+                      int64_t H, int64_t W, void* stream);
+/* tokens [B,F*H*W,C] -> latents [B,C,F,H,W]                              (unpatchify :67-84) */
+int ltx_unpatchify_bf16(const void* tokens, void* latents, int64_t B, int64_t C, int64_t F,
+                        int64_t H, int64_t W, void* stream);
+/* coords [B,3,F*H*W] int64 (t,h,w), w fastest                   (get_latent_coords :33-51) */
+int ltx_latent_coords(int64_t* coords, int64_t B, int64_t F, int64_t H, int64_t W, void* stream);
+
+/* ---- K4: rectified flow (rf.py:376-426, training.py:138-146) ----------------------------------- */
+/* x_t = bf16((1-t)x0 + t*eps), v = bf16(eps - x0) in f32; x0/eps [B,N,C] bf16, t [B] f32 */
+int ltx_rf_noise_velocity(const void* tokens, const void* noise, const float* t, void* x_t,
+                          void* v_target, int64_t B, int64_t NC, void* stream);
+/* ---- K2: conditioning lerp of Transformer3DModel.forward (transformer3d.py:447-466) ----------- */
+/* tokens [B,F*H*W,C] -> out tokens: frame 0 = lerp(x, ref, 0.85), frames >=1 lerp(x, pose, 0.5),
+ * torch.lerp float formula, bf16 result. ref [B,C,1,H,W], pose [B,C,F,H,W]. out may alias tokens. */
+int ltx_condition_lerp(const void* tokens, const void* ref, const void* pose, void* out,
+                       int64_t B, int64_t C, int64_t F, int64_t H, int64_t W, void* stream);
+/* Fused K1+K4+K2 for one train step: latents/pose [B,C,F,H,W], ref [B,C,1,H,W], noise [B,N,C]
+ * (all bf16), t [B] f32 -> x_t (pre-lerp, optional), model_in (post-lerp) and v_target, [B,N,C]. */
+int ltx_rf_prepare_tokens(const void* latents, const void* ref, const void* pose,
+                          const void* noise, const float* t, void* x_t, void* model_in,
+                          void* v_target, int64_t B, int64_t C, int64_t F, int64_t H, int64_t W,
+                          void* stream);
+
+/* ---- K8: RMSNorm (no affine) + AdaLN modulate (attention.py:223-239, 288-290) --------------- */
+/* y = bf16(bf16(bf16(x*rstd) * onep[b]) + shift[b]); rstd = rsqrt(mean(x^2)+eps) (f32, saved).
+ * x [M,D] bf16; shift/onep rows of D bf16 with row stride ld_mod per batch b = m / rows_per_batch. */
+int ltx_rmsnorm_modulate_fwd(const void* x, const void* shift, const void* onep, int64_t ld_mod,
+                             void* y, float* rstd, int64_t M, int64_t D, int64_t rows_per_batch,
+                             float eps, void* stream);
+/* dx = [dres +] d/dx of the above given dy (mirrors eager autograd roundings). dx may alias dres. */
+int ltx_rmsnorm_modulate_bwd(const void* dy, const void* x, const float* rstd, const void* onep,
+                             int64_t ld_mod, const void* dres, void* dx, int64_t M, int64_t D,
+                             int64_t rows_per_batch, void* stream);
+/* modulation rows: out[b,j,:] = bf16(sst[j,:] + tmod[b*ld_tmod + j*ld_j + :]) and, for the
+ * rows flagged in scale_mask (bit j), onep = bf16(1 + that) (attention.py:229-239 with ld_j = D;
+ * transformer3d.py:554-560 with ld_j = 0, the embedded timestep broadcast). out/onep [B,P,D]. */
+int ltx_ada_modulation(const void* sst, const void* tmod, int64_t ld_tmod, int64_t ld_j,
+                       void* out, void* onep_out, int64_t B, int64_t P, int64_t D,
+                       int64_t scale_mask, void* stream);
+/* out = bf16(dy * gate[b]) per row, b = m / rows_per_batch (grad of `gate * y`,
+ * attention.py:265-266, 305-306). dy/out [M,D] dense, gate rows of ld_gate. */
+int ltx_gate_mul_bf16(const void* dy, const void* gate, int64_t ld_gate, void* out, int64_t M,
+                      int64_t D, int64_t rows_per_batch, void* stream);
+
+/* ---- K17: output LayerNorm (no affine) + modulate (transformer3d.py:554-561) ---------------- */
+int ltx_layernorm_modulate_fwd(const void* x, const void* shift, const void* onep, int64_t ld_mod,
+                               void* y, float* mean, float* rstd, int64_t M, int64_t D,
+                               int64_t rows_per_batch, float eps, void* stream);
+int ltx_layernorm_modulate_bwd(const void* dy, const void* x, const float* mean,
+                               const float* rstd, const void* onep, int64_t ld_mod, void* dx,
+                               int64_t M, int64_t D, int64_t rows_per_batch, void* stream);
+
+/* ---- K9 tail: q/k RMSNorm (affine, eps 1e-5, across all heads) + 3-D RoPE ------------------- */
+/* q_out = rope(bf16(bf16(q_in * rstd) * q_weight)) (attention.py:996-1012, RoPE :917-932), same
+ * for k. cos/sin of transformer3d.py:221-277 are formed in-kernel: omega [D/6] f32 is the
+ * reference's `theta ** linspace(0,1,D//6) * pi/2` table (computed once on the host),
+ * phi = omega[j] * (grid[b,a,n]/max_pos[a]*2 - 1), D%6 leading pad dims (cos 1, sin 0); grid is
+ * [B,3,N] int64 (grid_is_float == 0) or f32. rope == 0 skips the rotation (cross-attention).
+ * k_in / k_out may be null (q only). Saves f32 rstd_q / rstd_k [M] (M = B*N rows). */
+int ltx_qk_norm_rope_fwd(const void* q_in, int64_t ldq_in, const void* k_in, int64_t ldk_in,
+                         void* q_out, int64_t ldq_out, void* k_out, int64_t ldk_out,
+                         const void* q_weight, const void* k_weight, float* rstd_q,
+                         float* rstd_k, const void* indices_grid, int grid_is_float, int64_t B,
+                         int64_t N, int64_t D, const float* omega, float max_pos_t,
+                         float max_pos_h, float max_pos_w, int rope, float eps, void* stream);
+/* Backward: incoming dq (f32 when dq_is_f32, else bf16; it is rounded to bf16 first, as SDPA's
+ * backward returns bf16) -> dq_raw bf16, the gradient w.r.t. q_in; same for k. */
+int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const void* dk_in,
+                         int64_t ldk_in, int dk_is_f32, const void* q_raw, int64_t ldq_raw,
+                         const void* k_raw, int64_t ldk_raw, const void* q_weight,
+                         const void* k_weight, const float* rstd_q, const float* rstd_k,
+                         void* dq_out, int64_t ldq_out, void* dk_out, int64_t ldk_out,
+                         const void* indices_grid, int grid_is_float, int64_t B, int64_t N,
+                         int64_t D, const float* omega, float max_pos_t, float max_pos_h,
+                         float max_pos_w, int rope, void* stream);
+
+/* ---- K10/K14: flash attention (F.scaled_dot_product_attention, attention.py:1057-1064) ------- */
+/* Q [B,Nq,H,d] (row stride ldq per token, head h at column h*d), K/V [B,Nk,H,d], O likewise;
+ * lse [B,H,Nq] f32 in log2 units (saved for the backward); key_bias [B,Nk] f32 added to the scaled scores
+ * (encoder mask bias, transformer3d.py:441-445) or null. d in {32, 64}. */
+int ltx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                 int64_t ldv, void* o, int64_t ldo, float* lse, const float* key_bias, int64_t B,
+                 int64_t H, int64_t Nq, int64_t Nk, int64_t d, float scale, void* stream);
+/* Backward (deterministic, no atomics): delta[b,h,i] = sum_d dO*O (f32, caller workspace
+ * [B,H,Nq]); dQ [B,Nq,H,d] (f32 if dq_is_f32 else bf16, row stride lddq), dK/dV bf16. lse as
+ * written by ltx_attn_fwd (log2 units). */
+int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                 int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                 const float* lse, const float* key_bias, float* delta_ws, void* dq,
+                 int64_t lddq, int dq_is_f32, void* dk, int64_t lddk, void* dv, int64_t lddv,
+                 int64_t B, int64_t H, int64_t Nq, int64_t Nk, int64_t d, float scale,
+                 void* stream);
+
+/* ---- bf16 MFMA GEMM: C[M,N] = epilogue(A[M,K] . W[N,K]^T) ------------------------------------ */
+/* nn.Linear forward (W as stored) and dgrad (W^T packed once: frozen weights). K % 64 == 0,
+ * N % 8 == 0, leading dims % 8 == 0, 16-B aligned operands. rank in {8,16,32} for LoRA. */
+int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
+                     int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue,
+                     const void* bias, const void* aux0, int64_t ld0, const void* aux1,
+                     int64_t ld1, const void* aux2, int64_t ld2, float alpha, int64_t rank,
+                     int64_t rows_per_batch, void* stream);
+
+/* ---- LoRA skinny contractions in f32 (peft lora_A / lora_B, training.py:50-68) --------------- */
+/* out[m,j] = alpha * sum_k x[m,k] * Wr[j,k], Wr element (j,k) at Wr[j*wj + k*wk]; x bf16 [M,K]
+ * (ldx), out f32 [M,r] (ldo). lora_A forward (u = x.A^T: wj = K, wk = 1) and the lora_B dgrad
+ * (w = s*dY.B with B f32 [N,r]: wj = 1, wk = r). r <= 32. */
+int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk,
+                  float* out, int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha,
+                  void* stream);
+/* dW(n,j) = alpha * sum_m Y[m,n] * U[m,j], stored at dw[n*on + j*oj] (f32, overwritten):
+ * lora_B grad (Y = dY, U = u: on = r, oj = 1) and lora_A grad (Y = x, U = w: on = 1, oj = K).
+ * Y bf16 [M,N] (ldy), U f32 [M,r] (ldu). Split-M partial sums are combined with f32 atomics. */
+int ltx_lora_wgrad(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw,
+                   int64_t on, int64_t oj, int64_t M, int64_t N, int64_t r, float alpha,
+                   void* stream);
+
+/* ---- small ops -------------------------------------------------------------------------------- */
+/* AdaLayerNormSingle sinusoid: out[b,:] = bf16([cos(s*t*f), sin(s*t*f)]) (256 ch), s = scale */
+int ltx_timestep_embedding(const float* t, float scale, void* out, int64_t B, int64_t dim,
+                           void* stream);
+int ltx_silu_bf16(const void* x, void* y, int64_t n, void* stream);
+/* bf16 [R,C] (ld_in) -> [C,R] (ld_out) */
+int ltx_transpose_bf16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int64_t R,
+                       int64_t C, void* stream);
+/* column sums of bf16 [M,N] -> bf16 [N] (bias grads; f32 accumulation) */
+int ltx_colsum_bf16(const void* x, int64_t ldx, void* out, int64_t M, int64_t N, void* stream);
+/* F.mse_loss(out, v) (mean) + its backward seed and std(v) (training.py:159-166):
+ * stats[0] = sum (o-v)^2 in f32 over bf16-rounded squares, stats[1] = sum v, stats[2] = sum v^2
+ * (f32 atomics into a zeroed 4-float buffer); dout = bf16(bf16(bf16(o-v) * 2/n) * gscale). */
+int ltx_mse_fwd_bwd(const void* out, const void* v, void* dout, float* stats, int64_t n,
+                    float grad_scale, void* stream);
+/* torch.optim.AdamW single-tensor step (training.py:270-271): f32 or bf16 param/state.
+ * is_bf16 selects the dtype of param/grad/exp_avg/exp_avg_sq (all the same). */
+int ltx_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n,
+                   int is_bf16, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int64_t step, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LTX_HIP_H_ */

@@ -1,0 +1,345 @@
+"""Per-kernel parity on the MI355X: every C-ABI entry point against a torch reference of the same
+op (the oracle's eager bf16 op sequence where rounding points matter, an fp32 torch evaluation
+for the MFMA contractions). Tolerances are written next to each check:
+  * integer / index / permutation work: bit exact;
+  * elementwise ops that mirror eager bf16 rounding: <= 1 bf16 ulp on a tiny fraction of entries;
+  * MFMA contractions (f32 accumulate, bf16 out): rel-Frobenius <= 1e-2 vs the fp32 evaluation.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import ltx_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from ltx_amd import _lib as L
+    L.ensure_device()
+    return L
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def ulps_bad(a, b, max_ulp=1):
+    """fraction of bf16 entries that differ by more than max_ulp ulps"""
+    ai = a.contiguous().view(torch.int16).to(torch.int32)
+    bi = b.contiguous().view(torch.int16).to(torch.int32)
+    return float(((ai - bi).abs() > max_ulp).float().mean())
+
+
+def g(*shape, dtype=torch.bfloat16, scale=1.0, seed=0):
+    gen = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=gen) * scale).to(dtype).to(DEV)
+
+
+# ------------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 136, 128), (1024, 2048, 2048), (8, 768, 256),
+                                   (14336 // 7, 6144, 2048)])
+def test_gemm_store(M, N, K):
+    from ltx_amd import ops
+    a, w, b = g(M, K, seed=1), g(N, K, seed=2, scale=K ** -0.5), g(N, seed=3)
+    out = ops.gemm(a, w, bias=b)
+    ref = a.float() @ w.float().t() + b.float()
+    assert rel(out, ref) < 1e-2
+    # bf16-rounded result must be within 1 ulp of the fp32 result rounded once
+    assert ulps_bad(out, ref.to(torch.bfloat16), 2) < 1e-3
+
+
+def test_gemm_strided_views_and_no_bias():
+    from ltx_amd import ops
+    M, K, N = 384, 256, 256
+    big = g(M, 3 * K, seed=4)
+    a = big[:, K:2 * K]  # row stride 3K
+    w = g(N, K, seed=5, scale=K ** -0.5)
+    outbuf = torch.zeros(M, 2 * N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(a, w, out=outbuf[:, N:])
+    ref = a.float() @ w.float().t()
+    assert rel(outbuf[:, N:], ref) < 1e-2
+    assert float(outbuf[:, :N].abs().max()) == 0.0
+
+
+def test_gemm_epilogues():
+    from ltx_amd import ops
+    M, N, K, r, B = 512, 256, 256, 16, 4
+    a, w, b = g(M, K, seed=6), g(N, K, seed=7, scale=K ** -0.5), g(N, seed=8)
+    y = (a.float() @ w.float().t() + b.float()).to(torch.bfloat16)
+    # GELU + pre-activation store
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out = ops.gemm(a, w, bias=b, epilogue="gelu", aux0=pre)
+    assert ulps_bad(pre, y, 2) < 1e-3
+    ref = F.gelu(pre.float(), approximate="tanh").to(torch.bfloat16)
+    assert ulps_bad(out, ref, 1) < 1e-3
+    # gated residual
+    R = g(M, N, seed=9)
+    gate = g(B, N, seed=10)
+    out = ops.gemm(a, w, bias=b, epilogue="gated_residual", aux0=R, aux1=gate, rows_per_batch=M // B)
+    ybf = y
+    ref = R + gate.repeat_interleave(M // B, 0) * ybf
+    assert rel(out, ref.float()) < 1e-2
+    # LoRA (+ residual)
+    u = torch.randn(M, r, device=DEV)
+    lb = torch.randn(N, r, device=DEV) * 0.1
+    out = ops.gemm(a, w, bias=b, epilogue="lora", aux1=u, aux2=lb, alpha=0.5, rank=r)
+    ref = (y.float() + 0.5 * (u @ lb.t())).to(torch.bfloat16)
+    assert ulps_bad(out, ref, 2) < 2e-3
+    out = ops.gemm(a, w, bias=b, epilogue="lora_residual", aux0=R, aux1=u, aux2=lb, alpha=0.5, rank=r)
+    assert rel(out, R.float() + ref.float()) < 1e-2
+    # GELU backward
+    Fpre = g(M, N, seed=11)
+    out = ops.gemm(a, w, epilogue="gelu_bwd", aux0=Fpre)
+    acc = (a.float() @ w.float().t()).to(torch.bfloat16).float()
+    x = Fpre.float()
+    ref = torch.ops.aten.gelu_backward(acc, x, approximate="tanh")
+    assert rel(out, ref) < 1e-2
+    # accumulate (in place on R)
+    R2 = R.clone()
+    ops.gemm(a, w, epilogue="accum", aux0=R2, out=R2)
+    assert rel(R2, R.float() + acc) < 1e-2
+    # LoRA dgrad accumulate: [R +] acc + alpha * Wd . A
+    Wd = torch.randn(M, r, device=DEV)
+    A = torch.randn(r, N, device=DEV) * 0.1
+    out = ops.gemm(a, w, epilogue="lora_dgrad_accum", aux0=R, aux1=Wd, aux2=A, alpha=1.0, rank=r)
+    assert rel(out, R.float() + acc + (Wd @ A).to(torch.bfloat16).float()) < 1e-2
+
+
+# ------------------------------------------------------------------------------------- attention
+def _sdpa_ref(q, k, v, B, H, d, bias=None):
+    Nq, Nk = q.shape[0] // B, k.shape[0] // B
+    qh = q.float().view(B, Nq, H, d).transpose(1, 2)
+    kh = k.float().view(B, Nk, H, d).transpose(1, 2)
+    vh = v.float().view(B, Nk, H, d).transpose(1, 2)
+    mask = None if bias is None else bias.view(B, 1, 1, Nk)
+    o = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask)
+    return o.transpose(1, 2).reshape(B * Nq, H * d)
+
+
+@pytest.mark.parametrize("B,H,Nq,Nk,d,masked", [(2, 4, 128, 128, 64, False), (1, 3, 100, 77, 64, True),
+                                                 (2, 4, 64, 4, 32, True), (2, 2, 256, 256, 32, False),
+                                                 (1, 32, 1792, 256, 64, True)])
+def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
+    from ltx_amd import ops
+    scale = d ** -0.5
+    q = g(B * Nq, H * d, seed=1)
+    k = g(B * Nk, H * d, seed=2)
+    v = g(B * Nk, H * d, seed=3)
+    bias = None
+    if masked:
+        keep = torch.arange(Nk, device=DEV)[None, :] < (Nk - 3 - torch.arange(B, device=DEV)[:, None]).clamp(min=2)
+        bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
+    o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias)
+    ref = _sdpa_ref(q, k, v, B, H, d, bias)
+    assert rel(o, ref) < 1e-2
+    # lse (log2 units) vs logsumexp of the scaled scores
+    qh = q.float().view(B, Nq, H, d).transpose(1, 2)
+    kh = k.float().view(B, Nk, H, d).transpose(1, 2)
+    sc = qh @ kh.transpose(-1, -2) * scale
+    if bias is not None:
+        sc = sc + bias.view(B, 1, 1, Nk)
+    lse_ref = torch.logsumexp(sc, -1) * (1 / math.log(2))
+    assert float((lse - lse_ref).abs().max()) < 1e-2
+    # backward vs fp32 autograd
+    do = g(B * Nq, H * d, seed=4)
+    qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    _sdpa_ref(qf, kf, vf, B, H, d, bias).backward(do.float())
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias)
+    assert rel(dq, qf.grad) < 2e-2
+    assert rel(dk, kf.grad) < 2e-2
+    assert rel(dv, vf.grad) < 2e-2
+    dq32, _, _ = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, dq_f32=True)
+    assert rel(dq32, qf.grad) < 2e-2
+
+
+def test_attention_strided_fused_qkv():
+    """Q/K/V read in place from the fused [M, 3*H*d] projection buffer (attn1 layout)."""
+    from ltx_amd import ops
+    B, H, N, d = 2, 4, 192, 64
+    D = H * d
+    qkv = g(B * N, 3 * D, seed=5)
+    q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+    o, _ = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5)
+    assert rel(o, _sdpa_ref(q, k, v, B, H, d)) < 1e-2
+
+
+# ---------------------------------------------------------------------------------- normalisation
+def test_rmsnorm_modulate_fwd_bwd():
+    from ltx_amd import ops
+    B, N, D = 2, 96, 2048
+    x = g(B * N, D, seed=1)
+    sst = g(6, D, seed=2, scale=D ** -0.5)
+    tmod = g(B, 6 * D, seed=3)
+    mod, onep = ops.ada_modulation(sst, tmod, scale_mask=(1 << 1) | (1 << 4))
+    ada = sst[None] + tmod.view(B, 6, D)
+    assert torch.equal(mod, ada)
+    assert torch.equal(onep[:, 1], 1 + ada[:, 1])
+    shift, one = mod[:, 0], onep[:, 1]
+    y, rstd = ops.rmsnorm_modulate_fwd(x, shift, one, mod.stride(0), N, 1e-6)
+    xr = x.view(B, N, D).clone().requires_grad_(True)
+    ref = O.rmsnorm(xr, 1e-6) * (1 + ada[:, 1][:, None]) + ada[:, 0][:, None]
+    assert ulps_bad(y, ref.detach().view(B * N, D), 1) < 1e-3
+    dy = g(B * N, D, seed=4)
+    dres = g(B * N, D, seed=5)
+    dx = ops.rmsnorm_modulate_bwd(dy, x, rstd, one, mod.stride(0), N, dres=dres)
+    ref.backward(dy.view(B, N, D))
+    assert rel(dx, xr.grad.view(B * N, D).float() + dres.float()) < 5e-3
+
+
+def test_layernorm_modulate_fwd_bwd():
+    from ltx_amd import ops
+    B, N, D = 2, 64, 2048
+    x = g(B * N, D, seed=6)
+    sst = g(2, D, seed=7, scale=D ** -0.5)
+    emb = g(B, D, seed=8)
+    mod, onep = ops.ada_modulation(sst, emb, scale_mask=1 << 1, broadcast=True)
+    # reference: transformer3d.py:554-560 (shift = row 0, scale = row 1, both sst + emb)
+    ssv = sst[None] + emb[:, None]
+    y, mean, rstd = ops.layernorm_modulate_fwd(x, mod[:, 0], onep[:, 1], mod.stride(0), N, 1e-6)
+    xr = x.view(B, N, D).clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (D,), eps=1e-6) * (1 + ssv[:, 1][:, None]) + ssv[:, 0][:, None]
+    assert ulps_bad(y, ref.detach().view(B * N, D), 1) < 2e-3
+    dy = g(B * N, D, seed=9)
+    dx = ops.layernorm_modulate_bwd(dy, x, mean, rstd, onep[:, 1], mod.stride(0), N)
+    ref.backward(dy.view(B, N, D))
+    assert rel(dx, xr.grad.view(B * N, D)) < 5e-3
+
+
+@pytest.mark.parametrize("D,grid_float", [(2048, False), (128, False), (2048, True)])
+def test_qk_norm_rope_fwd_bwd(D, grid_float):
+    from ltx_amd import ops
+    B, F_, H_, W_ = 2, 3, 4, 5
+    N = F_ * H_ * W_
+    coords = O.latent_coords(F_, H_, W_, B, DEV)
+    if grid_float:
+        coords = coords.float() * torch.tensor([8.0, 32.0, 32.0], device=DEV).view(1, 3, 1) / 25.0
+    rope = ops.RopeSpec(coords, D, 10000.0, [20, 2048, 2048])
+    qkv = g(B * N, 3 * D, seed=1)
+    qw, kw = g(D, seed=2, scale=0.1) + 1, g(D, seed=3, scale=0.1) + 1
+    q_out, k_out, rq, rk = ops.qk_norm_rope_fwd(qkv[:, :D], qkv[:, D:2 * D], qw, kw, rope)
+    cos, sin = O.rope_freqs(coords.cpu(), D, 10000.0, [20, 2048, 2048], torch.bfloat16)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    qi = qkv[:, :D].reshape(B, N, D).clone().requires_grad_(True)
+    ki = qkv[:, D:2 * D].reshape(B, N, D).clone().requires_grad_(True)
+    qr = O.apply_rotary_emb(O.rmsnorm(qi, 1e-5, qw), cos, sin)
+    kr = O.apply_rotary_emb(O.rmsnorm(ki, 1e-5, kw), cos, sin)
+    # device sincos vs host libm can flip a bf16 table entry: allow a small fraction of 1-ulp
+    assert ulps_bad(q_out, qr.detach().reshape(B * N, D), 1) < 5e-3
+    assert rel(q_out, qr.detach().reshape(B * N, D)) < 5e-3
+    assert rel(k_out, kr.detach().reshape(B * N, D)) < 5e-3
+    dq = g(B * N, D, seed=4)
+    dk = g(B * N, D, seed=5)
+    dq_raw, dk_raw = ops.qk_norm_rope_bwd(dq, qkv[:, :D], qw, rq, dk, qkv[:, D:2 * D], kw, rk, rope)
+    (qr * dq.view(B, N, D)).sum().backward()
+    (kr * dk.view(B, N, D)).sum().backward()
+    assert rel(dq_raw, qi.grad.reshape(B * N, D)) < 1e-2
+    assert rel(dk_raw, ki.grad.reshape(B * N, D)) < 1e-2
+    # q-only / no-rope variant (attn2 q_norm) + f32 incoming gradient
+    q2, _, rq2, _ = ops.qk_norm_rope_fwd(qkv[:, :D], None, qw, None, None, B=B, N=N)
+    assert ulps_bad(q2, O.rmsnorm(qkv[:, :D], 1e-5, qw), 1) < 1e-3
+    dq2, _ = ops.qk_norm_rope_bwd(dq.float(), qkv[:, :D], qw, rq2, B=B, N=N)
+    qi2 = qkv[:, :D].clone().requires_grad_(True)
+    O.rmsnorm(qi2, 1e-5, qw).backward(dq)
+    assert rel(dq2, qi2.grad) < 1e-2
+
+
+# ------------------------------------------------------------------------- patchify / rf / misc
+def test_patchify_coords_bit_exact():
+    from ltx_amd import ops
+    for (B, C, F_, H_, W_) in [(2, 128, 7, 16, 16), (1, 8, 3, 4, 5), (2, 3, 1, 8, 8)]:
+        lat = g(B, C, F_, H_, W_, seed=1)
+        tok = ops.patchify(lat)
+        ref, coords = O.patchify(lat)
+        assert torch.equal(tok, ref)
+        assert torch.equal(ops.latent_coords(B, F_, H_, W_, DEV), coords)
+        assert torch.equal(ops.unpatchify(tok, F_, H_, W_), lat)
+
+
+def test_rf_prepare_tokens():
+    from ltx_amd import ops
+    B, C, F_, H_, W_ = 2, 128, 3, 8, 8
+    lat, ref, pose = g(B, C, F_, H_, W_, seed=1), g(B, C, 1, H_, W_, seed=2), g(B, C, F_, H_, W_, seed=3)
+    tok, _ = O.patchify(lat)
+    noise = g(*tok.shape, seed=4)
+    t = torch.tensor([0.3, 0.77], device=DEV)
+    x_t, model_in, v = ops.rf_prepare_tokens(lat, ref, pose, noise, t, want_x_t=True)
+    x_ref = O.add_noise(tok, noise, t).to(torch.bfloat16)
+    v_ref = O.velocity_target(tok, noise, t).to(torch.bfloat16)
+    assert torch.equal(x_t, x_ref)
+    assert torch.equal(v, v_ref)
+    u = O.unpatchify(x_ref.clone(), H_, W_, C)
+    u[:, :, 0:1] = torch.lerp(u[:, :, 0:1], ref, 0.85)
+    u[:, :, 1:] = torch.lerp(u[:, :, 1:], pose[:, :, 1:], 0.5)
+    mi_ref, _ = O.patchify(u)
+    assert torch.equal(model_in, mi_ref)
+    assert torch.equal(ops.condition_lerp(x_t, ref, pose), mi_ref)
+    x2, v2 = ops.rf_noise_velocity(tok, noise, t)
+    assert torch.equal(x2, x_ref) and torch.equal(v2, v_ref)
+
+
+def test_timestep_silu_transpose_colsum():
+    from ltx_amd import ops
+    t = torch.tensor([0.01, 0.5, 0.999, 0.25], device=DEV)
+    emb = ops.timestep_embedding(t, 1000.0)
+    ref = O.timestep_embedding(1000 * t).to(torch.bfloat16)
+    assert ulps_bad(emb, ref, 1) < 1e-2 and rel(emb, ref) < 5e-3
+    x = g(37, 2048, seed=3)
+    assert ulps_bad(ops.silu(x), F.silu(x), 1) < 1e-3
+    x = g(300, 136, seed=4)
+    assert torch.equal(ops.transpose(x), x.t().contiguous())
+    cs = ops.colsum(x)
+    assert rel(cs, x.float().sum(0)) < 5e-3
+
+
+def test_lora_kernels():
+    from ltx_amd import ops
+    M, K, N, r = 1000, 2048, 2048, 16
+    x = g(M, K, seed=1)
+    A = torch.randn(r, K, device=DEV) / K ** 0.5
+    Bm = torch.randn(N, r, device=DEV) * 0.05
+    u = ops.lora_down(x, A)
+    assert rel(u, x.float() @ A.t()) < 1e-5
+    dy = g(M, N, seed=2)
+    w = ops.lora_down(dy, Bm, alpha=0.5, transposed=True)
+    assert rel(w, 0.5 * dy.float() @ Bm) < 1e-5
+    dB = ops.lora_wgrad(dy, u, alpha=0.5)
+    assert rel(dB, 0.5 * dy.float().t() @ u) < 1e-5
+    dA = ops.lora_wgrad(x, w, transpose_out=True)
+    assert rel(dA, w.t() @ x.float()) < 1e-5
+
+
+def test_mse_and_adamw():
+    from ltx_amd import ops
+    o, v = g(2, 64, 128, seed=1), g(2, 64, 128, seed=2)
+    stats, dout = ops.mse_fwd_bwd(o, v, grad_scale=1 / 16)
+    n = o.numel()
+    oo = o.clone().requires_grad_(True)
+    loss = F.mse_loss(oo, v)
+    (loss / 16).backward()
+    assert abs(float(stats[0]) / n - float(loss)) < 1e-2 * float(loss)
+    assert ulps_bad(dout, oo.grad, 1) < 1e-3
+    std = torch.sqrt((stats[2] - stats[1] ** 2 / n) / (n - 1))
+    assert abs(float(std) - float(v.float().std())) < 1e-3
+    for dtype in (torch.float32, torch.bfloat16):
+        p0 = g(4096, dtype=dtype, seed=3)
+        grads = [g(4096, dtype=dtype, seed=10 + i) for i in range(3)]
+        pt = torch.nn.Parameter(p0.clone())
+        opt = torch.optim.AdamW([pt], lr=1e-4)
+        mine = p0.clone()
+        m = torch.zeros_like(mine)
+        vv = torch.zeros_like(mine)
+        for step, gr in enumerate(grads, start=1):
+            pt.grad = gr.clone()
+            opt.step()
+            ops.adamw_step(mine, gr, m, vv, 1e-4, 0.9, 0.999, 1e-8, 0.01, step)
+        if dtype == torch.float32:
+            assert rel(mine, pt.detach()) < 1e-6
+        else:
+            assert ulps_bad(mine, pt.detach(), 1) < 1e-3

@@ -1,0 +1,537 @@
+// Flash attention for the LTX-Video blocks on gfx950 (F.scaled_dot_product_attention,
+// attention.py:1057-1064): self-attention over the spatio-temporal tokens (no mask) and the
+// attn2 cross-attention over the caption tokens with the key-padding bias (1-mask)*-10000
+// (transformer3d.py:441-445). Head dim 64 (LTX-2B) or 32 (tiny config).
+//
+// All products use v_mfma_f32_32x32x16_bf16 in the "swapped" orientation: the softmax axis
+// lives in the accumulator REGISTERS and the other axis on the lanes, so
+//   * row statistics need no cross-lane shuffles except one xor-32 exchange,
+//   * the bf16-packed accumulator is directly the B operand of the next product (sum over the
+//     register axis), and the matching A operand comes from a transposed LDS read
+//     (ds_read_b64_tr_b16) of a row-major tile -- no LDS round trip for P or dS.
+// LDS tiles are row-major [rows][HD] bf16 with a 16-B chunk XOR swizzle
+// (chunk ^ ((row >> 1) & (HD/8 - 1))): conflict-free for the 16-B row reads of a 32-row fragment.
+//
+// Forward: a workgroup = 4 waves x 32 queries; K/V tiles of 64 keys are register-prefetched
+// (global -> VGPR while the current tile computes) and written to LDS after a barrier.
+// Per 64-key tile a wave runs 8 MFMAs for S^T = K.Q^T and 8 for O^T += V^T.P^T.
+// lse is stored in log2 units: lse2 = max2 + log2(sum 2^(s*log2e - max2)).
+//
+// Backward (deterministic, no atomics): dq_kernel (workgroup = 128 queries, loop over keys:
+// S^T, dP^T = V.dO^T, dS^T, dQ^T += K^T.dS^T) and dkdv_kernel (workgroup = 128 keys, each wave's
+// 32 keys' K/V fragments in registers, loop over 32-query tiles: S, dP, dV^T += dO^T.P,
+// dK^T += Q^T.dS). Recomputing S/dP in both costs two extra products per tile but removes the
+// f32 atomics a fused kernel needs for dQ (which on MI355X would be bound by the ~1.3 TB/s
+// atomic rate at these sizes).
+#include "common.h"
+#include "ltx_hip.h"
+
+namespace ltx {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr int ATT_THREADS = 256;
+
+template <int HD>
+__device__ __forceinline__ int toff(int row, int chunk) {
+  constexpr int CH = HD / 8;
+  return row * (HD * 2) + ((chunk ^ ((row >> 1) & (CH - 1))) << 4);
+}
+
+// 16-B row fragment: lane reads row (base + (l&31)), dims ks*16 + 8*(l>>5) .. +7
+template <int HD>
+__device__ __forceinline__ s16x8 row_frag(const char* tile, int base, int ks, int lane) {
+  return *(const s16x8*)(tile + toff<HD>(base + (lane & 31), ks * 2 + (lane >> 5)));
+}
+
+// Transposed fragment for an A operand that sums over the tile's ROW axis, matching an
+// accumulator-as-B operand (k-step s of a 32-row accumulator tile): element j of lane half h
+// is row 16s + 8(j>>2) + 4h + (j&3) (+ rbase), column c0 + (lane & 31).
+template <int HD>
+__device__ __forceinline__ s16x8 tr_frag(const char* tile, int rbase, int s, int c0, int lane) {
+  const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane & 15) >> 2, p = lane & 3;
+  const int col = c0 + 16 * g + 4 * p;
+  const int row = rbase + 16 * s + 4 * h + q;
+  const char* a0 = tile + toff<HD>(row, col >> 3) + ((col & 7) << 1);
+  const char* a1 = tile + toff<HD>(row + 8, col >> 3) + ((col & 7) << 1);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+  s16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+// accumulator registers 8s..8s+7 -> bf16 B-operand fragment for k-step s
+__device__ __forceinline__ s16x8 acc_frag(const f32x16& a, int s) {
+  s16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(a[8 * s + j]);
+  return r;
+}
+
+__device__ __forceinline__ f32x16 mfma32(const s16x8& a, const s16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// row (in the register axis) of accumulator register r for lane half h
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// global 16-B loads of a [ROWS][HD] tile (rows clamped), staged in registers, written swizzled
+template <int HD, int ROWS>
+struct TileStage {
+  static constexpr int CH = HD / 8;
+  static constexpr int PER = (ROWS * CH + ATT_THREADS - 1) / ATT_THREADS;
+  u32x4 v[PER];
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int row0, int nrows, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = tid + i * ATT_THREADS;
+      if (idx < ROWS * CH) {
+        const int r = idx / CH, c = idx % CH;
+        const int gr = min(row0 + r, nrows - 1);
+        v[i] = *(const u32x4*)(base + (int64_t)gr * ld + c * 8);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* tile, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = tid + i * ATT_THREADS;
+      if (idx < ROWS * CH) {
+        const int r = idx / CH, c = idx % CH;
+        *(u32x4*)(tile + toff<HD>(r, c)) = v[i];
+      }
+    }
+  }
+};
+
+struct AttnParams {
+  const bf16_t* q; int64_t ldq;
+  const bf16_t* k; int64_t ldk;
+  const bf16_t* v; int64_t ldv;
+  const bf16_t* o; int64_t ldo;      // forward output (bwd: the saved output, for delta)
+  bf16_t* o_out;
+  const bf16_t* dout; int64_t lddo;
+  float* lse;                          // [B,H,Nq] log2 units
+  const float* delta;                  // [B,H,Nq]
+  const float* key_bias;               // [B,Nk] natural units, or null
+  void* dq; int64_t lddq; int dq_f32;  // dQ output
+  bf16_t* dk; int64_t lddk;
+  bf16_t* dv; int64_t lddv;
+  int B, H, Nq, Nk;
+  float scale;
+};
+
+// per-key additive term in log2 units for keys key0..key0+63 -> LDS
+__device__ __forceinline__ void key_bias_tile(float* kb, const AttnParams& p, int b, int key0, int n, int tid) {
+  if (tid < n) {
+    const int key = key0 + tid;
+    float v = -INFINITY;
+    if (key < p.Nk) v = p.key_bias ? p.key_bias[(int64_t)b * p.Nk + key] * LOG2E : 0.f;
+    kb[tid] = v;
+  }
+}
+
+// =============================================================================================
+// forward (MODE 0) and dQ (MODE 1): queries on lanes, keys in registers
+// =============================================================================================
+template <int HD, int MODE>
+__global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams p) {
+  constexpr int KT = 64;                 // keys per tile
+  constexpr int KS = HD / 16;            // 16-deep k-steps over the head dim
+  constexpr int DS = HD / 32;            // 32-wide d subtiles
+  constexpr int TILE = KT * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
+  __shared__ float kb[KT];
+  char* ktile = smem;
+  char* vtile = smem + TILE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int qi = q0 + (lane & 31);
+  const int qc = min(qi, p.Nq - 1);
+  const float c2 = p.scale * LOG2E;
+
+  const bf16_t* kbase = p.k + (int64_t)b * p.Nk * p.ldk + hh * HD;
+  const bf16_t* vbase = p.v + (int64_t)b * p.Nk * p.ldv + hh * HD;
+
+  // Q^T fragments (B operand): lane holds Q[qc][ks*16 + 8h .. +7]
+  s16x8 qf[KS];
+  {
+    const bf16_t* qr = p.q + ((int64_t)b * p.Nq + qc) * p.ldq + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *(const s16x8*)(qr + ks * 16 + 8 * h);
+  }
+  // dO^T fragments (dQ mode), same layout; lse / delta per lane (one query)
+  s16x8 of[KS];
+  float lse2 = 0.f, dlt = 0.f;
+  if constexpr (MODE == 1) {
+    const bf16_t* dr = p.dout + ((int64_t)b * p.Nq + qc) * p.lddo + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) of[ks] = *(const s16x8*)(dr + ks * 16 + 8 * h);
+    const int64_t si = ((int64_t)b * p.H + hh) * p.Nq + qc;
+    lse2 = p.lse[si];
+    dlt = p.delta[si];
+  }
+
+  f32x16 acc[DS];  // O^T (fwd) or dQ^T (dq): rows = d, lanes = queries
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+
+  TileStage<HD, KT> ks_, vs_;
+  const int ntiles = (p.Nk + KT - 1) / KT;
+  ks_.load(kbase, p.ldk, 0, p.Nk, tid);
+  vs_.load(vbase, p.ldv, 0, p.Nk, tid);
+  ks_.store(ktile, tid);
+  vs_.store(vtile, tid);
+  key_bias_tile(kb, p, b, 0, KT, tid);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int key0 = t * KT;
+    if (t + 1 < ntiles) {
+      ks_.load(kbase, p.ldk, key0 + KT, p.Nk, tid);
+      vs_.load(vbase, p.ldv, key0 + KT, p.Nk, tid);
+    }
+    // S^T[key][q] for the two 32-key halves of the tile
+    f32x16 s[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(ktile, u * 32, ks, lane), qf[ks], s[u]);
+    }
+    if constexpr (MODE == 0) {
+      float mt = -1e30f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float x = s[u][r] * c2 + kb[u * 32 + acc_row(r, h)];
+          s[u][r] = x;
+          mt = fmaxf(mt, x);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float m_new = fmaxf(m_run, mt);
+      const float alpha = exp2f(m_run - m_new);
+      m_run = m_new;
+      float ls = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = exp2f(s[u][r] - m_new);
+          s[u][r] = e;
+          ls += e;
+        }
+      l_run = l_run * alpha + ls;
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[d][r] *= alpha;
+      // O^T[d][q] += V^T[d][key] . P^T[key][q]
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const s16x8 pb = acc_frag(s[u], ss);
+#pragma unroll
+          for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vtile, u * 32, ss, d * 32, lane), pb, acc[d]);
+        }
+    } else {
+      // P^T = 2^(s*c2 + kb - lse2); dP^T = V . dO^T; dS^T = P^T (dP^T - delta)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        f32x16 dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) dp = mfma32(row_frag<HD>(vtile, u * 32, ks, lane), of[ks], dp);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pr = exp2f(s[u][r] * c2 + kb[u * 32 + acc_row(r, h)] - lse2);
+          s[u][r] = pr * (dp[r] - dlt);
+        }
+        // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const s16x8 db = acc_frag(s[u], ss);
+#pragma unroll
+          for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(ktile, u * 32, ss, d * 32, lane), db, acc[d]);
+        }
+      }
+    }
+    if (t + 1 < ntiles) {
+      __syncthreads();
+      ks_.store(ktile, tid);
+      vs_.store(vtile, tid);
+      key_bias_tile(kb, p, b, key0 + KT, KT, tid);
+      __syncthreads();
+    }
+  }
+
+  if (qi >= p.Nq) return;
+  if constexpr (MODE == 0) {
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = 1.0f / l_tot;
+    bf16_t* orow = p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD;
+#pragma unroll
+    for (int d = 0; d < DS; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 w;
+        w[0] = pack2(acc[d][4 * g] * inv, acc[d][4 * g + 1] * inv);
+        w[1] = pack2(acc[d][4 * g + 2] * inv, acc[d][4 * g + 3] * inv);
+        *(u32x2*)(orow + d * 32 + 8 * g + 4 * h) = w;
+      }
+    if (h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
+  } else {
+    if (p.dq_f32) {
+      float* qrow = (float*)p.dq + ((int64_t)b * p.Nq + qi) * p.lddq + hh * HD;
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          f32x4 w = {acc[d][4 * g] * p.scale, acc[d][4 * g + 1] * p.scale, acc[d][4 * g + 2] * p.scale,
+                     acc[d][4 * g + 3] * p.scale};
+          *(f32x4*)(qrow + d * 32 + 8 * g + 4 * h) = w;
+        }
+    } else {
+      bf16_t* qrow = (bf16_t*)p.dq + ((int64_t)b * p.Nq + qi) * p.lddq + hh * HD;
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u32x2 w;
+          w[0] = pack2(acc[d][4 * g] * p.scale, acc[d][4 * g + 1] * p.scale);
+          w[1] = pack2(acc[d][4 * g + 2] * p.scale, acc[d][4 * g + 3] * p.scale);
+          *(u32x2*)(qrow + d * 32 + 8 * g + 4 * h) = w;
+        }
+    }
+  }
+}
+
+// =============================================================================================
+// dK / dV: keys on lanes, queries in registers; workgroup = 4 waves x 32 keys
+// =============================================================================================
+template <int HD>
+__global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnParams p) {
+  constexpr int QT = 32;
+  constexpr int KS = HD / 16;
+  constexpr int DS = HD / 32;
+  constexpr int TILE = QT * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
+  __shared__ __attribute__((aligned(16))) float st_lse[QT];
+  __shared__ __attribute__((aligned(16))) float st_dl[QT];
+  char* qtile = smem;
+  char* otile = smem + TILE;  // dO
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hh = blockIdx.y, b = blockIdx.z;
+  const int key = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const int kc = min(key, p.Nk - 1);
+  const float c2 = p.scale * LOG2E;
+  float kbias = -INFINITY;
+  if (key < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.Nk + key] * LOG2E : 0.f;
+
+  // K^T / V^T fragments (B operands): lane holds K[kc][ks*16 + 8h .. +7]
+  s16x8 kf[KS], vf[KS];
+  {
+    const bf16_t* kr = p.k + ((int64_t)b * p.Nk + kc) * p.ldk + hh * HD;
+    const bf16_t* vr = p.v + ((int64_t)b * p.Nk + kc) * p.ldv + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = *(const s16x8*)(kr + ks * 16 + 8 * h);
+      vf[ks] = *(const s16x8*)(vr + ks * 16 + 8 * h);
+    }
+  }
+  f32x16 dka[DS], dva[DS];  // dK^T / dV^T: rows = d, lanes = keys
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dka[d][r] = 0.f;
+      dva[d][r] = 0.f;
+    }
+
+  const bf16_t* qbase = p.q + (int64_t)b * p.Nq * p.ldq + hh * HD;
+  const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
+  const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
+  const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
+  TileStage<HD, QT> qs_, os_;
+  const int ntiles = (p.Nq + QT - 1) / QT;
+  auto stage_stats = [&](int qb) {
+    if (tid < QT) {
+      const int qq = qb + tid;
+      st_lse[tid] = qq < p.Nq ? lbase[qq] : INFINITY;  // rows past Nq contribute P = 0
+      st_dl[tid] = qq < p.Nq ? dbase[qq] : 0.f;
+    }
+  };
+  qs_.load(qbase, p.ldq, 0, p.Nq, tid);
+  os_.load(obase, p.lddo, 0, p.Nq, tid);
+  qs_.store(qtile, tid);
+  os_.store(otile, tid);
+  stage_stats(0);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int qb = t * QT;
+    if (t + 1 < ntiles) {
+      qs_.load(qbase, p.ldq, qb + QT, p.Nq, tid);
+      os_.load(obase, p.lddo, qb + QT, p.Nq, tid);
+    }
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = 0.f;
+      dp[r] = 0.f;
+    }
+    // S[q][key] = Q.K^T ; dP[q][key] = dO.V^T
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      s = mfma32(row_frag<HD>(qtile, 0, ks, lane), kf[ks], s);
+      dp = mfma32(row_frag<HD>(otile, 0, ks, lane), vf[ks], dp);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qr = acc_row(r, h);
+      const float pr = exp2f(s[r] * c2 + kbias - st_lse[qr]);
+      s[r] = pr;                           // P
+      dp[r] = pr * (dp[r] - st_dl[qr]);    // dS
+    }
+    // dV^T[d][key] += dO^T[d][q] . P[q][key] ; dK^T[d][key] += Q^T[d][q] . dS[q][key]
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const s16x8 pb = acc_frag(s, ss);
+      const s16x8 sb = acc_frag(dp, ss);
+#pragma unroll
+      for (int d = 0; d < DS; ++d) {
+        dva[d] = mfma32(tr_frag<HD>(otile, 0, ss, d * 32, lane), pb, dva[d]);
+        dka[d] = mfma32(tr_frag<HD>(qtile, 0, ss, d * 32, lane), sb, dka[d]);
+      }
+    }
+    if (t + 1 < ntiles) {
+      __syncthreads();
+      qs_.store(qtile, tid);
+      os_.store(otile, tid);
+      stage_stats(qb + QT);
+      __syncthreads();
+    }
+  }
+  if (key >= p.Nk) return;
+  bf16_t* krow = p.dk + ((int64_t)b * p.Nk + key) * p.lddk + hh * HD;
+  bf16_t* vrow = p.dv + ((int64_t)b * p.Nk + key) * p.lddv + hh * HD;
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 wk, wv;
+      wk[0] = pack2(dka[d][4 * g] * p.scale, dka[d][4 * g + 1] * p.scale);
+      wk[1] = pack2(dka[d][4 * g + 2] * p.scale, dka[d][4 * g + 3] * p.scale);
+      wv[0] = pack2(dva[d][4 * g], dva[d][4 * g + 1]);
+      wv[1] = pack2(dva[d][4 * g + 2], dva[d][4 * g + 3]);
+      *(u32x2*)(krow + d * 32 + 8 * g + 4 * h) = wk;
+      *(u32x2*)(vrow + d * 32 + 8 * g + 4 * h) = wv;
+    }
+}
+
+// delta[b,h,q] = sum_d dO*O (f32), one wave per (b, q) row covering all heads
+template <int HD>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const AttnParams p, float* __restrict__ delta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = blockIdx.x * 4 + (threadIdx.x >> 6);  // b*Nq + q
+  if (row >= (int64_t)p.B * p.Nq) return;
+  const int b = (int)(row / p.Nq), q = (int)(row % p.Nq);
+  constexpr int LPH = HD / 8;  // lanes per head (8 elements each)
+  const int HPP = 64 / LPH;    // heads per pass
+  for (int h0 = 0; h0 < p.H; h0 += HPP) {
+    const int hh = h0 + lane / LPH;
+    float s = 0.f;
+    if (hh < p.H) {
+      const int d0 = (lane % LPH) * 8;
+      const u32x4 a = *(const u32x4*)(p.dout + row * p.lddo + hh * HD + d0);
+      const u32x4 o = *(const u32x4*)(p.o + row * p.ldo + hh * HD + d0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        s += bf2f((bf16_t)(a[j >> 1] >> ((j & 1) * 16))) * bf2f((bf16_t)(o[j >> 1] >> ((j & 1) * 16)));
+    }
+#pragma unroll
+    for (int off = LPH / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (hh < p.H && (lane % LPH) == 0) delta[((int64_t)b * p.H + hh) * p.Nq + q] = s;
+  }
+}
+
+template <int HD>
+static int launch_fwd(const AttnParams& p, hipStream_t s) {
+  dim3 grid((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
+  hipLaunchKernelGGL((attn_q_kernel<HD, 0>), grid, dim3(ATT_THREADS), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+template <int HD>
+static int launch_bwd(AttnParams p, float* delta, hipStream_t s) {
+  hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)(((int64_t)p.B * p.Nq + 3) / 4)), dim3(256), 0, s, p,
+                     delta);
+  LTX_LAUNCH_CHECK();
+  p.delta = delta;
+  dim3 gq((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
+  hipLaunchKernelGGL((attn_q_kernel<HD, 1>), gq, dim3(ATT_THREADS), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  dim3 gk((unsigned)((p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
+  hipLaunchKernelGGL(attn_dkdv_kernel<HD>, gk, dim3(ATT_THREADS), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+static int check_common(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                        int64_t B, int64_t H, int64_t Nq, int64_t Nk, int64_t d) {
+  if (!(q && k && v)) return fail(LTX_ERR_BAD_ARG, "attn: null q/k/v");
+  if (!(d == 32 || d == 64)) return fail(LTX_ERR_BAD_ARG, "attn: head dim must be 32 or 64");
+  if (B <= 0 || H <= 0 || Nq <= 0 || Nk <= 0) return fail(LTX_ERR_BAD_ARG, "attn: empty shape");
+  if (ldq < H * d || ldk < H * d || ldv < H * d) return fail(LTX_ERR_BAD_ARG, "attn: row stride < H*d");
+  if ((ldq | ldk | ldv) % 8 != 0) return fail(LTX_ERR_BAD_ARG, "attn: row strides must be multiples of 8");
+  if (((uintptr_t)q | (uintptr_t)k | (uintptr_t)v) % 16 != 0) return fail(LTX_ERR_BAD_ARG, "attn: 16-B alignment");
+  return LTX_OK;
+}
+
+}  // namespace ltx
+
+using namespace ltx;
+
+extern "C" int ltx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                            void* o, int64_t ldo, float* lse, const float* key_bias, int64_t B, int64_t H,
+                            int64_t Nq, int64_t Nk, int64_t d, float scale, void* stream) {
+  int rc = check_common(q, ldq, k, ldk, v, ldv, B, H, Nq, Nk, d);
+  if (rc) return rc;
+  LTX_CHECK_ARG(o && lse && ldo >= H * d && ldo % 8 == 0, "attn_fwd: bad output");
+  AttnParams p = {};
+  p.q = (const bf16_t*)q; p.ldq = ldq; p.k = (const bf16_t*)k; p.ldk = ldk; p.v = (const bf16_t*)v; p.ldv = ldv;
+  p.o_out = (bf16_t*)o; p.ldo = ldo; p.lse = lse; p.key_bias = key_bias;
+  p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.scale = scale;
+  return d == 64 ? launch_fwd<64>(p, (hipStream_t)stream) : launch_fwd<32>(p, (hipStream_t)stream);
+}
+
+extern "C" int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                            const void* o, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
+                            const float* key_bias, float* delta_ws, void* dq, int64_t lddq, int dq_is_f32,
+                            void* dk, int64_t lddk, void* dv, int64_t lddv, int64_t B, int64_t H, int64_t Nq,
+                            int64_t Nk, int64_t d, float scale, void* stream) {
+  int rc = check_common(q, ldq, k, ldk, v, ldv, B, H, Nq, Nk, d);
+  if (rc) return rc;
+  LTX_CHECK_ARG(o && dout && lse && delta_ws && dq && dk && dv, "attn_bwd: null operand");
+  LTX_CHECK_ARG((ldo | lddo | lddq | lddk | lddv) % 8 == 0, "attn_bwd: strides must be multiples of 8");
+  AttnParams p = {};
+  p.q = (const bf16_t*)q; p.ldq = ldq; p.k = (const bf16_t*)k; p.ldk = ldk; p.v = (const bf16_t*)v; p.ldv = ldv;
+  p.o = (const bf16_t*)o; p.ldo = ldo; p.dout = (const bf16_t*)dout; p.lddo = lddo;
+  p.lse = (float*)lse; p.key_bias = key_bias;
+  p.dq = dq; p.lddq = lddq; p.dq_f32 = dq_is_f32;
+  p.dk = (bf16_t*)dk; p.lddk = lddk; p.dv = (bf16_t*)dv; p.lddv = lddv;
+  p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.scale = scale;
+  return d == 64 ? launch_bwd<64>(p, delta_ws, (hipStream_t)stream) : launch_bwd<32>(p, delta_ws, (hipStream_t)stream);
+}

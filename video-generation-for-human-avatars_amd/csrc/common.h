@@ -1,0 +1,86 @@
+// Shared helpers for the LTX-Video MI355X (gfx950 / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+namespace ltx {
+
+typedef unsigned short bf16_t;  // raw bf16 bits in HBM
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+__device__ __forceinline__ float bf2f(bf16_t x) { return __uint_as_float(((unsigned)x) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (NaN kept a NaN: lowers to v_cvt_pk_bf16_f32 on gfx950)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+// value rounded through bf16 and back (mirrors an eager bf16 op boundary)
+__device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// tanh-approximate GELU exactly as ATen computes it in float (F.gelu(approximate="tanh"))
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float kBeta = 0.7978845608028654f;  // sqrt(2/pi)
+  const float kKappa = 0.044715f;
+  float x_cube = x * x * x;
+  float inner = kBeta * (x + kKappa * x_cube);
+  return 0.5f * x * (1.0f + tanhf(inner));
+}
+// d gelu_tanh / dx, same association as ATen's GeluBackward (approximate="tanh"); the caller
+// multiplies by dy
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float kBeta = 0.7978845608028654f;
+  const float kKappa = 0.044715f;
+  float x_sq = x * x;
+  float x_cube = x_sq * x;
+  float inner = kBeta * (x + kKappa * x_cube);
+  float tanh_inner = tanhf(inner);
+  float left = 0.5f * x;
+  float right = 1.0f + tanh_inner;
+  float left_derivative = 0.5f * right;
+  float tanh_derivative = 1.0f - tanh_inner * tanh_inner;
+  float inner_derivative = kBeta * (1.0f + 3.0f * kKappa * x_sq);
+  float right_derivative = left * tanh_derivative * inner_derivative;
+  return left_derivative + right_derivative;
+}
+
+}  // namespace ltx
+
+// ---- host-side error plumbing -----------------------------------------------------------------
+namespace ltx {
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+}  // namespace ltx
+
+#define LTX_CHECK_ARG(cond, msg)                                   \
+  do {                                                             \
+    if (!(cond)) return ::ltx::fail(LTX_ERR_BAD_ARG, (msg));      \
+  } while (0)
+
+#define LTX_LAUNCH_CHECK()                                                         \
+  do {                                                                             \
+    hipError_t e_ = hipGetLastError();                                             \
+    if (e_ != hipSuccess) return ::ltx::fail((int)e_, hipGetErrorString(e_));      \
+  } while (0)

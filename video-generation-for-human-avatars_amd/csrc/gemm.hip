@@ -1,0 +1,354 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues: C[M,N] = epi(A[M,K] . W[N,K]^T).
+//
+// Every dense contraction on the LTX-2B training step maps onto this one "NT" form:
+//   forward   X[M,K] . W[N,K]^T          (nn.Linear: weights stored [out,in], K contiguous)
+//   dgrad     dY[M,N] . (W^T)[K,N]^T     (frozen weights: the W^T copy is packed once at load)
+//   wgrad     dY^T[N,M] . X^T[K,M]^T     (caption_projection only; operands transposed first)
+//
+// Tiling: 128x128 output tile, BK = 64, 256 threads = 4 waves in 2x2, each wave 64x64 as 4x4
+// v_mfma_f32_16x16x32_bf16. The MFMA "A" operand is the W tile (rows n), the "B" operand the X
+// tile (rows m), so each lane's accumulator holds 4 CONSECUTIVE n of one row m: the epilogue
+// packs them into one 8-byte LDS store, and the row-contiguous pass then writes 16 B per lane.
+// Staging: global_load_lds_dwordx4 (1 KiB per wave-instruction) into a 2-deep LDS ring; the
+// image is lane-linear in LDS, so the XOR swizzle (16-B chunk ^= row & 7, conflict-free for the
+// 16x16x32 fragment reads) is applied to the per-lane SOURCE address and to the ds_read address.
+// Block order: XCD-aware (blocks b, b+8 share an XCD / L2) then grouped by 8 row-tiles.
+#include "common.h"
+#include "ltx_hip.h"
+
+namespace ltx {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int GEMM_THREADS = 256;
+constexpr int TILE_BYTES = BM * BK * 2;           // 16 KiB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;       // A + W
+constexpr int C_STRIDE = BN * 2 + 8;              // bf16 C image row stride (bytes), 8-B aligned
+constexpr int LDS_BYTES = (2 * STAGE_BYTES > BM * C_STRIDE) ? 2 * STAGE_BYTES : BM * C_STRIDE;
+
+struct GemmParams {
+  const bf16_t* A;  // [M, K] activations, row stride lda
+  const bf16_t* W;  // [N, K] weights (or W^T for dgrad), row stride ldw
+  bf16_t* C;        // [M, N], row stride ldc
+  int64_t lda, ldw, ldc;
+  int M, N, K;
+  const bf16_t* bias;  // [N] or null
+  // epilogue auxiliaries (meaning per epilogue, see ltx_hip.h)
+  const void* aux0;
+  int64_t ld0;
+  const void* aux1;
+  int64_t ld1;
+  const void* aux2;
+  int64_t ld2;
+  float alpha;
+  int rank;
+  int rows_per_batch;
+};
+
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, LDS_PTR(lds_wave_base), 16, 0, 0);
+}
+
+// byte offset of (row, logical 16-B chunk) inside a [128][64] bf16 swizzled tile image
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+__device__ __forceinline__ void block_to_tile(int bid, int ntm, int ntn, int& tm, int& tn) {
+  const int nwg = ntm * ntn;
+  // bijective XCD remap: blocks dealt round-robin over 8 XCDs -> give each XCD a contiguous range
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  // grouped raster: 8 row-tiles share each W column panel
+  const int GROUP = 8;
+  const int group = wg / (GROUP * ntn);
+  const int first = group * GROUP;
+  const int gsize = min(ntm - first, GROUP);
+  tm = first + (wg % (GROUP * ntn)) % gsize;
+  tn = (wg % (GROUP * ntn)) / gsize;
+}
+
+template <int EPI, int R>
+__device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0, const bf16_t* cvals,
+                                              float* out8) {
+  // cvals: 8 bf16 of bf16(acc [+ bias]) for columns n0..n0+7 of row m
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(cvals[j]);
+  if constexpr (EPI == LTX_EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out8[j] = v[j];
+  } else if constexpr (EPI == LTX_EPI_GELU) {
+    // aux0: optional pre-activation store (bf16, ld0) for the backward
+    if (p.aux0) {
+      u32x4 pk;
+      pk[0] = (unsigned)cvals[0] | ((unsigned)cvals[1] << 16);
+      pk[1] = (unsigned)cvals[2] | ((unsigned)cvals[3] << 16);
+      pk[2] = (unsigned)cvals[4] | ((unsigned)cvals[5] << 16);
+      pk[3] = (unsigned)cvals[6] | ((unsigned)cvals[7] << 16);
+      *(u32x4*)((bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0) = pk;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out8[j] = gelu_tanh(v[j]);
+  } else if constexpr (EPI == LTX_EPI_GATED_RESIDUAL) {
+    // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1)
+    const int b = m / p.rows_per_batch;
+    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    const u32x4 g4 = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)b * p.ld1 + n0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float r = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16)));
+      const float g = bf2f((bf16_t)(g4[j >> 1] >> ((j & 1) * 16)));
+      out8[j] = r + rbf(g * v[j]);
+    }
+  } else if constexpr (EPI == LTX_EPI_LORA || EPI == LTX_EPI_LORA_RESIDUAL) {
+    // peft: y = bf16(bf16(base) + alpha * U[m,:] . Lb[n,:]), U = aux1 f32 [M,rank] (ld1),
+    // Lb = aux2 f32 [N,rank] (ld2). LORA_RESIDUAL adds R = aux0 afterwards (bf16 add).
+    const float* u = (const float*)p.aux1 + (int64_t)m * p.ld1;
+    float ur[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) ur[r] = u[r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float* lb = (const float*)p.aux2 + (int64_t)(n0 + j) * p.ld2;
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) s = fmaf(ur[r], lb[r], s);
+      out8[j] = v[j] + s * p.alpha;
+    }
+    if constexpr (EPI == LTX_EPI_LORA_RESIDUAL) {
+      const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + rbf(out8[j]);
+    }
+  } else if constexpr (EPI == LTX_EPI_GELU_BWD) {
+    // dF = bf16(bf16(acc) * gelu'(F)), F = aux0 pre-activation bf16 (ld0)
+    const u32x4 f4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = bf2f((bf16_t)(f4[j >> 1] >> ((j & 1) * 16)));
+      out8[j] = v[j] * gelu_tanh_grad(f);
+    }
+  } else if constexpr (EPI == LTX_EPI_ACCUM) {
+    // out = R + bf16(acc): R = aux0 (ld0); C may alias R
+    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + v[j];
+  } else if constexpr (EPI == LTX_EPI_LORA_DGRAD_ACCUM) {
+    // out = [R +] bf16( bf16(acc) + bf16(alpha * Wd[m,:] . A[:,n]) ), Wd = aux1 f32 [M,rank]
+    // (ld1), A = aux2 f32 [rank, N] (ld2 = row stride of A), R = aux0 optional (ld0)
+    const float* w = (const float*)p.aux1 + (int64_t)m * p.ld1;
+    float wr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) wr[r] = w[r];
+    float lo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lo[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float* a = (const float*)p.aux2 + (int64_t)r * p.ld2 + n0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lo[j] = fmaf(wr[r], a[j], lo[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out8[j] = v[j] + rbf(lo[j] * p.alpha);
+    if (p.aux0) {
+      const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + rbf(out8[j]);
+    }
+  }
+}
+
+template <int EPI, int R>
+__global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  int tm, tn;
+  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- staging addresses: wave w loads 4 x 1 KiB (8 rows each) of the X tile and of the W tile
+  // lane -> (row in 8-row group = lane>>3, physical chunk = lane&7); source chunk un-swizzled
+  const int lrow = lane >> 3;
+  const int pchunk = lane & 7;
+  const bf16_t* asrc[4];
+  const bf16_t* wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 8 + lrow;             // 0..127 within the tile
+    const int lchunk = pchunk ^ (row & 7);
+    const int am = min(m0 + row, p.M - 1);                  // clamp: rows past M are never stored
+    const int wn = min(n0 + row, p.N - 1);
+    asrc[i] = p.A + (int64_t)am * p.lda + lchunk * 8;
+    wsrc[i] = p.W + (int64_t)wn * p.ldw + lchunk * 8;
+  }
+  auto stage = [&](int buf, int kt) {
+    char* base = smem + buf * STAGE_BYTES;
+    const int koff = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(asrc[i] + koff, base + (wave * 4 + i) * 1024);
+      glds16(wsrc[i] + koff, base + TILE_BYTES + (wave * 4 + i) * 1024);
+    }
+  };
+
+  // wave (wm, wn) owns rows m: wm*64..+63 and cols n: wn*64..+63 of the tile
+  const int wm = wave >> 1, wn = wave & 1;
+  f32x4 acc[4][4];  // [n-subtile i][m-subtile j]
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int frow = lane & 15;   // fragment row within a 16-row subtile
+  const int fchunk = lane >> 4;  // fragment k-chunk (8 elements) within a 32-deep k-step
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const char* xs = smem + cur * STAGE_BYTES;
+    const char* ws = xs + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      s16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wn * 64 + i * 16 + frow;
+        af[i] = *(const s16x8*)(ws + swz(row, kk * 4 + fchunk));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wm * 64 + j * 16 + frow;
+        bfr[j] = *(const s16x8*)(xs + swz(row, kk * 4 + fchunk));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue stage 1: bf16(acc + bias) -> LDS image [128 m][128 n] (row stride C_STRIDE)
+  // lane holds C^T[n = i*16 + (lane>>4)*4 + r][m = j*16 + (lane&15)], r = 0..3
+  char* cimg = smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int nl = wn * 64 + i * 16 + (lane >> 4) * 4;  // local n of register 0
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+      const int gn = n0 + nl;
+      if (gn + 3 < p.N) {
+        const u32x2 bb = *(const u32x2*)(p.bias + gn);
+        b4[0] = bf2f((bf16_t)bb[0]); b4[1] = bf2f((bf16_t)(bb[0] >> 16));
+        b4[2] = bf2f((bf16_t)bb[1]); b4[3] = bf2f((bf16_t)(bb[1] >> 16));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ml = wm * 64 + j * 16 + (lane & 15);
+      u32x2 pk;
+      pk[0] = pack2(acc[i][j][0] + b4[0], acc[i][j][1] + b4[1]);
+      pk[1] = pack2(acc[i][j][2] + b4[2], acc[i][j][3] + b4[3]);
+      *(u32x2*)(cimg + ml * C_STRIDE + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue stage 2: row-contiguous, 8 columns (16 B) per thread, 16 threads per row
+  const int cgrp = tid & 15;
+  for (int rr = tid >> 4; rr < BM; rr += GEMM_THREADS / 16) {
+    const int m = m0 + rr;
+    const int n = n0 + cgrp * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const u32x2 lo = *(const u32x2*)(cimg + rr * C_STRIDE + cgrp * 16);
+    const u32x2 hi = *(const u32x2*)(cimg + rr * C_STRIDE + cgrp * 16 + 8);
+    bf16_t cv[8] = {(bf16_t)lo[0], (bf16_t)(lo[0] >> 16), (bf16_t)lo[1], (bf16_t)(lo[1] >> 16),
+                    (bf16_t)hi[0], (bf16_t)(hi[0] >> 16), (bf16_t)hi[1], (bf16_t)(hi[1] >> 16)};
+    float o[8];
+    epilogue_row8<EPI, R>(p, m, n, cv, o);
+    u32x4 pk;
+    pk[0] = pack2(o[0], o[1]);
+    pk[1] = pack2(o[2], o[3]);
+    pk[2] = pack2(o[4], o[5]);
+    pk[3] = pack2(o[6], o[7]);
+    *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
+  }
+}
+
+template <int EPI, int R = 0>
+static int launch(const GemmParams& p, hipStream_t s) {
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(ntm * ntn), dim3(GEMM_THREADS), LDS_BYTES, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+template <int EPI>
+static int launch_lora(const GemmParams& p, hipStream_t s) {
+  switch (p.rank) {
+    case 8: return launch<EPI, 8>(p, s);
+    case 16: return launch<EPI, 16>(p, s);
+    case 32: return launch<EPI, 32>(p, s);
+    default: return fail(LTX_ERR_BAD_ARG, "gemm lora: rank must be 8, 16 or 32");
+  }
+}
+
+}  // namespace ltx
+
+using namespace ltx;
+
+extern "C" int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
+                                int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue,
+                                const void* bias, const void* aux0, int64_t ld0, const void* aux1,
+                                int64_t ld1, const void* aux2, int64_t ld2, float alpha,
+                                int64_t rank, int64_t rows_per_batch, void* stream) {
+  LTX_CHECK_ARG(A && W && C, "gemm: null operand");
+  LTX_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: empty shape");
+  LTX_CHECK_ARG(K % BK == 0, "gemm: K must be a multiple of 64");
+  LTX_CHECK_ARG(N % 8 == 0, "gemm: N must be a multiple of 8");
+  LTX_CHECK_ARG(lda % 8 == 0 && ldw % 8 == 0 && ldc % 8 == 0, "gemm: leading dims must be multiples of 8");
+  LTX_CHECK_ARG(lda >= K && ldw >= K && ldc >= N, "gemm: leading dim smaller than the row");
+  LTX_CHECK_ARG(((uintptr_t)A | (uintptr_t)W | (uintptr_t)C) % 16 == 0, "gemm: operands must be 16-B aligned");
+  LTX_CHECK_ARG(M < (1LL << 31) && N < (1LL << 31), "gemm: shape too large");
+  LTX_CHECK_ARG(ld0 % 8 == 0 && ((uintptr_t)aux0 % 16) == 0, "gemm: aux0 must be 16-B aligned rows");
+  LTX_CHECK_ARG(bias == nullptr || ((uintptr_t)bias % 8) == 0, "gemm: bias must be 8-B aligned");
+  GemmParams p;
+  p.A = (const bf16_t*)A; p.W = (const bf16_t*)W; p.C = (bf16_t*)C;
+  p.lda = lda; p.ldw = ldw; p.ldc = ldc;
+  p.M = (int)M; p.N = (int)N; p.K = (int)K;
+  p.bias = (const bf16_t*)bias;
+  p.aux0 = aux0; p.ld0 = ld0; p.aux1 = aux1; p.ld1 = ld1; p.aux2 = aux2; p.ld2 = ld2;
+  p.alpha = alpha; p.rank = (int)rank; p.rows_per_batch = (int)(rows_per_batch > 0 ? rows_per_batch : M);
+  hipStream_t s = (hipStream_t)stream;
+  switch (epilogue) {
+    case LTX_EPI_STORE: return launch<LTX_EPI_STORE>(p, s);
+    case LTX_EPI_GELU: return launch<LTX_EPI_GELU>(p, s);
+    case LTX_EPI_GATED_RESIDUAL:
+      LTX_CHECK_ARG(aux0 && aux1, "gemm gated residual: needs residual (aux0) and gate (aux1)");
+      return launch<LTX_EPI_GATED_RESIDUAL>(p, s);
+    case LTX_EPI_LORA:
+    case LTX_EPI_LORA_RESIDUAL:
+      LTX_CHECK_ARG(aux1 && aux2, "gemm lora: needs U (aux1) and B (aux2)");
+      LTX_CHECK_ARG(epilogue == LTX_EPI_LORA || aux0, "gemm lora residual: needs residual (aux0)");
+      return epilogue == LTX_EPI_LORA ? launch_lora<LTX_EPI_LORA>(p, s)
+                                      : launch_lora<LTX_EPI_LORA_RESIDUAL>(p, s);
+    case LTX_EPI_GELU_BWD:
+      LTX_CHECK_ARG(aux0, "gemm gelu bwd: needs the pre-activation (aux0)");
+      return launch<LTX_EPI_GELU_BWD>(p, s);
+    case LTX_EPI_ACCUM:
+      LTX_CHECK_ARG(aux0, "gemm accum: needs the accumulator input (aux0)");
+      return launch<LTX_EPI_ACCUM>(p, s);
+    case LTX_EPI_LORA_DGRAD_ACCUM:
+      LTX_CHECK_ARG(aux1 && aux2, "gemm lora dgrad: needs Wd (aux1) and A (aux2)");
+      return launch_lora<LTX_EPI_LORA_DGRAD_ACCUM>(p, s);
+    default:
+      return fail(LTX_ERR_BAD_ARG, "gemm: unknown epilogue");
+  }
+}

@@ -1,0 +1,502 @@
+// Row-normalisation kernels (HBM-bound): RMSNorm + AdaLN modulate, LayerNorm + modulate, and
+// the attention q/k RMSNorm fused with the 3-D RoPE rotation -- forward and backward.
+// One wave per row (D <= 2048): each lane keeps its 8-element slices in registers, 16-B loads
+// and stores, the row reduction is a 64-lane xor-shuffle. Rounding points mirror the
+// reference's eager bf16 op boundaries (see the per-kernel comments).
+#include "common.h"
+#include "ltx_hip.h"
+
+namespace ltx {
+
+constexpr int ROW_THREADS = 256;  // 4 waves -> 4 rows per block
+constexpr int MAXP = 4;           // passes of 512 elements -> D <= 2048
+
+__device__ __forceinline__ void load8(const bf16_t* p, float* v) {
+  const u32x4 w = *(const u32x4*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f((bf16_t)(w[j >> 1] >> ((j & 1) * 16)));
+}
+__device__ __forceinline__ void load8f(const float* p, float* v) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float* v) {
+  u32x4 w;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) w[j] = pack2(v[2 * j], v[2 * j + 1]);
+  *(u32x4*)p = w;
+}
+
+// =============================================================================================
+// RMSNorm (no affine) + modulate.  diffusers RMSNorm (attention.py:117-119, :161):
+//   var = mean(x_f32^2); n = bf16(x * rsqrt(var + eps))
+// then attention.py:229-239 / :289-290:  y = bf16(bf16(n * onep) + shift)
+// =============================================================================================
+__global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ shift, const bf16_t* __restrict__ onep,
+    int64_t ld_mod, bf16_t* __restrict__ y, float* __restrict__ rstd_out, int M, int D, int rows_per_batch,
+    float eps) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const bf16_t* xr = x + (int64_t)m * D;
+  float v[MAXP][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      load8(xr + e, v[p]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (lane == 0 && rstd_out) rstd_out[m] = r;
+  const int b = m / rows_per_batch;
+  const bf16_t* sh = shift + (int64_t)b * ld_mod;
+  const bf16_t* op = onep + (int64_t)b * ld_mod;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float s8[8], o8[8], out[8];
+      load8(sh + e, s8);
+      load8(op + e, o8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] = rbf(rbf(v[p][j] * r) * o8[j]) + s8[j];
+      store8(y + (int64_t)m * D + e, out);
+    }
+  }
+}
+
+// Backward of the above + the residual gradient. Eager autograd roundings:
+//   dn  = bf16(dy * onep)                      (MulBackward, bf16)
+//   g   = f32(dn)                              (ToCopyBackward)
+//   dx1 = bf16(g * r)                          (MulBackward grad for the bf16 x, cast)
+//   dr  = sum(g * x); dvar = -0.5 * dr * r^3   (RsqrtBackward)
+//   dx2 = bf16((dvar / D) * (2 * x))           (MeanBackward, PowBackward, ToCopyBackward)
+//   dx  = bf16(dres + bf16(dx1 + dx2))
+__global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ rstd,
+    const bf16_t* __restrict__ onep, int64_t ld_mod, const bf16_t* dres, bf16_t* dx, int M, int D,
+    int rows_per_batch) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const int b = m / rows_per_batch;
+  const bf16_t* op = onep + (int64_t)b * ld_mod;
+  float g[MAXP][8], xv[MAXP][8];
+  float dr = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float d8[8], o8[8];
+      load8(dy + (int64_t)m * D + e, d8);
+      load8(op + e, o8);
+      load8(x + (int64_t)m * D + e, xv[p]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        g[p][j] = rbf(d8[j] * o8[j]);
+        dr += g[p][j] * xv[p][j];
+      }
+    }
+  }
+  dr = wave_sum(dr);
+  const float r = rstd[m];
+  const float dvar = (-0.5f * dr) * (r * r * r);
+  const float dmean = dvar / (float)D;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float res[8], out[8];
+      if (dres) load8(dres + (int64_t)m * D + e, res);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dx1 = rbf(g[p][j] * r);
+        const float dx2 = rbf(dmean * (2.0f * xv[p][j]));
+        const float d = rbf(dx1 + dx2);
+        out[j] = dres ? res[j] + d : d;
+      }
+      store8(dx + (int64_t)m * D + e, out);
+    }
+  }
+}
+
+// =============================================================================================
+// LayerNorm (no affine, eps 1e-6) + modulate: transformer3d.py:554-560.
+//   xhat = bf16((x - mean) * rstd) (ATen layer_norm, f32 statistics); y = bf16(bf16(xhat*onep)+shift)
+// =============================================================================================
+__global__ __launch_bounds__(ROW_THREADS) void layernorm_mod_fwd_kernel(
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ shift, const bf16_t* __restrict__ onep,
+    int64_t ld_mod, bf16_t* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out, int M,
+    int D, int rows_per_batch, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  float v[MAXP][8];
+  float s = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      load8(x + (int64_t)m * D + e, v[p]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[p][j];
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[p][j] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float r = rsqrtf(wave_sum(q) / (float)D + eps);
+  if (lane == 0) {
+    mean_out[m] = mean;
+    rstd_out[m] = r;
+  }
+  const int b = m / rows_per_batch;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float s8[8], o8[8], out[8];
+      load8(shift + (int64_t)b * ld_mod + e, s8);
+      load8(onep + (int64_t)b * ld_mod + e, o8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] = rbf(rbf((v[p][j] - mean) * r) * o8[j]) + s8[j];
+      store8(y + (int64_t)m * D + e, out);
+    }
+  }
+}
+
+// dn = bf16(dy * onep); g = f32(dn); dx = bf16(r * (g - mean(g) - xhat * mean(g * xhat)))
+__global__ __launch_bounds__(ROW_THREADS) void layernorm_mod_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ mean_in,
+    const float* __restrict__ rstd, const bf16_t* __restrict__ onep, int64_t ld_mod, bf16_t* __restrict__ dx,
+    int M, int D, int rows_per_batch) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const int b = m / rows_per_batch;
+  const float mean = mean_in[m], r = rstd[m];
+  float g[MAXP][8], xh[MAXP][8];
+  float sg = 0.f, sgx = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float d8[8], o8[8], x8[8];
+      load8(dy + (int64_t)m * D + e, d8);
+      load8(onep + (int64_t)b * ld_mod + e, o8);
+      load8(x + (int64_t)m * D + e, x8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        g[p][j] = rbf(d8[j] * o8[j]);
+        xh[p][j] = (x8[j] - mean) * r;
+        sg += g[p][j];
+        sgx += g[p][j] * xh[p][j];
+      }
+    }
+  }
+  const float mg = wave_sum(sg) / (float)D;
+  const float mgx = wave_sum(sgx) / (float)D;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float out[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out[j] = r * (g[p][j] - mg - xh[p][j] * mgx);
+      store8(dx + (int64_t)m * D + e, out);
+    }
+  }
+}
+
+// =============================================================================================
+// q/k RMSNorm (affine, across all heads) + 3-D RoPE (attention.py:996-1012, 917-932;
+// cos/sin: transformer3d.py:221-277).
+// =============================================================================================
+struct RopeRow {
+  float fr[3];  // grid[a] / max_pos[a] * 2 - 1
+};
+
+__device__ __forceinline__ RopeRow rope_row(const void* grid, int is_float, int b, int n, int N, float mp0,
+                                            float mp1, float mp2) {
+  RopeRow rr;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const int64_t idx = ((int64_t)b * 3 + a) * N + n;
+    const float gv = is_float ? ((const float*)grid)[idx] : (float)((const int64_t*)grid)[idx];
+    const float mpa = a == 0 ? mp0 : (a == 1 ? mp1 : mp2);
+    rr.fr[a] = (gv / mpa) * 2.0f - 1.0f;
+  }
+  return rr;
+}
+
+// (cos, sin) of element pair starting at even element e, rounded to bf16 like the tables
+__device__ __forceinline__ void rope_cs(const RopeRow& rr, const float* __restrict__ omega, int e, int pad,
+                                        float& c, float& s) {
+  if (e < pad) {
+    c = 1.f;
+    s = 0.f;
+    return;
+  }
+  const int q = (e - pad) >> 1;
+  const int j = q / 3, a = q - 3 * j;
+  const float phi = omega[j] * rr.fr[a];
+  float sv, cv;
+  sincosf(phi, &sv, &cv);
+  c = rbf(cv);
+  s = rbf(sv);
+}
+
+// one wave = one (row, q|k) item
+__global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
+    const bf16_t* __restrict__ q_in, int64_t ldq_in, const bf16_t* __restrict__ k_in, int64_t ldk_in,
+    bf16_t* __restrict__ q_out, int64_t ldq_out, bf16_t* __restrict__ k_out, int64_t ldk_out,
+    const bf16_t* __restrict__ qw, const bf16_t* __restrict__ kw, float* __restrict__ rstd_q,
+    float* __restrict__ rstd_k, const void* grid, int grid_is_float, int N, int M, int D,
+    const float* __restrict__ omega, float mp0, float mp1, float mp2, int rope, int nsel, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  const int m = item / nsel;
+  const int which = item - m * nsel;  // 0 = q, 1 = k
+  if (m >= M) return;
+  const bf16_t* in = which ? k_in + (int64_t)m * ldk_in : q_in + (int64_t)m * ldq_in;
+  bf16_t* out = which ? k_out + (int64_t)m * ldk_out : q_out + (int64_t)m * ldq_out;
+  const bf16_t* w = which ? kw : qw;
+  float v[MAXP][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      load8(in + e, v[p]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
+    }
+  }
+  ss = wave_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (lane == 0) (which ? rstd_k : rstd_q)[m] = r;
+  RopeRow rr;
+  const int pad = D % 6;
+  if (rope) rr = rope_row(grid, grid_is_float, m / N, m % N, N, mp0, mp1, mp2);
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float w8[8], nv[8], o[8];
+      load8(w + e, w8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) nv[j] = rbf(rbf(v[p][j] * r) * w8[j]);
+      if (rope) {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          float c, s;
+          rope_cs(rr, omega, e + j, pad, c, s);
+          // out = bf16(bf16(x * cos) + bf16(rot(x) * sin)), rot = (-x1, x0)
+          o[j] = rbf(nv[j] * c) + rbf(-nv[j + 1] * s);
+          o[j + 1] = rbf(nv[j + 1] * c) + rbf(nv[j] * s);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = nv[j];
+      }
+      store8(out + e, o);
+    }
+  }
+}
+
+// Backward. g (bf16) -> RoPE^T: dn[2i] = bf16(bf16(g0*c) + bf16(g1*s)), dn[2i+1] =
+// bf16(bf16(g1*c) + (-bf16(g0*s))); weight: dxr = bf16(dn * w); then the RMSNorm backward with
+// the same roundings as rmsnorm_mod_bwd_kernel.
+__global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
+    const void* __restrict__ dq_in, int64_t ldq_in, int dq_f32, const void* __restrict__ dk_in, int64_t ldk_in,
+    int dk_f32, const bf16_t* __restrict__ q_raw, int64_t ldq_raw, const bf16_t* __restrict__ k_raw,
+    int64_t ldk_raw, const bf16_t* __restrict__ qw, const bf16_t* __restrict__ kw,
+    const float* __restrict__ rstd_q, const float* __restrict__ rstd_k, bf16_t* __restrict__ dq_out,
+    int64_t ldq_out, bf16_t* __restrict__ dk_out, int64_t ldk_out, const void* grid, int grid_is_float, int N,
+    int M, int D, const float* __restrict__ omega, float mp0, float mp1, float mp2, int rope, int nsel) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
+  const int m = item / nsel;
+  const int which = item - m * nsel;
+  if (m >= M) return;
+  const void* gin = which ? dk_in : dq_in;
+  const int64_t ldg = which ? ldk_in : ldq_in;
+  const int gf32 = which ? dk_f32 : dq_f32;
+  const bf16_t* xin = which ? k_raw + (int64_t)m * ldk_raw : q_raw + (int64_t)m * ldq_raw;
+  bf16_t* out = which ? dk_out + (int64_t)m * ldk_out : dq_out + (int64_t)m * ldq_out;
+  const bf16_t* w = which ? kw : qw;
+  const float r = (which ? rstd_k : rstd_q)[m];
+  RopeRow rr;
+  const int pad = D % 6;
+  if (rope) rr = rope_row(grid, grid_is_float, m / N, m % N, N, mp0, mp1, mp2);
+  float gx[MAXP][8], xv[MAXP][8];
+  float dr = 0.f;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float g8[8], w8[8], dn[8];
+      if (gf32) {
+        load8f((const float*)gin + (int64_t)m * ldg + e, g8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g8[j] = rbf(g8[j]);
+      } else {
+        load8((const bf16_t*)gin + (int64_t)m * ldg + e, g8);
+      }
+      if (rope) {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          float c, s;
+          rope_cs(rr, omega, e + j, pad, c, s);
+          const float da0 = rbf(g8[j] * c), da1 = rbf(g8[j + 1] * c);
+          const float dr0 = rbf(g8[j] * s), dr1 = rbf(g8[j + 1] * s);  // d(rot)
+          // rot[2i] = -x[2i+1], rot[2i+1] = x[2i]
+          dn[j] = rbf(da0 + dr1);
+          dn[j + 1] = rbf(da1 + (-dr0));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dn[j] = g8[j];
+      }
+      load8(w + e, w8);
+      load8(xin + e, xv[p]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        gx[p][j] = rbf(dn[j] * w8[j]);
+        dr += gx[p][j] * xv[p][j];
+      }
+    }
+  }
+  dr = wave_sum(dr);
+  const float dvar = (-0.5f * dr) * (r * r * r);
+  const float dmean = dvar / (float)D;
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 512 + lane * 8;
+    if (e < D) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rbf(gx[p][j] * r) + rbf(dmean * (2.0f * xv[p][j]));
+      store8(out + e, o);
+    }
+  }
+}
+
+static inline unsigned row_blocks(int64_t items) { return (unsigned)((items + 3) / 4); }
+
+}  // namespace ltx
+
+using namespace ltx;
+
+extern "C" {
+
+int ltx_rmsnorm_modulate_fwd(const void* x, const void* shift, const void* onep, int64_t ld_mod, void* y,
+                             float* rstd, int64_t M, int64_t D, int64_t rows_per_batch, float eps, void* stream) {
+  LTX_CHECK_ARG(x && shift && onep && y && M > 0 && D > 0, "rmsnorm_modulate_fwd: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048 && ld_mod % 8 == 0, "rmsnorm_modulate_fwd: D must be %8 and <= 2048");
+  hipLaunchKernelGGL(rmsnorm_mod_fwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, (const bf16_t*)shift, (const bf16_t*)onep, ld_mod, (bf16_t*)y, rstd, (int)M,
+                     (int)D, (int)(rows_per_batch > 0 ? rows_per_batch : M), eps);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_rmsnorm_modulate_bwd(const void* dy, const void* x, const float* rstd, const void* onep, int64_t ld_mod,
+                             const void* dres, void* dx, int64_t M, int64_t D, int64_t rows_per_batch,
+                             void* stream) {
+  LTX_CHECK_ARG(dy && x && rstd && onep && dx && M > 0 && D > 0, "rmsnorm_modulate_bwd: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048 && ld_mod % 8 == 0, "rmsnorm_modulate_bwd: D must be %8 and <= 2048");
+  hipLaunchKernelGGL(rmsnorm_mod_bwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, (const bf16_t*)x, rstd, (const bf16_t*)onep, ld_mod, (const bf16_t*)dres,
+                     (bf16_t*)dx, (int)M, (int)D, (int)(rows_per_batch > 0 ? rows_per_batch : M));
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_layernorm_modulate_fwd(const void* x, const void* shift, const void* onep, int64_t ld_mod, void* y,
+                               float* mean, float* rstd, int64_t M, int64_t D, int64_t rows_per_batch, float eps,
+                               void* stream) {
+  LTX_CHECK_ARG(x && shift && onep && y && mean && rstd && M > 0, "layernorm_modulate_fwd: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048 && ld_mod % 8 == 0, "layernorm_modulate_fwd: D must be %8 and <= 2048");
+  hipLaunchKernelGGL(layernorm_mod_fwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, (const bf16_t*)shift, (const bf16_t*)onep, ld_mod, (bf16_t*)y, mean, rstd,
+                     (int)M, (int)D, (int)(rows_per_batch > 0 ? rows_per_batch : M), eps);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_layernorm_modulate_bwd(const void* dy, const void* x, const float* mean, const float* rstd,
+                               const void* onep, int64_t ld_mod, void* dx, int64_t M, int64_t D,
+                               int64_t rows_per_batch, void* stream) {
+  LTX_CHECK_ARG(dy && x && mean && rstd && onep && dx && M > 0, "layernorm_modulate_bwd: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048 && ld_mod % 8 == 0, "layernorm_modulate_bwd: D must be %8 and <= 2048");
+  hipLaunchKernelGGL(layernorm_mod_bwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, (const bf16_t*)x, mean, rstd, (const bf16_t*)onep, ld_mod, (bf16_t*)dx,
+                     (int)M, (int)D, (int)(rows_per_batch > 0 ? rows_per_batch : M));
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_qk_norm_rope_fwd(const void* q_in, int64_t ldq_in, const void* k_in, int64_t ldk_in, void* q_out,
+                         int64_t ldq_out, void* k_out, int64_t ldk_out, const void* q_weight, const void* k_weight,
+                         float* rstd_q, float* rstd_k, const void* indices_grid, int grid_is_float, int64_t B,
+                         int64_t N, int64_t D, const float* omega, float max_pos_t, float max_pos_h,
+                         float max_pos_w, int rope, float eps, void* stream) {
+  LTX_CHECK_ARG(q_in && q_out && q_weight && rstd_q && B > 0 && N > 0, "qk_norm_rope_fwd: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "qk_norm_rope_fwd: D must be %8 and <= 2048");
+  LTX_CHECK_ARG(!rope || (indices_grid && omega), "qk_norm_rope_fwd: rope needs indices_grid and omega");
+  const bool has_k = k_in != nullptr;
+  LTX_CHECK_ARG(!has_k || (k_out && k_weight && rstd_k), "qk_norm_rope_fwd: k needs k_out, k_weight, rstd_k");
+  LTX_CHECK_ARG(ldq_in % 8 == 0 && ldq_out % 8 == 0 && (!has_k || (ldk_in % 8 == 0 && ldk_out % 8 == 0)),
+                "qk_norm_rope_fwd: leading dims must be %8");
+  const int nsel = has_k ? 2 : 1;
+  const int64_t M = B * N;
+  hipLaunchKernelGGL(qk_norm_rope_fwd_kernel, dim3(row_blocks(M * nsel)), dim3(ROW_THREADS), 0,
+                     (hipStream_t)stream, (const bf16_t*)q_in, ldq_in, (const bf16_t*)k_in, ldk_in, (bf16_t*)q_out,
+                     ldq_out, (bf16_t*)k_out, ldk_out, (const bf16_t*)q_weight, (const bf16_t*)k_weight, rstd_q,
+                     rstd_k, indices_grid, grid_is_float, (int)N, (int)M, (int)D, omega, max_pos_t, max_pos_h,
+                     max_pos_w, rope, nsel, eps);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const void* dk_in, int64_t ldk_in,
+                         int dk_is_f32, const void* q_raw, int64_t ldq_raw, const void* k_raw, int64_t ldk_raw,
+                         const void* q_weight, const void* k_weight, const float* rstd_q, const float* rstd_k,
+                         void* dq_out, int64_t ldq_out, void* dk_out, int64_t ldk_out, const void* indices_grid,
+                         int grid_is_float, int64_t B, int64_t N, int64_t D, const float* omega, float max_pos_t,
+                         float max_pos_h, float max_pos_w, int rope, void* stream) {
+  LTX_CHECK_ARG(dq_in && q_raw && q_weight && rstd_q && dq_out && B > 0 && N > 0, "qk_norm_rope_bwd: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "qk_norm_rope_bwd: D must be %8 and <= 2048");
+  LTX_CHECK_ARG(!rope || (indices_grid && omega), "qk_norm_rope_bwd: rope needs indices_grid and omega");
+  const bool has_k = dk_in != nullptr;
+  LTX_CHECK_ARG(!has_k || (k_raw && k_weight && rstd_k && dk_out), "qk_norm_rope_bwd: incomplete k operands");
+  const int nsel = has_k ? 2 : 1;
+  const int64_t M = B * N;
+  hipLaunchKernelGGL(qk_norm_rope_bwd_kernel, dim3(row_blocks(M * nsel)), dim3(ROW_THREADS), 0,
+                     (hipStream_t)stream, dq_in, ldq_in, dq_is_f32, dk_in, ldk_in, dk_is_f32, (const bf16_t*)q_raw,
+                     ldq_raw, (const bf16_t*)k_raw, ldk_raw, (const bf16_t*)q_weight, (const bf16_t*)k_weight,
+                     rstd_q, rstd_k, (bf16_t*)dq_out, ldq_out, (bf16_t*)dk_out, ldk_out, indices_grid,
+                     grid_is_float, (int)N, (int)M, (int)D, omega, max_pos_t, max_pos_h, max_pos_w, rope, nsel);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+}  // extern "C"

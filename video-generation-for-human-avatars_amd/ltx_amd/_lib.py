@@ -1,0 +1,124 @@
+"""ctypes binding of libltxhip.so (include/ltx_hip.h).
+
+The library is built in-tree by ``make -C video-generation-for-human-avatars_amd/csrc`` (or
+``__graft_entry__.build()``). There is NO fallback: if the library is missing or the device is
+not gfx950, every op raises -- the product path never silently drops to eager torch.
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LTX_HIP_LIB", os.path.join(_HERE, "libltxhip.so"))
+
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f32 = ctypes.c_float
+_p = ctypes.c_void_p
+
+# name -> argtypes (all return int status)
+_SIGNATURES = {
+    "ltx_abi_version": [],
+    "ltx_device_info": [ctypes.POINTER(_i32), ctypes.POINTER(_i32)],
+    "ltx_patchify_bf16": [_p, _p, _i64, _i64, _i64, _i64, _i64, _p],
+    "ltx_unpatchify_bf16": [_p, _p, _i64, _i64, _i64, _i64, _i64, _p],
+    "ltx_latent_coords": [_p, _i64, _i64, _i64, _i64, _p],
+    "ltx_rf_noise_velocity": [_p, _p, _p, _p, _p, _i64, _i64, _p],
+    "ltx_condition_lerp": [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p],
+    "ltx_rf_prepare_tokens": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p],
+    "ltx_rmsnorm_modulate_fwd": [_p, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _p],
+    "ltx_rmsnorm_modulate_bwd": [_p, _p, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _p],
+    "ltx_ada_modulation": [_p, _p, _i64, _i64, _p, _p, _i64, _i64, _i64, _i64, _p],
+    "ltx_gate_mul_bf16": [_p, _p, _i64, _p, _i64, _i64, _i64, _p],
+    "ltx_layernorm_modulate_fwd": [_p, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _f32, _p],
+    "ltx_layernorm_modulate_bwd": [_p, _p, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _p],
+    "ltx_qk_norm_rope_fwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _i32,
+                             _i64, _i64, _i64, _p, _f32, _f32, _f32, _i32, _f32, _p],
+    "ltx_qk_norm_rope_bwd": [_p, _i64, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _p, _p, _p, _p,
+                             _p, _i64, _p, _i64, _p, _i32, _i64, _i64, _i64, _p, _f32, _f32, _f32,
+                             _i32, _p],
+    "ltx_attn_fwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64,
+                     _f32, _p],
+    "ltx_attn_bwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i32,
+                     _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _p],
+    "ltx_gemm_bf16_nt": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i32, _p, _p, _i64, _p,
+                         _i64, _p, _i64, _f32, _i64, _i64, _p],
+    "ltx_lora_down": [_p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _f32, _p],
+    "ltx_lora_wgrad": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p],
+    "ltx_timestep_embedding": [_p, _f32, _p, _i64, _i64, _p],
+    "ltx_silu_bf16": [_p, _p, _i64, _p],
+    "ltx_transpose_bf16": [_p, _i64, _p, _i64, _i64, _i64, _p],
+    "ltx_colsum_bf16": [_p, _i64, _p, _i64, _i64, _p],
+    "ltx_mse_fwd_bwd": [_p, _p, _p, _p, _i64, _f32, _p],
+    "ltx_adamw_step": [_p, _p, _p, _p, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i64, _p],
+}
+
+EPI = {"store": 0, "gelu": 1, "gated_residual": 2, "lora": 3, "lora_residual": 4,
+       "gelu_bwd": 5, "accum": 6, "lora_dgrad_accum": 7}
+
+_lib = None
+_lock = threading.Lock()
+_checked_device = set()
+
+
+class LtxHipError(RuntimeError):
+    pass
+
+
+def load(path: str = None):
+    """Load (once) and return the ctypes library; raises if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        path = path or LIB_PATH
+        if not os.path.exists(path):
+            raise LtxHipError(
+                f"libltxhip.so not found at {path}: build it with `make -C "
+                f"video-generation-for-human-avatars_amd/csrc` (no CPU/eager fallback exists)")
+        lib = ctypes.CDLL(path)
+        for name, args in _SIGNATURES.items():
+            fn = getattr(lib, name)  # AttributeError = ABI mismatch, loud by design
+            fn.argtypes = args
+            fn.restype = _i32
+        lib.ltx_last_error.argtypes = []
+        lib.ltx_last_error.restype = ctypes.c_char_p
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return list(_SIGNATURES) + ["ltx_last_error"]
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load().ltx_last_error().decode(errors="replace")
+        raise LtxHipError(f"{what} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    check(rc, name)
+
+
+def ensure_device(device=None):
+    """Verify once per device that it is a gfx950 (MI355X) and the library is loadable."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if dev.type != "cuda":
+        raise LtxHipError(f"libltxhip kernels need a ROCm device tensor, got {dev}")
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key in _checked_device:
+        return
+    lib = load()
+    arch, cus = _i32(0), _i32(0)
+    with torch.cuda.device(key):
+        check(lib.ltx_device_info(ctypes.byref(arch), ctypes.byref(cus)), "ltx_device_info")
+    _checked_device.add(key)
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

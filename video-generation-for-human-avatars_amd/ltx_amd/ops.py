@@ -1,0 +1,374 @@
+"""Typed torch-tensor wrappers over the C ABI (one function per entry point of ltx_hip.h).
+
+Tensors are only plumbing here: device memory, shapes, strides and the current HIP stream.
+Every computation happens in libltxhip.so. 2-D operands may be strided row views (unit column
+stride, any row stride that is a multiple of 8 elements), so fused buffers such as the
+[M, 6144] QKV projection are consumed in place without copies.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import EPI, call
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _s():
+    return _lib.stream_ptr()
+
+
+def _rows(t, name):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a 2-D row-major view, got shape {tuple(t.shape)} "
+                         f"strides {t.stride()}")
+    return t.stride(0)
+
+
+def _need(t, dtype, name):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise _lib.LtxHipError(f"{name}: tensor is not on a ROCm device (no CPU fallback)")
+
+
+# ---------------------------------------------------------------------------------------------
+# patchifier / rectified flow / conditioning
+# ---------------------------------------------------------------------------------------------
+def patchify(latents):
+    _need(latents, BF16, "patchify")
+    B, C, F, H, W = latents.shape
+    latents = latents.contiguous()
+    out = torch.empty(B, F * H * W, C, dtype=BF16, device=latents.device)
+    call("ltx_patchify_bf16", _p(latents), _p(out), B, C, F, H, W, _s())
+    return out
+
+
+def unpatchify(tokens, F, H, W):
+    _need(tokens, BF16, "unpatchify")
+    B, N, C = tokens.shape
+    assert N == F * H * W
+    tokens = tokens.contiguous()
+    out = torch.empty(B, C, F, H, W, dtype=BF16, device=tokens.device)
+    call("ltx_unpatchify_bf16", _p(tokens), _p(out), B, C, F, H, W, _s())
+    return out
+
+
+def latent_coords(B, F, H, W, device):
+    out = torch.empty(B, 3, F * H * W, dtype=torch.int64, device=device)
+    call("ltx_latent_coords", _p(out), B, F, H, W, _s())
+    return out
+
+
+def rf_prepare_tokens(latents, ref, pose, noise, t, want_x_t=False):
+    """Fused patchify + add_noise + velocity target + conditioning lerp (train step prologue)."""
+    for x, n in ((latents, "latents"), (ref, "ref"), (pose, "pose"), (noise, "noise")):
+        _need(x, BF16, n)
+    _need(t, F32, "t")
+    B, C, F, H, W = latents.shape
+    N = F * H * W
+    dev = latents.device
+    x_t = torch.empty(B, N, C, dtype=BF16, device=dev) if want_x_t else None
+    model_in = torch.empty(B, N, C, dtype=BF16, device=dev)
+    v = torch.empty(B, N, C, dtype=BF16, device=dev)
+    call("ltx_rf_prepare_tokens", _p(latents.contiguous()), _p(ref.contiguous()),
+         _p(pose.contiguous()), _p(noise.contiguous()), _p(t.contiguous()), _p(x_t),
+         _p(model_in), _p(v), B, C, F, H, W, _s())
+    return x_t, model_in, v
+
+
+def rf_noise_velocity(tokens, noise, t):
+    _need(tokens, BF16, "tokens")
+    _need(noise, BF16, "noise")
+    _need(t, F32, "t")
+    B = tokens.shape[0]
+    tokens = tokens.contiguous()
+    x_t = torch.empty(tokens.shape, dtype=BF16, device=tokens.device)
+    v = torch.empty(tokens.shape, dtype=BF16, device=tokens.device)
+    call("ltx_rf_noise_velocity", _p(tokens), _p(noise.contiguous()),
+         _p(t.contiguous()), _p(x_t), _p(v), B, tokens[0].numel(), _s())
+    return x_t, v
+
+
+def condition_lerp(tokens, ref, pose, out=None):
+    """transformer3d.py:447-466 on token-major input (returns a new tensor unless out given)."""
+    _need(tokens, BF16, "tokens")
+    B, C, F, H, W = pose.shape
+    tokens = tokens.contiguous()
+    out = torch.empty(tokens.shape, dtype=BF16, device=tokens.device) if out is None else out
+    call("ltx_condition_lerp", _p(tokens), _p(ref.contiguous()),
+         _p(pose.contiguous()), _p(out), B, C, F, H, W, _s())
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# normalisation
+# ---------------------------------------------------------------------------------------------
+def ada_modulation(sst, tmod, scale_mask, broadcast=False):
+    """sst [P,D] bf16 + tmod rows -> (mod [B,P,D], onep [B,P,D]). tmod is [B, P*D] (block AdaLN)
+    or, with broadcast=True, [B, D] added to every one of the P rows (output head)."""
+    P, D = sst.shape
+    B = tmod.shape[0]
+    ld = _rows(tmod, "tmod")
+    out = torch.empty(B, P, D, dtype=BF16, device=sst.device)
+    onep = torch.empty(B, P, D, dtype=BF16, device=sst.device)
+    call("ltx_ada_modulation", _p(sst.contiguous()), _p(tmod), ld, 0 if broadcast else D, _p(out),
+         _p(onep), B, P, D, scale_mask, _s())
+    return out, onep
+
+
+def gate_mul(dy, gate, rows_per_batch):
+    """bf16(dy * gate[m // rows_per_batch]); gate is a [B, D] row view."""
+    M, D = dy.shape
+    dy = dy.contiguous()
+    out = torch.empty(M, D, dtype=BF16, device=dy.device)
+    call("ltx_gate_mul_bf16", _p(dy), _p(gate), _rows(gate, "gate"), _p(out), M, D, rows_per_batch,
+         _s())
+    return out
+
+
+def _dense(t, name):
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: expected a dense [M, D] tensor")
+    return t
+
+
+def rmsnorm_modulate_fwd(x, shift, onep, ld_mod, rows_per_batch, eps, out=None):
+    M, D = _dense(x, "x").shape
+    y = torch.empty(M, D, dtype=BF16, device=x.device) if out is None else out
+    rstd = torch.empty(M, dtype=F32, device=x.device)
+    call("ltx_rmsnorm_modulate_fwd", _p(x), _p(shift), _p(onep), ld_mod, _p(y), _p(rstd), M, D,
+         rows_per_batch, eps, _s())
+    return y, rstd
+
+
+def rmsnorm_modulate_bwd(dy, x, rstd, onep, ld_mod, rows_per_batch, dres=None, out=None):
+    M, D = _dense(x, "x").shape
+    _dense(dy, "dy")
+    dx = torch.empty(M, D, dtype=BF16, device=x.device) if out is None else out
+    call("ltx_rmsnorm_modulate_bwd", _p(dy), _p(x), _p(rstd), _p(onep), ld_mod, _p(dres), _p(dx),
+         M, D, rows_per_batch, _s())
+    return dx
+
+
+def layernorm_modulate_fwd(x, shift, onep, ld_mod, rows_per_batch, eps):
+    M, D = _dense(x, "x").shape
+    y = torch.empty(M, D, dtype=BF16, device=x.device)
+    mean = torch.empty(M, dtype=F32, device=x.device)
+    rstd = torch.empty(M, dtype=F32, device=x.device)
+    call("ltx_layernorm_modulate_fwd", _p(x), _p(shift), _p(onep), ld_mod, _p(y), _p(mean),
+         _p(rstd), M, D, rows_per_batch, eps, _s())
+    return y, mean, rstd
+
+
+def layernorm_modulate_bwd(dy, x, mean, rstd, onep, ld_mod, rows_per_batch):
+    M, D = _dense(x, "x").shape
+    _dense(dy, "dy")
+    dx = torch.empty(M, D, dtype=BF16, device=x.device)
+    call("ltx_layernorm_modulate_bwd", _p(dy), _p(x), _p(mean), _p(rstd), _p(onep), ld_mod,
+         _p(dx), M, D, rows_per_batch, _s())
+    return dx
+
+
+class RopeSpec:
+    """Per-forward RoPE description: indices_grid + the reference's frequency table.
+
+    ``omega`` is computed exactly as precompute_freqs_cis does (transformer3d.py:231-250):
+    ``theta ** linspace(log(1,theta), log(theta,theta), dim//6) * pi / 2`` in f32 -- a 341-entry
+    constant, computed once on the host and copied to the device."""
+
+    def __init__(self, indices_grid, dim, theta, max_pos):
+        import math
+        self.grid = indices_grid.contiguous()
+        self.is_float = 0 if indices_grid.dtype == torch.int64 else 1
+        if self.is_float and self.grid.dtype != F32:
+            self.grid = self.grid.to(F32)
+        idx = theta ** torch.linspace(math.log(1, theta), math.log(theta, theta), dim // 6,
+                                      dtype=torch.float32)
+        idx = idx.to(torch.float32) * math.pi / 2
+        self.omega = idx.to(indices_grid.device)
+        self.max_pos = [float(m) for m in max_pos]
+        self.B, _, self.N = indices_grid.shape
+
+
+def qk_norm_rope_fwd(q_in, k_in, q_w, k_w, rope: RopeSpec = None, B=None, N=None, eps=1e-5,
+                     q_out=None, k_out=None):
+    """q_in/k_in [M,D] row views -> (q_out, k_out, rstd_q, rstd_k). k_in may be None."""
+    M, D = q_in.shape
+    dev = q_in.device
+    q_out = torch.empty(M, D, dtype=BF16, device=dev) if q_out is None else q_out
+    rq = torch.empty(M, dtype=F32, device=dev)
+    rk = None
+    if k_in is not None:
+        k_out = torch.empty(M, D, dtype=BF16, device=dev) if k_out is None else k_out
+        rk = torch.empty(M, dtype=F32, device=dev)
+    if rope is not None:
+        B, N = rope.B, rope.N
+    assert B * N == M
+    mp = rope.max_pos if rope is not None else [1.0, 1.0, 1.0]
+    call("ltx_qk_norm_rope_fwd", _p(q_in), _rows(q_in, "q_in"), _p(k_in),
+         _rows(k_in, "k_in") if k_in is not None else 0, _p(q_out), _rows(q_out, "q_out"),
+         _p(k_out), _rows(k_out, "k_out") if k_in is not None else 0, _p(q_w), _p(k_w), _p(rq),
+         _p(rk), _p(rope.grid) if rope else None, rope.is_float if rope else 0, B, N, D,
+         _p(rope.omega) if rope else None, mp[0], mp[1], mp[2], 1 if rope else 0, eps, _s())
+    return q_out, (k_out if k_in is not None else None), rq, rk
+
+
+def qk_norm_rope_bwd(dq, q_raw, q_w, rq, dk=None, k_raw=None, k_w=None, rk=None,
+                     rope: RopeSpec = None, B=None, N=None, dq_out=None, dk_out=None):
+    M, D = q_raw.shape
+    dev = q_raw.device
+    dq_out = torch.empty(M, D, dtype=BF16, device=dev) if dq_out is None else dq_out
+    if dk is not None and dk_out is None:
+        dk_out = torch.empty(M, D, dtype=BF16, device=dev)
+    if rope is not None:
+        B, N = rope.B, rope.N
+    mp = rope.max_pos if rope is not None else [1.0, 1.0, 1.0]
+    call("ltx_qk_norm_rope_bwd", _p(dq), _rows(dq, "dq"), 1 if dq.dtype == F32 else 0, _p(dk),
+         _rows(dk, "dk") if dk is not None else 0,
+         1 if (dk is not None and dk.dtype == F32) else 0, _p(q_raw), _rows(q_raw, "q_raw"),
+         _p(k_raw), _rows(k_raw, "k_raw") if k_raw is not None else 0, _p(q_w), _p(k_w), _p(rq),
+         _p(rk), _p(dq_out), _rows(dq_out, "dq_out"), _p(dk_out),
+         _rows(dk_out, "dk_out") if dk is not None else 0, _p(rope.grid) if rope else None,
+         rope.is_float if rope else 0, B, N, D, _p(rope.omega) if rope else None, mp[0], mp[1],
+         mp[2], 1 if rope else 0, _s())
+    return dq_out, (dk_out if dk is not None else None)
+
+
+# ---------------------------------------------------------------------------------------------
+# attention
+# ---------------------------------------------------------------------------------------------
+def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None):
+    """q [B*Nq, >=H*d] row view, k/v [B*Nk, ...] -> (o [B*Nq, H*d], lse [B,H,Nq] f32 log2)."""
+    Nq = q.shape[0] // B
+    Nk = k.shape[0] // B
+    o = torch.empty(B * Nq, H * d, dtype=BF16, device=q.device) if out is None else out
+    lse = torch.empty(B, H, Nq, dtype=F32, device=q.device)
+    call("ltx_attn_fwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
+         _rows(o, "o"), _p(lse), _p(key_bias), B, H, Nq, Nk, d, scale, _s())
+    return o, lse
+
+
+def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, dq=None,
+             dk=None, dv=None):
+    Nq = q.shape[0] // B
+    Nk = k.shape[0] // B
+    dev = q.device
+    dq = torch.empty(B * Nq, H * d, dtype=F32 if dq_f32 else BF16, device=dev) if dq is None else dq
+    dk = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dk is None else dk
+    dv = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dv is None else dv
+    delta = torch.empty(B, H, Nq, dtype=F32, device=dev)
+    call("ltx_attn_bwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
+         _rows(o, "o"), _p(do), _rows(do, "do"), _p(lse), _p(key_bias), _p(delta), _p(dq),
+         _rows(dq, "dq"), 1 if dq.dtype == F32 else 0, _p(dk), _rows(dk, "dk"), _p(dv),
+         _rows(dv, "dv"), B, H, Nq, Nk, d, scale, _s())
+    return dq, dk, dv
+
+
+# ---------------------------------------------------------------------------------------------
+# GEMM + LoRA
+# ---------------------------------------------------------------------------------------------
+def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2=None,
+         alpha=1.0, rank=0, rows_per_batch=0):
+    """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias)); see LTX_EPI_* in ltx_hip.h."""
+    _need(a, BF16, "gemm a")
+    _need(w, BF16, "gemm w")
+    M, K = a.shape
+    N, K2 = w.shape
+    if K != K2:
+        raise ValueError(f"gemm: K mismatch {K} vs {K2}")
+    out = torch.empty(M, N, dtype=BF16, device=a.device) if out is None else out
+    ld0 = _rows(aux0, "aux0") if aux0 is not None else 0
+    ld1 = _rows(aux1, "aux1") if aux1 is not None else 0
+    ld2 = _rows(aux2, "aux2") if aux2 is not None else 0
+    call("ltx_gemm_bf16_nt", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(out), _rows(out, "out"),
+         M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1), ld1, _p(aux2), ld2,
+         float(alpha), rank, rows_per_batch, _s())
+    return out
+
+
+def lora_down(x, wr, alpha=1.0, transposed=False, out=None):
+    """out[m,j] = alpha * x[m,:] . Wr[j,:]; Wr = lora_A [r,K]; transposed=True takes lora_B [K,r]
+    (i.e. uses B^T) for the dgrad w = s * dY . B."""
+    M, K = x.shape
+    if transposed:
+        r = wr.shape[1]
+        wj, wk = 1, wr.stride(0)
+    else:
+        r = wr.shape[0]
+        wj, wk = wr.stride(0), 1
+    out = torch.empty(M, r, dtype=F32, device=x.device) if out is None else out
+    call("ltx_lora_down", _p(x), _rows(x, "x"), _p(wr), wj, wk, _p(out), _rows(out, "out"), M, K, r,
+         float(alpha), _s())
+    return out
+
+
+def lora_wgrad(y, u, alpha=1.0, transpose_out=False):
+    """dW[n,j] = alpha * sum_m y[m,n] u[m,j] -> [N,r] (or [r,N] when transpose_out)."""
+    M, N = y.shape
+    r = u.shape[1]
+    if transpose_out:
+        dw = torch.empty(r, N, dtype=F32, device=y.device)
+        on, oj = 1, N
+    else:
+        dw = torch.empty(N, r, dtype=F32, device=y.device)
+        on, oj = r, 1
+    call("ltx_lora_wgrad", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(dw), on, oj, M, N, r,
+         float(alpha), _s())
+    return dw
+
+
+# ---------------------------------------------------------------------------------------------
+# small ops
+# ---------------------------------------------------------------------------------------------
+def timestep_embedding(t, scale, dim=256):
+    _need(t, F32, "t")
+    B = t.shape[0]
+    out = torch.empty(B, dim, dtype=BF16, device=t.device)
+    call("ltx_timestep_embedding", _p(t.contiguous()), float(scale), _p(out), B, dim, _s())
+    return out
+
+
+def silu(x):
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=BF16, device=x.device)
+    call("ltx_silu_bf16", _p(x), _p(y), x.numel(), _s())
+    return y
+
+
+def transpose(x, out=None):
+    R, C = x.shape
+    out = torch.empty(C, R, dtype=BF16, device=x.device) if out is None else out
+    call("ltx_transpose_bf16", _p(x), _rows(x, "x"), _p(out), _rows(out, "out"), R, C, _s())
+    return out
+
+
+def colsum(x):
+    M, N = x.shape
+    out = torch.empty(N, dtype=BF16, device=x.device)
+    call("ltx_colsum_bf16", _p(x), _rows(x, "x"), _p(out), M, N, _s())
+    return out
+
+
+def mse_fwd_bwd(out, v, grad_scale=1.0, want_grad=True):
+    """Returns (stats[4] f32 device: sum sq-err, sum v, sum v^2, -, dout bf16 or None)."""
+    n = out.numel()
+    out, v = out.contiguous(), v.contiguous()
+    stats = torch.empty(4, dtype=F32, device=out.device)
+    dout = torch.empty(out.shape, dtype=BF16, device=out.device) if want_grad else None
+    call("ltx_mse_fwd_bwd", _p(out), _p(v), _p(dout), _p(stats), n,
+         float(grad_scale), _s())
+    return stats, dout
+
+
+def adamw_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
+    is_bf16 = 1 if param.dtype == BF16 else 0
+    call("ltx_adamw_step", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(),
+         is_bf16, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
+         int(step), _s())

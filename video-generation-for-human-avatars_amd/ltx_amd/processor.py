@@ -1,0 +1,55 @@
+"""HipAttnProcessor: the operator-level plugin for Attention.set_processor (attention.py:532-552,
+935-1114). Computes one Attention call (q/k/v projections with optional LoRA, q/k RMSNorm, RoPE
+for self-attention, SDPA, to_out) with the same kernels the fused block uses.
+
+Round-1 scope: forward only (inference / pipeline use, e.g. LTXVideoPipeline's
+`transformer(...)` calls). Training runs the fused per-block autograd Function instead; calling
+this processor on tensors that require grad raises.
+"""
+import torch
+
+from . import ops
+
+
+class HipAttnProcessor:
+    def __call__(self, attn, hidden_states, freqs_cis=None, encoder_hidden_states=None,
+                 attention_mask=None, temb=None, skip_layer_mask=None, skip_layer_strategy=None,
+                 *args, **kwargs):
+        from .transformer3d import _lin
+        if torch.is_grad_enabled() and hidden_states.requires_grad:
+            raise NotImplementedError("HipAttnProcessor is forward-only; training uses the fused block")
+        if skip_layer_mask is not None:
+            raise NotImplementedError("skip-layer (STG) blending is an inference row not yet built")
+        B, N, Dq = hidden_states.shape
+        src = hidden_states if encoder_hidden_states is None else encoder_hidden_states
+        L = src.shape[1]
+        H, d = attn.heads, attn.dim_head
+        D = H * d
+        x = hidden_states.reshape(B * N, Dq).contiguous()
+        e = src.reshape(B * L, src.shape[2]).contiguous()
+
+        def proj(lin, inp):
+            w, b, lora = _lin(lin)
+            if lora is None:
+                return ops.gemm(inp, w, bias=b)
+            u = ops.lora_down(inp, lora.lora_A["default"].weight)
+            return ops.gemm(inp, w, bias=b, epilogue="lora", aux1=u,
+                            aux2=lora.lora_B["default"].weight, alpha=lora.scaling, rank=lora.r)
+
+        q_raw = proj(attn.to_q, x)
+        k_raw = proj(attn.to_k, e)
+        v = proj(attn.to_v, e)
+        if encoder_hidden_states is None and attn.use_rope:
+            if not isinstance(freqs_cis, ops.RopeSpec):
+                raise TypeError("freqs_cis must be an ltx_amd.ops.RopeSpec (cos/sin are formed in-kernel)")
+            q, k, _, _ = ops.qk_norm_rope_fwd(q_raw, k_raw, attn.q_norm.weight, attn.k_norm.weight,
+                                              freqs_cis)
+        else:
+            q, _, _, _ = ops.qk_norm_rope_fwd(q_raw, None, attn.q_norm.weight, None, None, B=B, N=N)
+            k, _, _, _ = ops.qk_norm_rope_fwd(k_raw, None, attn.k_norm.weight, None, None, B=B, N=L)
+        bias = None
+        if attention_mask is not None:
+            bias = attention_mask.reshape(B, -1).float().contiguous()
+        o, _ = ops.attn_fwd(q, k, v, B, H, d, attn.scale, key_bias=bias)
+        out = proj(attn.to_out[0], o)
+        return out.view(B, N, -1)

@@ -1,0 +1,777 @@
+"""Transformer3DModel for MI355X: the reference's module tree and call surface
+(ltx_video/models/transformers/transformer3d.py:49-565, attention.py:38-1264) executed by fused
+HIP kernels through libltxhip.so.
+
+Module / parameter names are the reference's (and therefore PEFT-targetable and state-dict
+compatible): transformer_blocks.{i}.attn1.to_q ..., attn2.to_out.0, q_norm.weight, ff.net.0.proj,
+ff.net.2, scale_shift_table, adaln_single.emb.timestep_embedder.linear_1, caption_projection ...
+
+Execution: each BasicTransformerBlock runs as ONE torch.autograd.Function (_BlockFn) whose
+forward/backward are explicit sequences of C-ABI kernel launches (see DESIGN.md for the list and
+for which tensors are kept for the backward). Frozen weights are packed once into the layouts the
+kernels want (fused QKV [3D, D], and W^T copies for the dgrad GEMMs -- the weights never change
+in lora_audio training, so no wgrad and no repacking per step). The caption projection (trainable)
+and the output head are their own Functions; the AdaLN-single timestep path needs no gradient.
+"""
+import glob
+import json
+import math
+import os
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Any, Dict, List, Optional
+
+import torch
+from torch import nn
+
+from . import _lib, ops
+from .patchifier import SymmetricPatchifier
+
+# LTX-Video 2B transformer config (ltx_video/utils/diffusers_config_mapping.py:74-105)
+OURS_TRANSFORMER_CONFIG = {
+    "_class_name": "Transformer3DModel",
+    "activation_fn": "gelu-approximate",
+    "attention_bias": True,
+    "attention_head_dim": 64,
+    "attention_type": "default",
+    "caption_channels": 4096,
+    "cross_attention_dim": 2048,
+    "double_self_attention": False,
+    "dropout": 0.0,
+    "in_channels": 128,
+    "norm_elementwise_affine": False,
+    "norm_eps": 1e-06,
+    "norm_num_groups": 32,
+    "num_attention_heads": 32,
+    "num_embeds_ada_norm": 1000,
+    "num_layers": 28,
+    "num_vector_embeds": None,
+    "only_cross_attention": False,
+    "out_channels": 128,
+    "project_to_2d_pos": True,
+    "upcast_attention": False,
+    "use_linear_projection": False,
+    "qk_norm": "rms_norm",
+    "standardization_norm": "rms_norm",
+    "positional_embedding_type": "rope",
+    "positional_embedding_theta": 10000.0,
+    "positional_embedding_max_pos": [20, 2048, 2048],
+    "timestep_scale_multiplier": 1000,
+}
+
+# diffusers checkpoint key renames (diffusers_config_mapping.py:140-145)
+TRANSFORMER_KEYS_RENAME_DICT = {"proj_in": "patchify_proj", "time_embed": "adaln_single",
+                                "norm_q": "q_norm", "norm_k": "k_norm"}
+
+
+@dataclass
+class Transformer3DModelOutput:
+    sample: torch.Tensor
+
+    def __getitem__(self, i):
+        return (self.sample,)[i] if isinstance(i, int) else getattr(self, i)
+
+
+# ===============================================================================================
+# parameter holders (reference module tree)
+# ===============================================================================================
+class RMSNorm(nn.Module):
+    """diffusers RMSNorm parameters (the math runs in the fused kernels)."""
+
+    def __init__(self, dim, eps, elementwise_affine=True):
+        super().__init__()
+        self.eps = eps
+        self.weight = nn.Parameter(torch.ones(dim)) if elementwise_affine else None
+
+
+class LoraLinear(nn.Module):
+    """peft 0.17.1 lora.Linear naming: base_layer, lora_A/lora_B ModuleDicts keyed 'default';
+    f32 adapters on a bf16 base (autocast_adapter_dtype). The math is fused into the GEMMs."""
+
+    def __init__(self, base_layer: nn.Linear, r: int, lora_alpha: int):
+        super().__init__()
+        self.base_layer = base_layer
+        self.r = r
+        self.lora_alpha = lora_alpha
+        self.scaling = lora_alpha / r
+        dev = base_layer.weight.device
+        self.lora_A = nn.ModuleDict({"default": nn.Linear(base_layer.in_features, r, bias=False,
+                                                          device=dev, dtype=torch.float32)})
+        self.lora_B = nn.ModuleDict({"default": nn.Linear(r, base_layer.out_features, bias=False,
+                                                          device=dev, dtype=torch.float32)})
+        nn.init.kaiming_uniform_(self.lora_A["default"].weight, a=math.sqrt(5))
+        nn.init.zeros_(self.lora_B["default"].weight)
+
+    @property
+    def weight(self):
+        return self.base_layer.weight
+
+    @property
+    def bias(self):
+        return self.base_layer.bias
+
+    @property
+    def in_features(self):
+        return self.base_layer.in_features
+
+    @property
+    def out_features(self):
+        return self.base_layer.out_features
+
+    @torch.no_grad()
+    def merged_weight(self):
+        """W + s * B A (peft merge_and_unload), in the base dtype."""
+        a = self.lora_A["default"].weight
+        b = self.lora_B["default"].weight
+        return (self.base_layer.weight.float() + self.scaling * (b @ a)).to(self.base_layer.weight.dtype)
+
+
+def _lin(m):
+    """(weight, bias, lora) of an nn.Linear or LoraLinear."""
+    if isinstance(m, LoraLinear):
+        return m.base_layer.weight, m.base_layer.bias, m
+    return m.weight, m.bias, None
+
+
+class Attention(nn.Module):
+    """Attention module of attention.py:325-932 (rms_norm qk-norm across all heads, biases)."""
+
+    def __init__(self, query_dim, cross_attention_dim=None, heads=8, dim_head=64, bias=False,
+                 out_bias=True, qk_norm=None, use_rope=False, **_unused):
+        super().__init__()
+        self.inner_dim = dim_head * heads
+        self.heads = heads
+        self.dim_head = dim_head
+        self.scale = dim_head ** -0.5
+        self.is_cross_attention = cross_attention_dim is not None
+        self.cross_attention_dim = cross_attention_dim or query_dim
+        self.use_rope = use_rope
+        self.use_tpu_flash_attention = False
+        if qk_norm != "rms_norm":
+            raise NotImplementedError("LTX-Video uses qk_norm='rms_norm'")
+        self.q_norm = RMSNorm(self.inner_dim, eps=1e-5)
+        self.k_norm = RMSNorm(self.inner_dim, eps=1e-5)
+        self.to_q = nn.Linear(query_dim, self.inner_dim, bias=bias)
+        self.to_k = nn.Linear(self.cross_attention_dim, self.inner_dim, bias=bias)
+        self.to_v = nn.Linear(self.cross_attention_dim, self.inner_dim, bias=bias)
+        self.to_out = nn.ModuleList([nn.Linear(self.inner_dim, query_dim, bias=out_bias),
+                                     nn.Dropout(0.0)])
+        self.processor = None
+        from .processor import HipAttnProcessor
+        self.set_processor(HipAttnProcessor())
+
+    def set_processor(self, processor):
+        """Operator plugin point (attention.py:532-552)."""
+        self.processor = processor
+
+    def get_processor(self, return_deprecated_lora=False):
+        return self.processor
+
+    def set_use_tpu_flash_attention(self):
+        raise NotImplementedError("TPU flash attention is out of scope on MI355X")
+
+    def forward(self, hidden_states, freqs_cis=None, encoder_hidden_states=None,
+                attention_mask=None, skip_layer_mask=None, skip_layer_strategy=None,
+                **cross_attention_kwargs):
+        return self.processor(self, hidden_states, freqs_cis=freqs_cis,
+                              encoder_hidden_states=encoder_hidden_states,
+                              attention_mask=attention_mask, skip_layer_mask=skip_layer_mask,
+                              skip_layer_strategy=skip_layer_strategy)
+
+
+class GELU(nn.Module):
+    """diffusers GELU(dim_in, dim_out, approximate='tanh'): Linear `proj` then tanh-GELU."""
+
+    def __init__(self, dim_in, dim_out, approximate="tanh", bias=True):
+        super().__init__()
+        self.proj = nn.Linear(dim_in, dim_out, bias=bias)
+        self.approximate = approximate
+
+
+class FeedForward(nn.Module):
+    """attention.py:1204-1264 with activation_fn='gelu-approximate' (non-gated 4x MLP)."""
+
+    def __init__(self, dim, dim_out=None, mult=4, dropout=0.0, activation_fn="gelu-approximate",
+                 inner_dim=None, bias=True, **_unused):
+        super().__init__()
+        inner_dim = inner_dim or int(dim * mult)
+        dim_out = dim_out or dim
+        if activation_fn != "gelu-approximate":
+            raise NotImplementedError(f"activation_fn={activation_fn!r}: LTX-2B uses "
+                                      "'gelu-approximate' (diffusers_config_mapping.py:76)")
+        self.net = nn.ModuleList([GELU(dim, inner_dim, "tanh", bias), nn.Dropout(dropout),
+                                  nn.Linear(inner_dim, dim_out, bias=bias)])
+
+
+class BasicTransformerBlock(nn.Module):
+    """attention.py:38-321, adaptive_norm='single_scale_shift', standardization rms_norm."""
+
+    def __init__(self, dim, num_attention_heads, attention_head_dim, cross_attention_dim=None,
+                 activation_fn="gelu-approximate", attention_bias=False, norm_eps=1e-5,
+                 qk_norm=None, use_rope=False, adaptive_norm="single_scale_shift",
+                 standardization_norm="rms_norm", norm_elementwise_affine=False, **_unused):
+        super().__init__()
+        if adaptive_norm != "single_scale_shift" or standardization_norm != "rms_norm":
+            raise NotImplementedError("LTX-2B: adaptive_norm single_scale_shift + rms_norm")
+        if norm_elementwise_affine:
+            raise NotImplementedError("LTX-2B: norm_elementwise_affine=False")
+        self.adaptive_norm = adaptive_norm
+        self.norm_eps = norm_eps
+        self.norm1 = RMSNorm(dim, eps=norm_eps, elementwise_affine=False)
+        self.attn1 = Attention(dim, None, num_attention_heads, attention_head_dim,
+                               bias=attention_bias, qk_norm=qk_norm, use_rope=use_rope)
+        self.attn2 = Attention(dim, cross_attention_dim, num_attention_heads, attention_head_dim,
+                               bias=attention_bias, qk_norm=qk_norm, use_rope=use_rope)
+        self.norm2 = RMSNorm(dim, eps=norm_eps, elementwise_affine=False)
+        self.ff = FeedForward(dim, activation_fn=activation_fn)
+        self.scale_shift_table = nn.Parameter(torch.randn(6, dim) / dim ** 0.5)
+        self._pack = None
+        self._pack_key = None
+
+    # ---- frozen-weight packing (fused QKV + W^T copies for the dgrad GEMMs) ----
+    def _frozen(self):
+        a1, a2, ff = self.attn1, self.attn2, self.ff
+        return [a1.to_q.weight, a1.to_q.bias, a1.to_k.weight, a1.to_k.bias, a1.to_v.weight,
+                a1.to_v.bias, a1.to_out[0].weight, _lin(a2.to_q)[0], _lin(a2.to_k)[0],
+                _lin(a2.to_v)[0], _lin(a2.to_out[0])[0], ff.net[0].proj.weight, ff.net[2].weight]
+
+    @torch.no_grad()
+    def packed(self):
+        key = tuple((t.data_ptr(), t._version) for t in self._frozen())
+        if self._pack is not None and self._pack_key == key:
+            return self._pack
+        a1, a2, ff = self.attn1, self.attn2, self.ff
+        for t in self._frozen():
+            if t.requires_grad:
+                raise NotImplementedError(
+                    "fused block backward supports the lora_audio strategy (frozen attention/FF "
+                    "weights); train_mode='full' needs the wgrad path (DESIGN.md, next rows)")
+        p = {}
+        p["qkv_w"] = torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight], 0).contiguous()
+        p["qkv_b"] = torch.cat([a1.to_q.bias, a1.to_k.bias, a1.to_v.bias], 0).contiguous()
+        p["qkv_wT"] = ops.transpose(p["qkv_w"])
+        p["out1_wT"] = ops.transpose(a1.to_out[0].weight)
+        for name, lin in (("q2", a2.to_q), ("k2", a2.to_k), ("v2", a2.to_v), ("o2", a2.to_out[0])):
+            p[name + "_wT"] = ops.transpose(_lin(lin)[0])
+        p["ff1_wT"] = ops.transpose(ff.net[0].proj.weight)
+        p["ff2_wT"] = ops.transpose(ff.net[2].weight)
+        self._pack, self._pack_key = p, key
+        return p
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, in_channels, time_embed_dim):
+        super().__init__()
+        self.linear_1 = nn.Linear(in_channels, time_embed_dim)
+        self.linear_2 = nn.Linear(time_embed_dim, time_embed_dim)
+
+
+class _CombinedTimestepEmbeddings(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.timestep_embedder = TimestepEmbedding(256, dim)
+
+
+class AdaLayerNormSingle(nn.Module):
+    """diffusers AdaLayerNormSingle parameters (emb.timestep_embedder.linear_{1,2}, linear)."""
+
+    def __init__(self, embedding_dim, use_additional_conditions=False):
+        super().__init__()
+        self.emb = _CombinedTimestepEmbeddings(embedding_dim)
+        self.linear = nn.Linear(embedding_dim, 6 * embedding_dim, bias=True)
+
+
+class PixArtAlphaTextProjection(nn.Module):
+    def __init__(self, in_features, hidden_size, out_features=None, act_fn="gelu_tanh"):
+        super().__init__()
+        self.linear_1 = nn.Linear(in_features, hidden_size, bias=True)
+        self.linear_2 = nn.Linear(hidden_size, out_features or hidden_size, bias=True)
+
+
+# ===============================================================================================
+# fused autograd functions
+# ===============================================================================================
+class _Shared:
+    """Per-forward constants shared by all blocks."""
+
+    def __init__(self, B, N, L, heads, head_dim, rope, enc_bias, eps):
+        self.B, self.N, self.L = B, N, L
+        self.H, self.d = heads, head_dim
+        self.D = heads * head_dim
+        self.rope = rope
+        self.enc_bias = enc_bias
+        self.eps = eps
+
+
+_LORA_KEYS = ("q", "k", "v", "o")
+
+
+def _lora_params(blk):
+    """attn2 LoRA (A, B) per target in _LORA_KEYS order, or None (no adapters)."""
+    a2 = blk.attn2
+    lins = (a2.to_q, a2.to_k, a2.to_v, a2.to_out[0])
+    if not all(isinstance(m, LoraLinear) for m in lins):
+        if any(isinstance(m, LoraLinear) for m in lins):
+            raise NotImplementedError("LoRA must wrap all four attn2 projections (training.py:52-60)")
+        return None
+    return lins
+
+
+class _BlockFn(torch.autograd.Function):
+    """One BasicTransformerBlock.forward (attention.py:198-321) + its backward."""
+
+    @staticmethod
+    def forward(ctx, blk, sh, keep, h, enc2, mods, onep, *lora_ab):
+        B, N, L, H, d, D = sh.B, sh.N, sh.L, sh.H, sh.d, sh.D
+        M = B * N
+        W = blk.packed()
+        a1, a2, ff = blk.attn1, blk.attn2, blk.ff
+        ldm = mods.stride(0)
+        has_lora = len(lora_ab) > 0
+        lora = _lora_params(blk) if has_lora else None
+        r = lora[0].r if has_lora else 0
+        s = lora[0].scaling if has_lora else 1.0
+        # ---- 1. norm1 + AdaLN(msa) -> fused QKV -> q/k RMSNorm + RoPE -> SDPA -> gated residual
+        x1, rstd1 = ops.rmsnorm_modulate_fwd(h, mods[:, 0], onep[:, 1], ldm, N, blk.norm_eps)
+        qkv = ops.gemm(x1, W["qkv_w"], bias=W["qkv_b"])
+        del x1
+        qk = torch.empty(M, 2 * D, dtype=torch.bfloat16, device=h.device)
+        _, _, rq1, rk1 = ops.qk_norm_rope_fwd(qkv[:, :D], qkv[:, D:2 * D], a1.q_norm.weight,
+                                              a1.k_norm.weight, sh.rope, q_out=qk[:, :D],
+                                              k_out=qk[:, D:])
+        o1, lse1 = ops.attn_fwd(qk[:, :D], qk[:, D:], qkv[:, 2 * D:], B, H, d, a1.scale)
+        h1 = ops.gemm(o1, a1.to_out[0].weight, bias=a1.to_out[0].bias, epilogue="gated_residual",
+                      aux0=h, aux1=mods[:, 2], rows_per_batch=N)
+        # ---- 2. attn2 on the un-normalised h1 (attention.py:273-285), LoRA fused into the GEMMs
+        wq, bq, _ = _lin(a2.to_q)
+        wk, bk, _ = _lin(a2.to_k)
+        wv, bv, _ = _lin(a2.to_v)
+        wo, bo, _ = _lin(a2.to_out[0])
+        if has_lora:
+            Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo = lora_ab
+            u_q = ops.lora_down(h1, Aq)
+            q2raw = ops.gemm(h1, wq, bias=bq, epilogue="lora", aux1=u_q, aux2=Bq, alpha=s, rank=r)
+            u_k = ops.lora_down(enc2, Ak)
+            k2raw = ops.gemm(enc2, wk, bias=bk, epilogue="lora", aux1=u_k, aux2=Bk, alpha=s, rank=r)
+            u_v = ops.lora_down(enc2, Av)
+            v2 = ops.gemm(enc2, wv, bias=bv, epilogue="lora", aux1=u_v, aux2=Bv, alpha=s, rank=r)
+        else:
+            u_q = u_k = u_v = None
+            q2raw = ops.gemm(h1, wq, bias=bq)
+            k2raw = ops.gemm(enc2, wk, bias=bk)
+            v2 = ops.gemm(enc2, wv, bias=bv)
+        q2, _, rq2, _ = ops.qk_norm_rope_fwd(q2raw, None, a2.q_norm.weight, None, None, B=B, N=N)
+        k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, a2.k_norm.weight, None, None, B=B, N=L)
+        o2, lse2 = ops.attn_fwd(q2, k2, v2, B, H, d, a2.scale, key_bias=sh.enc_bias)
+        if has_lora:
+            u_o = ops.lora_down(o2, Ao)
+            h2 = ops.gemm(o2, wo, bias=bo, epilogue="lora_residual", aux0=h1, aux1=u_o, aux2=Bo,
+                          alpha=s, rank=r)
+        else:
+            u_o = None
+            h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1)
+        # ---- 3. norm2 + AdaLN(mlp) -> FF (tanh-GELU fused) -> gated residual
+        x2, rstd2 = ops.rmsnorm_modulate_fwd(h2, mods[:, 3], onep[:, 4], ldm, N, blk.norm_eps)
+        fpre = torch.empty(M, ff.net[0].proj.out_features, dtype=torch.bfloat16, device=h.device)
+        act = ops.gemm(x2, ff.net[0].proj.weight, bias=ff.net[0].proj.bias, epilogue="gelu",
+                       aux0=fpre)
+        del x2
+        h3 = ops.gemm(act, ff.net[2].weight, bias=ff.net[2].bias, epilogue="gated_residual",
+                      aux0=h2, aux1=mods[:, 5], rows_per_batch=N)
+        del act
+        if keep:
+            lora_saved = (u_q, u_k, u_v, u_o) if has_lora else ()
+            ctx.save_for_backward(h, enc2, mods, onep, rstd1, qkv, qk, rq1, rk1, o1, lse1, h1,
+                                  q2raw, rq2, q2, k2raw, rk2, k2, v2, o2, lse2, h2, rstd2, fpre,
+                                  *lora_ab, *lora_saved)
+            ctx.blk, ctx.sh, ctx.has_lora = blk, sh, has_lora
+        return h3
+
+    @staticmethod
+    def backward(ctx, dh3):
+        blk, sh = ctx.blk, ctx.sh
+        B, N, L, H, d, D = sh.B, sh.N, sh.L, sh.H, sh.d, sh.D
+        has_lora = ctx.has_lora
+        saved = ctx.saved_tensors
+        (h, enc2, mods, onep, rstd1, qkv, qk, rq1, rk1, o1, lse1, h1, q2raw, rq2, q2, k2raw, rk2,
+         k2, v2, o2, lse2, h2, rstd2, fpre) = saved[:24]
+        W = blk.packed()
+        a1, a2 = blk.attn1, blk.attn2
+        ldm = mods.stride(0)
+        dh3 = dh3.contiguous()
+        grads_lora = []
+        if has_lora:
+            Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo = saved[24:32]
+            u_q, u_k, u_v, u_o = saved[32:36]
+            lora = _lora_params(blk)
+            r, s = lora[0].r, lora[0].scaling
+        # ---- FF: h3 = h2 + g_mlp * ff(x2)
+        d_ffo = ops.gate_mul(dh3, mods[:, 5], N)
+        d_f = ops.gemm(d_ffo, W["ff2_wT"], epilogue="gelu_bwd", aux0=fpre)
+        del d_ffo
+        dx2 = ops.gemm(d_f, W["ff1_wT"])
+        del d_f
+        dh2 = ops.rmsnorm_modulate_bwd(dx2, h2, rstd2, onep[:, 4], ldm, N, dres=dh3)
+        del dx2
+        # ---- attn2: h2 = h1 + to_out(o2)   (LoRA grads: peft f32 adapters)
+        if has_lora:
+            dBo = ops.lora_wgrad(dh2, u_o, alpha=s)
+            w_o = ops.lora_down(dh2, Bo, alpha=s, transposed=True)
+            dAo = ops.lora_wgrad(o2, w_o, transpose_out=True)
+            do2 = ops.gemm(dh2, W["o2_wT"], epilogue="lora_dgrad_accum", aux1=w_o, aux2=Ao,
+                           rank=r)
+        else:
+            do2 = ops.gemm(dh2, W["o2_wT"])
+        dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
+                                     key_bias=sh.enc_bias)
+        del do2
+        dq2raw, _ = ops.qk_norm_rope_bwd(dq2, q2raw, a2.q_norm.weight, rq2, B=B, N=N)
+        dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=B, N=L)
+        del dq2, dk2
+        if has_lora:
+            dBq = ops.lora_wgrad(dq2raw, u_q, alpha=s)
+            w_q = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True)
+            dAq = ops.lora_wgrad(h1, w_q, transpose_out=True)
+            dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="lora_dgrad_accum", aux0=dh2, aux1=w_q,
+                           aux2=Aq, rank=r)
+            dBk = ops.lora_wgrad(dk2raw, u_k, alpha=s)
+            w_k = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True)
+            dAk = ops.lora_wgrad(enc2, w_k, transpose_out=True)
+            denc = ops.gemm(dk2raw, W["k2_wT"], epilogue="lora_dgrad_accum", aux1=w_k, aux2=Ak,
+                            rank=r)
+            dBv = ops.lora_wgrad(dv2, u_v, alpha=s)
+            w_v = ops.lora_down(dv2, Bv, alpha=s, transposed=True)
+            dAv = ops.lora_wgrad(enc2, w_v, transpose_out=True)
+            ops.gemm(dv2, W["v2_wT"], epilogue="lora_dgrad_accum", aux0=denc, aux1=w_v, aux2=Av,
+                     rank=r, out=denc)
+            grads_lora = [dAq, dBq, dAk, dBk, dAv, dBv, dAo, dBo]
+        else:
+            dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2)
+            denc = ops.gemm(dk2raw, W["k2_wT"])
+            ops.gemm(dv2, W["v2_wT"], epilogue="accum", aux0=denc, out=denc)
+        del dq2raw, dk2raw, dv2, dh2
+        # ---- attn1: h1 = h + g_msa * to_out(sdpa(rope(qn(q)), rope(kn(k)), v))
+        d_y1 = ops.gate_mul(dh1, mods[:, 2], N)
+        do1 = ops.gemm(d_y1, W["out1_wT"])
+        del d_y1
+        M = B * N
+        dqkv = torch.empty(M, 3 * D, dtype=torch.bfloat16, device=h.device)
+        dq1, dk1, _ = ops.attn_bwd(qk[:, :D], qk[:, D:], qkv[:, 2 * D:], o1, do1, lse1, B, H, d,
+                                   a1.scale, dv=dqkv[:, 2 * D:])
+        del do1
+        ops.qk_norm_rope_bwd(dq1, qkv[:, :D], a1.q_norm.weight, rq1, dk1, qkv[:, D:2 * D],
+                             a1.k_norm.weight, rk1, sh.rope, dq_out=dqkv[:, :D],
+                             dk_out=dqkv[:, D:2 * D])
+        del dq1, dk1
+        dh = None
+        if ctx.needs_input_grad[3]:  # (blk, sh, keep, h, ...)
+            dx1 = ops.gemm(dqkv, W["qkv_wT"])
+            dh = ops.rmsnorm_modulate_bwd(dx1, h, rstd1, onep[:, 1], ldm, N, dres=dh1)
+        return (None, None, None, dh, denc, None, None, *grads_lora)
+
+
+class _CaptionProjFn(torch.autograd.Function):
+    """PixArtAlphaTextProjection (transformer3d.py:167-172, 494-499): Linear -> tanh-GELU ->
+    Linear, trainable in lora_audio (training.py:69-73). Weight grads via transposed GEMMs."""
+
+    @staticmethod
+    def forward(ctx, enc, w1, b1, w2, b2):
+        pre = torch.empty(enc.shape[0], w1.shape[0], dtype=torch.bfloat16, device=enc.device)
+        act = ops.gemm(enc, w1, bias=b1, epilogue="gelu", aux0=pre)
+        out = ops.gemm(act, w2, bias=b2)
+        ctx.save_for_backward(enc, pre, act, w2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        enc, pre, act, w2 = ctx.saved_tensors
+        dout = dout.contiguous()
+        n = enc.shape[0]
+        npad = (n + 63) // 64 * 64  # GEMM K must be a multiple of 64: zero-pad the token axis
+
+        def tpad(x):
+            buf = torch.zeros(x.shape[1], npad, dtype=torch.bfloat16, device=x.device)
+            ops.transpose(x, out=buf[:, :n])
+            return buf
+
+        doT = tpad(dout)
+        dw2 = ops.gemm(doT, tpad(act))
+        db2 = ops.colsum(dout)
+        dpre = ops.gemm(dout, ops.transpose(w2), epilogue="gelu_bwd", aux0=pre)
+        dpT = tpad(dpre)
+        dw1 = ops.gemm(dpT, tpad(enc))
+        db1 = ops.colsum(dpre)
+        return None, dw1, db1, dw2, db2
+
+
+class _HeadFn(torch.autograd.Function):
+    """Output modulation + projection (transformer3d.py:553-561): LayerNorm (no affine,
+    eps 1e-6) * (1 + scale) + shift, then proj_out."""
+
+    @staticmethod
+    def forward(ctx, h, mod, onep, w, b, N, eps):
+        ldm = mod.stride(0)
+        y, mean, rstd = ops.layernorm_modulate_fwd(h, mod[:, 0], onep[:, 1], ldm, N, eps)
+        out = ops.gemm(y, w, bias=b)
+        ctx.save_for_backward(h, mean, rstd, onep, w)
+        ctx.N = N
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        h, mean, rstd, onep, w = ctx.saved_tensors
+        wT = ops.transpose(w)
+        dy = ops.gemm(dout.contiguous(), wT)
+        dh = ops.layernorm_modulate_bwd(dy, h, mean, rstd, onep[:, 1], onep.stride(0), ctx.N)
+        return dh, None, None, None, None, None, None
+
+
+# ===============================================================================================
+# the model
+# ===============================================================================================
+class Transformer3DModel(nn.Module):
+    _supports_gradient_checkpointing = True
+
+    def __init__(self, num_attention_heads: int = 16, attention_head_dim: int = 88,
+                 in_channels: Optional[int] = None, out_channels: Optional[int] = None,
+                 num_layers: int = 1, dropout: float = 0.0, norm_num_groups: int = 32,
+                 cross_attention_dim: Optional[int] = None, attention_bias: bool = False,
+                 num_vector_embeds: Optional[int] = None, activation_fn: str = "geglu",
+                 num_embeds_ada_norm: Optional[int] = None, use_linear_projection: bool = False,
+                 only_cross_attention: bool = False, double_self_attention: bool = False,
+                 upcast_attention: bool = False, adaptive_norm: str = "single_scale_shift",
+                 standardization_norm: str = "layer_norm", norm_elementwise_affine: bool = True,
+                 norm_eps: float = 1e-5, attention_type: str = "default",
+                 caption_channels: int = None, use_tpu_flash_attention: bool = False,
+                 qk_norm: Optional[str] = None, positional_embedding_type: str = "rope",
+                 positional_embedding_theta: Optional[float] = None,
+                 positional_embedding_max_pos: Optional[List[int]] = None,
+                 timestep_scale_multiplier: Optional[float] = None,
+                 causal_temporal_positioning: bool = False,
+                 patchifier: Optional[SymmetricPatchifier] = None):
+        super().__init__()
+        self.config = dict(
+            num_attention_heads=num_attention_heads, attention_head_dim=attention_head_dim,
+            in_channels=in_channels, out_channels=out_channels, num_layers=num_layers,
+            dropout=dropout, norm_num_groups=norm_num_groups,
+            cross_attention_dim=cross_attention_dim, attention_bias=attention_bias,
+            num_vector_embeds=num_vector_embeds, activation_fn=activation_fn,
+            num_embeds_ada_norm=num_embeds_ada_norm, use_linear_projection=use_linear_projection,
+            only_cross_attention=only_cross_attention,
+            double_self_attention=double_self_attention, upcast_attention=upcast_attention,
+            adaptive_norm=adaptive_norm, standardization_norm=standardization_norm,
+            norm_elementwise_affine=norm_elementwise_affine, norm_eps=norm_eps,
+            attention_type=attention_type, caption_channels=caption_channels,
+            use_tpu_flash_attention=use_tpu_flash_attention, qk_norm=qk_norm,
+            positional_embedding_type=positional_embedding_type,
+            positional_embedding_theta=positional_embedding_theta,
+            positional_embedding_max_pos=positional_embedding_max_pos,
+            timestep_scale_multiplier=timestep_scale_multiplier,
+            causal_temporal_positioning=causal_temporal_positioning)
+        if positional_embedding_type != "rope":
+            raise ValueError("Absolute positional embedding is no longer supported")
+        if positional_embedding_theta is None or positional_embedding_max_pos is None:
+            raise ValueError("rope needs positional_embedding_theta and _max_pos")
+        if use_tpu_flash_attention:
+            raise NotImplementedError("TPU flash attention is out of scope on MI355X")
+        self.use_tpu_flash_attention = False
+        self.num_attention_heads = num_attention_heads
+        self.attention_head_dim = attention_head_dim
+        inner_dim = num_attention_heads * attention_head_dim
+        self.inner_dim = inner_dim
+        self.patchify_proj = nn.Linear(in_channels, inner_dim, bias=True)
+        self.positional_embedding_type = positional_embedding_type
+        self.positional_embedding_theta = positional_embedding_theta
+        self.positional_embedding_max_pos = positional_embedding_max_pos
+        self.use_rope = True
+        self.timestep_scale_multiplier = timestep_scale_multiplier
+        self.patchifier = patchifier
+        self.transformer_blocks = nn.ModuleList([
+            BasicTransformerBlock(inner_dim, num_attention_heads, attention_head_dim,
+                                  cross_attention_dim=cross_attention_dim,
+                                  activation_fn=activation_fn, attention_bias=attention_bias,
+                                  norm_eps=norm_eps, qk_norm=qk_norm, use_rope=True,
+                                  adaptive_norm=adaptive_norm,
+                                  standardization_norm=standardization_norm,
+                                  norm_elementwise_affine=norm_elementwise_affine)
+            for _ in range(num_layers)])
+        self.out_channels = in_channels if out_channels is None else out_channels
+        self.norm_out = nn.LayerNorm(inner_dim, elementwise_affine=False, eps=1e-6)
+        self.scale_shift_table = nn.Parameter(torch.randn(2, inner_dim) / inner_dim ** 0.5)
+        self.proj_out = nn.Linear(inner_dim, self.out_channels)
+        self.adaln_single = AdaLayerNormSingle(inner_dim)
+        self.caption_projection = None
+        if caption_channels is not None:
+            self.caption_projection = PixArtAlphaTextProjection(caption_channels, inner_dim)
+        self.gradient_checkpointing = False
+
+    # ---- construction ----------------------------------------------------------------------
+    @classmethod
+    def from_config(cls, config: Dict[str, Any], **kwargs):
+        import inspect
+        merged = dict(config)
+        merged.update(kwargs)
+        accepted = inspect.signature(cls.__init__).parameters
+        return cls(**{k: v for k, v in merged.items() if k in accepted and k != "self"})
+
+    def load_state_dict(self, state_dict, *args, **kwargs):
+        """Strips the ComfyUI 'model.diffusion_model.' prefix (transformer3d.py:279-292)."""
+        if any(k.startswith("model.diffusion_model.") for k in state_dict):
+            state_dict = {k.replace("model.diffusion_model.", ""): v for k, v in state_dict.items()
+                          if k.startswith("model.diffusion_model.")}
+        return super().load_state_dict(state_dict, *args, **kwargs)
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_path, *args, **kwargs):
+        """Single-file safetensors with metadata['config'] = {"transformer": {...}}, or a
+        diffusers-style directory with transformer/config.json (transformer3d.py:294-359)."""
+        from safetensors import safe_open
+        path = Path(pretrained_model_path)
+        if path.is_dir():
+            with open(path / "transformer" / "config.json") as f:
+                config = json.load(f)
+            if "positional_embedding_theta" not in config:
+                config = OURS_TRANSFORMER_CONFIG  # the only diffusers config LTX maps
+            state = {}
+            for part in glob.glob(str(path / "transformer" / "diffusion_pytorch_model*.safetensors")):
+                with safe_open(part, framework="pt", device="cpu") as f:
+                    for k in f.keys():
+                        state[k] = f.get_tensor(k)
+            renamed = {}
+            for k, v in state.items():
+                nk = k
+                for a, b in TRANSFORMER_KEYS_RENAME_DICT.items():
+                    nk = nk.replace(a, b)
+                renamed[nk] = v
+            state = renamed
+        elif path.is_file() and str(path).endswith(".safetensors"):
+            state = {}
+            with safe_open(str(path), framework="pt", device="cpu") as f:
+                metadata = f.metadata()
+                for k in f.keys():
+                    state[k] = f.get_tensor(k)
+            config = json.loads(metadata["config"])["transformer"]
+        else:
+            raise FileNotFoundError(str(path))
+        with torch.device("meta"):
+            model = cls.from_config(config)
+        model.load_state_dict(state, assign=True, strict=True)
+        patchifier = kwargs.get("patchifier")
+        if patchifier is not None:
+            model.patchifier = patchifier
+        return model
+
+    @property
+    def dtype(self):
+        return self.patchify_proj.weight.dtype
+
+    @property
+    def device(self):
+        return self.patchify_proj.weight.device
+
+    def _set_gradient_checkpointing(self, module, value=False):
+        if hasattr(module, "gradient_checkpointing"):
+            module.gradient_checkpointing = value
+
+    def create_skip_layer_mask(self, batch_size, num_conds, ptb_index, skip_block_list=None):
+        """transformer3d.py:187-203 (used by the inference pipeline's STG)."""
+        if skip_block_list is None or len(skip_block_list) == 0:
+            return None
+        mask = torch.ones((len(self.transformer_blocks), batch_size * num_conds),
+                          device=self.device, dtype=self.dtype)
+        for block_idx in skip_block_list:
+            mask[block_idx, ptb_index::num_conds] = 0
+        return mask
+
+    def get_fractional_positions(self, indices_grid):
+        return torch.stack([indices_grid[:, i] / self.positional_embedding_max_pos[i]
+                            for i in range(3)], dim=-1)
+
+    # ---- forward ---------------------------------------------------------------------------
+    def forward(self, hidden_states, indices_grid, ref_image_hidden_states=None,
+                pose_hidden_states=None, encoder_hidden_states=None, timestep=None,
+                class_labels=None, cross_attention_kwargs=None, attention_mask=None,
+                encoder_attention_mask=None, skip_layer_mask=None, skip_layer_strategy=None,
+                return_dict=True):
+        """transformer3d.py:361-565 (training call). Does not mutate `hidden_states`."""
+        _lib.ensure_device(hidden_states.device)
+        if skip_layer_mask is not None or skip_layer_strategy is not None:
+            raise NotImplementedError("skip-layer (STG) guidance is an inference feature (next row)")
+        if attention_mask is not None:
+            raise NotImplementedError("self-attention masks are not used on the LTX training path")
+        dt = torch.bfloat16
+        if ref_image_hidden_states is None or pose_hidden_states is None:
+            raise ValueError("the avatar model conditions on ref_image_hidden_states and pose_hidden_states")
+        # conditioning lerp (transformer3d.py:447-466), out of place
+        x_in = ops.condition_lerp(hidden_states.to(dt), ref_image_hidden_states.to(dt),
+                                  pose_hidden_states.to(dt))
+        out = self._forward_tokens(x_in, indices_grid, encoder_hidden_states, timestep,
+                                   encoder_attention_mask)
+        if not return_dict:
+            return (out,)
+        return Transformer3DModelOutput(sample=out)
+
+    def _forward_tokens(self, x_in, indices_grid, encoder_hidden_states, timestep,
+                        encoder_attention_mask=None):
+        """Everything after the conditioning lerp: patchify_proj, AdaLN-single, RoPE, caption
+        projection, the block stack and the output head. x_in [B, N, C] bf16 -> [B, N, C_out]."""
+        B, N, C = x_in.shape
+        D = self.inner_dim
+        H = self.num_attention_heads
+        dt = torch.bfloat16
+        if self.dtype != dt:
+            raise TypeError("the MI355X path computes in bf16: call model.to(torch.bfloat16)")
+        # encoder mask -> additive bias (transformer3d.py:441-445): (1 - m) * -10000 in bf16
+        enc_bias = None
+        if encoder_attention_mask is not None:
+            if encoder_attention_mask.ndim == 2:
+                enc_bias = ((1 - encoder_attention_mask.to(dt)) * -10000.0).float().contiguous()
+            else:
+                enc_bias = encoder_attention_mask.reshape(B, -1).float().contiguous()
+        with torch.no_grad():
+            h = ops.gemm(x_in.reshape(B * N, C), self.patchify_proj.weight,
+                         bias=self.patchify_proj.bias)
+            tmod, emb = self._adaln(timestep, B)
+        rope = ops.RopeSpec(indices_grid, D, self.positional_embedding_theta,
+                            self.positional_embedding_max_pos)
+        enc = encoder_hidden_states.to(dt)
+        L = enc.shape[1]
+        enc2d = enc.reshape(B * L, enc.shape[2]).contiguous()
+        cp = self.caption_projection
+        enc2 = _CaptionProjFn.apply(enc2d, cp.linear_1.weight, cp.linear_1.bias,
+                                    cp.linear_2.weight, cp.linear_2.bias)
+        eps = self.transformer_blocks[0].norm_eps if len(self.transformer_blocks) else 1e-6
+        sh = _Shared(B, N, L, H, self.attention_head_dim, rope, enc_bias, eps)
+        keep = torch.is_grad_enabled()
+        for blk in self.transformer_blocks:
+            with torch.no_grad():
+                mods, onep = ops.ada_modulation(blk.scale_shift_table, tmod, (1 << 1) | (1 << 4))
+            lora = _lora_params(blk)
+            ab = []
+            if lora is not None:
+                for m in lora:
+                    ab += [m.lora_A["default"].weight, m.lora_B["default"].weight]
+            if self.training and self.gradient_checkpointing and keep:
+                h = torch.utils.checkpoint.checkpoint(
+                    lambda *a, _b=blk: _BlockFn.apply(_b, sh, True, *a),
+                    h, enc2, mods, onep, *ab, use_reentrant=False)
+            else:
+                h = _BlockFn.apply(blk, sh, keep, h, enc2, mods, onep, *ab)
+        with torch.no_grad():
+            hmod, honep = ops.ada_modulation(self.scale_shift_table, emb, 1 << 1, broadcast=True)
+        out = _HeadFn.apply(h, hmod, honep, self.proj_out.weight, self.proj_out.bias, N, 1e-6)
+        return out.view(B, N, self.out_channels)
+
+    def _adaln(self, timestep, B):
+        """AdaLayerNormSingle (transformer3d.py:473-491): returns (tmod [B,6D], emb [B,D])."""
+        if timestep.numel() != B:
+            raise NotImplementedError("per-token timesteps are an inference feature (next row)")
+        mult = float(self.timestep_scale_multiplier or 1.0)
+        ad = self.adaln_single
+        te = ops.timestep_embedding(timestep.reshape(B).float().contiguous(), mult)
+        e1 = ops.gemm(te, ad.emb.timestep_embedder.linear_1.weight,
+                      bias=ad.emb.timestep_embedder.linear_1.bias)
+        emb = ops.gemm(ops.silu(e1), ad.emb.timestep_embedder.linear_2.weight,
+                       bias=ad.emb.timestep_embedder.linear_2.bias)
+        tmod = ops.gemm(ops.silu(emb), ad.linear.weight, bias=ad.linear.bias)
+        return tmod, emb
