@@ -1,0 +1,264 @@
+"""LTX-2B LoRA training-step benchmark on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N --steps K --warmup W]            (N = 1)
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W  (N > 1, one rank per GPU, RCCL)
+
+Workload (BASELINE.json configs[1]): LTX-Video 2B (28 layers, D 2048, 32x64 heads,
+FF 8192, caption 4096), bf16, random-init weights of that architecture, LoRA r=16 (alpha 16) on
+attn2 q/k/v/out + trainable caption_projection, synthetic 49-frame 512x512 VAE latents
+[8,128,7,16,16] per GPU (N = 1792 tokens), pose [8,128,7,16,16], ref [8,128,1,16,16],
+T5-shaped prompt [1,256,4096] with the first 16 tokens valid. One "step" = one micro-batch
+forward + backward (train_step); every 16th step also runs the DP gradient all-reduce and the
+AdamW update (gradient_accumulation_steps 16, train-avatars.yaml:23), inside the timed region.
+
+Prints ONE JSON line (rank 0): value = samples/s summed over ranks (= tokens/s / 1792), plus the
+roofline of the dominant kernel (the FF-up GEMM, 2*M*N*K flops per launch, timed live with HIP
+events on its stream) and the CPU baseline (the oracle restatement, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "video-generation-for-human-avatars_amd"))
+
+import torch
+import torch.distributed as dist
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, spec)
+HBM_PEAK_GBS = 8000.0
+B_PER_GPU, F_LAT, H_LAT, W_LAT, L_TXT = 8, 7, 16, 16, 256
+LORA_RANK = 16
+ACCUM = 16
+
+
+def step_flops_per_sample(N, r=LORA_RANK, D=2048, FF=8192, Lyr=28, L=L_TXT, C=128, Cc=4096):
+    """Algorithmic FLOPs of one fwd+bwd per sample: dgrad-only for frozen
+    weights, wgrad for LoRA and caption_projection, attention bwd = 2x fwd, no recompute."""
+    lin = 2 * N * D * D * 6 + 4 * L * D * D + 4 * N * D * FF
+    att = 4 * N * N * D + 4 * N * L * D
+    lora = 8 * r * D * (N + L)
+    fwd = Lyr * (lin + att + lora) + 4 * N * C * D + 2 * L * (Cc * D + D * D)
+    bwd = Lyr * (lin + 2 * att + 2 * lora) + 2 * N * D * C + 2 * L * (Cc * D + D * D) + 2 * L * D * D
+    return fwd, bwd
+
+
+def build_model(device, seed=1234):
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.lora import apply_training_strategy
+    from ltx_amd.patchifier import SymmetricPatchifier
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG, Transformer3DModel
+    with torch.device("meta"):
+        model = Transformer3DModel.from_config(OURS_TRANSFORMER_CONFIG)
+        apply_training_strategy(model, TrainConfig(checkpoint_path="-", lora_rank=LORA_RANK,
+                                                   lora_alpha=LORA_RANK), "lora_audio")
+    g = torch.Generator(device=device).manual_seed(seed)
+    sd = {}
+    for name, p in model.named_parameters():
+        dt = torch.float32 if "lora_" in name else torch.bfloat16
+        t = torch.empty(p.shape, dtype=torch.float32, device=device)
+        if p.dim() == 2:
+            t.normal_(0, 1.0 / math.sqrt(p.shape[1]), generator=g)
+        elif "norm" in name:
+            t.fill_(1.0)
+        elif name.endswith("scale_shift_table"):
+            t.normal_(0, 1.0 / math.sqrt(p.shape[-1]), generator=g)
+        else:
+            t.normal_(0, 0.02, generator=g)
+        if "lora_B" in name:
+            t.normal_(0, 0.01, generator=g)  # non-zero so the dA path carries signal
+        sd[name] = t.to(dt)
+    model.load_state_dict(sd, assign=True, strict=True)
+    for n, p in model.named_parameters():
+        p.requires_grad_(("lora_" in n) or ("caption_projection" in n))
+    model.patchifier = SymmetricPatchifier(1)
+    model.train()
+    return model
+
+
+def synthetic_batch(device, rank):
+    g = torch.Generator().manual_seed(20251015 + rank)
+    B = B_PER_GPU
+    batch = {"latents": torch.randn(B, 128, F_LAT, H_LAT, W_LAT, generator=g),
+             "ref_image_latents": torch.randn(B, 128, 1, H_LAT, W_LAT, generator=g),
+             "pose_latents": torch.randn(B, 128, F_LAT, H_LAT, W_LAT, generator=g)}
+    batch = {k: v.to(device=device, dtype=torch.bfloat16) for k, v in batch.items()}
+    prompt = torch.randn(1, L_TXT, 4096, generator=g).to(device=device, dtype=torch.bfloat16)
+    mask = (torch.arange(L_TXT) < 16).long().view(1, L_TXT).to(device)
+    return batch, prompt, mask
+
+
+def cpu_baseline(budget_layers=4):
+    """The oracle restatement (oracle/ltx_oracle.py) on the host cores: config A at B=1,
+    N = 1792, `budget_layers` of the 28 blocks, one warm-up + one timed fwd+bwd; per-sample
+    time extrapolated x(28/budget_layers) (the non-block prologue/head is scaled too, which
+    makes the CPU figure slightly pessimistic)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import ltx_oracle as O
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = dict(OURS_TRANSFORMER_CONFIG)
+    cfg["num_layers"] = budget_layers
+    g = torch.Generator().manual_seed(0)
+    p = {}
+    for name, shape in O.param_shapes(cfg, LORA_RANK).items():
+        t = torch.randn(shape, generator=g) * (1.0 / math.sqrt(shape[-1]) if len(shape) == 2 else 0.02)
+        if len(shape) == 1 and "norm" in name:
+            t = torch.ones(shape)
+        t = t.to(torch.float32 if "lora_" in name else torch.bfloat16)
+        if ("lora_" in name) or ("caption_projection" in name):
+            t.requires_grad_(True)
+        p[name] = t
+    lat = torch.randn(1, 128, F_LAT, H_LAT, W_LAT, generator=g)
+    ref = torch.randn(1, 128, 1, H_LAT, W_LAT, generator=g)
+    pose = torch.randn(1, 128, F_LAT, H_LAT, W_LAT, generator=g)
+    prompt = torch.randn(1, L_TXT, 4096, generator=g)
+    mask = (torch.arange(L_TXT) < 16).long().view(1, L_TXT)
+    times = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        r = O.train_step(p, cfg, lat, ref, pose, prompt, mask)
+        r["loss"].backward()
+        times.append(time.perf_counter() - t0)
+        for v in p.values():
+            v.grad = None
+    per_sample = times[-1] * (28.0 / budget_layers)
+    return {"value": 1.0 / per_sample, "unit": "samples/s", "cores": threads, "kind": "port",
+            "tokens_per_s": F_LAT * H_LAT * W_LAT / per_sample,
+            "sample": (f"oracle/ltx_oracle.py train_step fwd+bwd, B=1, N={F_LAT*H_LAT*W_LAT}, "
+                       f"{budget_layers}/28 LTX-2B blocks timed (1 warm-up + 1 timed step, "
+                       f"{times[-1]:.1f} s) and scaled x{28/budget_layers:g}; torch "
+                       f"{torch.__version__} CPU, {threads} threads, cpu_count={os.cpu_count()}")}
+
+
+def load_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary (or None)."""
+    path = os.path.join(REPO, "profiles", "pmc_dominant_gemm.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    device = torch.device("cuda", torch.cuda.current_device())
+
+    from ltx_amd import _lib, ops
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    from ltx_amd.training import FusedAdamW, GradAllReduce, train_step
+    _lib.ensure_device(device)
+
+    model = build_model(device)
+    batch, prompt, mask = synthetic_batch(device, rank)
+    cfg = TrainConfig(checkpoint_path="-", batch_size=B_PER_GPU, learning_rate=1e-4,
+                      lora_rank=LORA_RANK, lora_alpha=LORA_RANK, gradient_accumulation_steps=ACCUM,
+                      rf_log_normal_mu=-0.5, rf_log_normal_sigma=1.0)
+    sched = RectifiedFlowScheduler(num_train_timesteps=1000, shifting=None)
+    trainable = [p for p in model.parameters() if p.requires_grad]
+    opt = FusedAdamW(trainable, lr=cfg.learning_rate)
+    reducer = GradAllReduce(trainable)
+    torch.manual_seed(20251015 + rank)
+
+    N = F_LAT * H_LAT * W_LAT
+    M = B_PER_GPU * N
+    dom_key = (M, 8192, 2048, "gelu")  # FF-up GEMM (x2 [M,2048] . W1^T -> [M,8192] + tanh-GELU)
+    timer = ops.LaunchTimer(dom_key)
+
+    def one_step(i):
+        train_step(model, batch, sched, model.patchifier, cfg, prompt, mask, device)
+        if (i + 1) % ACCUM == 0:
+            reducer()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+
+    for i in range(args.warmup):
+        one_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ops.set_launch_timer(timer)
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        one_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ops.set_launch_timer(None)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    dom_ms = timer.mean_ms()
+
+    samples = B_PER_GPU * args.steps * world
+    value = samples / elapsed
+    fwd, bwd = step_flops_per_sample(N)
+    step_tflops = (fwd + bwd) * B_PER_GPU * args.steps / (elapsed * 1e12)  # per GPU
+    dom_flops = 2.0 * dom_key[0] * dom_key[1] * dom_key[2]
+    achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+    line = {
+        "metric": "LTX-2B LoRA train-step samples/sec (latent-tokens/sec = samples/sec x 1792)",
+        "value": round(value, 4),
+        "unit": "samples/s",
+        "tokens_per_s": round(value * N, 1),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic latents/pose/ref/prompt of the configured shapes; random-init LTX-2B weights",
+        "config": {"workload": "LTX-Video 2B LoRA(r=16, attn2 q/k/v/out) + caption_projection "
+                               "train step, 49f 512x512 -> latent 7x16x16 (N=1792), 1xMI355X per rank",
+                   "model": "LTX-Video-2B (28 layers, D 2048, 32x64 heads)", "global_batch": B_PER_GPU * world,
+                   "micro_batch_per_gpu": B_PER_GPU, "seq_len": N, "text_len": L_TXT,
+                   "grad_accum": ACCUM, "parallelism": f"dp{world}"},
+        "step_tflops_per_gpu": round(step_tflops, 1),
+        "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+        "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel<GELU> FF-up [14336x2048].[8192x2048]^T",
+                     "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": load_traffic(),
+                     "launch_ms": round(dom_ms, 4), "launches": len(timer.pairs)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            line["cpu_baseline"] = cpu_baseline()
+        except Exception as exc:  # the baseline must never hide the GPU measurement
+            line["cpu_baseline"] = {"value": None, "error": repr(exc)[:200]}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

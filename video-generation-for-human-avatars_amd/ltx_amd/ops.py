@@ -274,6 +274,28 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
 # ---------------------------------------------------------------------------------------------
 # GEMM + LoRA
 # ---------------------------------------------------------------------------------------------
+class LaunchTimer:
+    """Brackets every GEMM launch of one (M, N, K, epilogue) with HIP events on the stream the
+    kernel is launched on (bench.py's live per-launch duration for the roofline figure)."""
+
+    def __init__(self, key):
+        self.key = key
+        self.pairs = []
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        ts = [a.elapsed_time(b) for a, b in self.pairs]
+        return sum(ts) / len(ts) if ts else float("nan")
+
+
+_timer = None
+
+
+def set_launch_timer(timer):
+    global _timer
+    _timer = timer
+
+
 def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2=None,
          alpha=1.0, rank=0, rows_per_batch=0):
     """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias)); see LTX_EPI_* in ltx_hip.h."""
@@ -287,9 +309,16 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
     ld0 = _rows(aux0, "aux0") if aux0 is not None else 0
     ld1 = _rows(aux1, "aux1") if aux1 is not None else 0
     ld2 = _rows(aux2, "aux2") if aux2 is not None else 0
+    timed = _timer is not None and _timer.key == (M, N, K, epilogue)
+    if timed:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
     call("ltx_gemm_bf16_nt", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(out), _rows(out, "out"),
          M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1), ld1, _p(aux2), ld2,
          float(alpha), rank, rows_per_batch, _s())
+    if timed:
+        ev1.record()
+        _timer.pairs.append((ev0, ev1))
     return out
 
 
