@@ -157,6 +157,10 @@ int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, voi
                      int64_t ld1, const void* aux2, int64_t ld2, float alpha, int64_t rank,
                      int64_t rows_per_batch, void* stream);
 
+/* Tuning knob for A/B measurements of GEMM schedules (0: per-tile DMA split over two quarters,
+ * the default; 1: one burst). Process-global. */
+int ltx_gemm_set_variant(int variant);
+
 /* ---- LoRA skinny contractions in f32 (peft lora_A / lora_B, training.py:50-68) --------------- */
 /* out[m,j] = alpha * sum_k x[m,k] * Wr[j,k], Wr element (j,k) at Wr[j*wj + k*wk]; x bf16 [M,K]
  * (ldx), out f32 [M,r] (ldo). lora_A forward (u = x.A^T: wj = K, wk = 1) and the lora_B dgrad

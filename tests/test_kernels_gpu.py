@@ -44,7 +44,7 @@ def g(*shape, dtype=torch.bfloat16, scale=1.0, seed=0):
 
 # ------------------------------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 136, 128), (1024, 2048, 2048), (8, 768, 256),
-                                   (14336 // 7, 6144, 2048)])
+                                   (14336 // 7, 6144, 2048), (4000, 4104, 192), (14336, 2048, 8192)])
 def test_gemm_store(M, N, K):
     from ltx_amd import ops
     a, w, b = g(M, K, seed=1), g(N, K, seed=2, scale=K ** -0.5), g(N, seed=3)

@@ -13,6 +13,8 @@
 // image is lane-linear in LDS, so the XOR swizzle (16-B chunk ^= row & 7, conflict-free for the
 // 16x16x32 fragment reads) is applied to the per-lane SOURCE address and to the ds_read address.
 // Block order: XCD-aware (blocks b, b+8 share an XCD / L2) then grouped by 8 row-tiles.
+#include <cstdlib>
+
 #include "common.h"
 #include "ltx_hip.h"
 
@@ -86,7 +88,7 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       *(u32x4*)((bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0) = pk;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) out8[j] = gelu_tanh(v[j]);
+    for (int j = 0; j < 8; ++j) out8[j] = gelu_tanh_fast(v[j]);
   } else if constexpr (EPI == LTX_EPI_GATED_RESIDUAL) {
     // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1)
     const int b = m / p.rows_per_batch;
@@ -282,10 +284,226 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Large-tile kernel: 256 (m) x 256 (n) output tile, BK = 64, 512 threads = 8 waves as 4 (m) x 2
+// (n), each wave 64 m x 128 n = 4 x 8 tiles of v_mfma_f32_16x16x32_bf16 (128 accumulator VGPRs).
+// One workgroup per CU: two 64 KiB stages (X[256][64] + W[256][64] swizzled bf16), 131 FLOP per
+// staged byte (vs 87 for 256x128), which keeps the L2 demand near 11 TB/s at 1.5 PF.
+// Per K-tile a wave runs 4 quarters Q=(k-half h, n-half nh) of 16 MFMAs; every quarter first
+// issues the ds_reads of the NEXT quarter (A = W fragments per quarter, B = X fragments per
+// k-half), so LDS latency always hides under 16 MFMAs. Between Q2 and Q3 all reads of tile t are
+// done: counted wait (tile t+1 landed) + lgkmcnt(0) + raw s_barrier in one asm statement, then
+// tile t+2 is DMA'd into tile t's stage while Q3 computes from registers. All LDS is one dynamic
+// array, so hipcc never adds a vmcnt(0) before the ds_reads.
+// ---------------------------------------------------------------------------------------------
+constexpr int BM2 = 256, BN2 = 256;
+constexpr int XT2 = BM2 * BK * 2;   // 32 KiB
+constexpr int WT2 = BN2 * BK * 2;   // 32 KiB
+constexpr int ST2 = XT2 + WT2;      // 64 KiB per stage
+constexpr int C_STRIDE2 = BN2 * 2 + 8;
+constexpr int LDS2 = (2 * ST2 > BM2 * C_STRIDE2) ? 2 * ST2 : BM2 * C_STRIDE2;
+
+template <int EPI, int R, int SPLIT>
+__global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ntm = (p.M + BM2 - 1) / BM2, ntn = (p.N + BN2 - 1) / BN2;
+  int tm, tn;
+  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
+  const int m0 = tm * BM2, n0 = tn * BN2;
+
+  // DMA: wave w moves rows [32w, 32w+32) of the X tile and of the W tile (4 + 4 x 1 KiB)
+  const int lrow = lane >> 3;
+  const int pchunk = lane & 7;
+  const bf16_t* xsrc[4];
+  const bf16_t* wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (wave * 4 + i) * 8 + lrow;
+    xsrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + ((pchunk ^ (row & 7)) * 8);
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.ldw + ((pchunk ^ (row & 7)) * 8);
+  }
+  auto stage = [&](int st, int kt) {
+    char* base = smem + st * ST2;
+    const int koff = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + koff, base + (wave * 4 + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(wsrc[i] + koff, base + XT2 + (wave * 4 + i) * 1024);
+  };
+  auto stage_x = [&](int st, int kt) {
+    char* base = smem + st * ST2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * BK, base + (wave * 4 + i) * 1024);
+  };
+  auto stage_w = [&](int st, int kt) {
+    char* base = smem + st * ST2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(wsrc[i] + kt * BK, base + XT2 + (wave * 4 + i) * 1024);
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  f32x4 acc[8][4];  // [n-tile][m-tile]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15;
+  const int fchunk = lane >> 4;
+  // A (W) fragment offsets per quarter q = 2h + nh, B (X) offsets per k-half h
+  int aoff[4][4], boff[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      boff[h][i] = swz(wm * 64 + i * 16 + frow, h * 4 + fchunk);
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) aoff[2 * h + nh][i] = XT2 + swz(wn * 128 + nh * 64 + i * 16 + frow, h * 4 + fchunk);
+    }
+  const int nk = p.K / BK;
+  stage(0, 0);
+  if (nk > 1) {
+    stage(1, 1);
+    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  s16x8 aE[4], aO[4], b0[4], b1[4];  // A even/odd quarter sets, B per k-half
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    aE[i] = *(const s16x8*)(smem + aoff[0][i]);
+    b0[i] = *(const s16x8*)(smem + boff[0][i]);
+  }
+#define LTX_MFMA_Q(AS, BS, NH)                                                                        \
+  __builtin_amdgcn_sched_barrier(0);                                                                  \
+  __builtin_amdgcn_s_setprio(1);                                                                      \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
+  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
+    acc[(NH) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * 4 + i][j], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);                                                                      \
+  __builtin_amdgcn_sched_barrier(0);
+
+  int cur = 0;
+  bool pend_w = false;  // SPLIT: W half of tile kt+1's DMA still to issue in Q0
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + cur * ST2;
+    // Q0 (h0, n0): prefetch A(Q1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aO[i] = *(const s16x8*)(st + aoff[1][i]);
+    if (SPLIT && pend_w) {
+      stage_w(cur ^ 1, kt + 1);
+      pend_w = false;
+    }
+    LTX_MFMA_Q(aE, b0, 0)
+    // Q1 (h0, n1): prefetch A(Q2), B(h1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      aE[i] = *(const s16x8*)(st + aoff[2][i]);
+      b1[i] = *(const s16x8*)(st + boff[1][i]);
+    }
+    LTX_MFMA_Q(aO, b0, 1)
+    // Q2 (h1, n0): prefetch A(Q3)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aO[i] = *(const s16x8*)(st + aoff[3][i]);
+    LTX_MFMA_Q(aE, b1, 0)
+    // all reads of tile t issued: wait tile t+1, free tile t's stage, DMA tile t+2 into it
+    if (kt + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + 2 < nk) {
+        if (SPLIT) {
+          stage_x(cur, kt + 2);
+          pend_w = true;
+        } else {
+          stage(cur, kt + 2);
+        }
+      }
+      const char* sn = smem + (cur ^ 1) * ST2;
+      // Q3 (h1, n1) of tile t: prefetch A(Q0), B(h0) of tile t+1
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        aE[i] = *(const s16x8*)(sn + aoff[0][i]);
+        b0[i] = *(const s16x8*)(sn + boff[0][i]);
+      }
+    }
+    LTX_MFMA_Q(aO, b1, 1)
+    cur ^= 1;
+  }
+#undef LTX_MFMA_Q
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // epilogue stage 1: bf16(acc + bias) -> LDS image [256 m][256 n]
+  char* cimg = smem;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int nl = wn * 128 + i * 16 + (lane >> 4) * 4;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+      const int gn = n0 + nl;
+      if (gn + 3 < p.N) {
+        const u32x2 bb = *(const u32x2*)(p.bias + gn);
+        b4[0] = bf2f((bf16_t)bb[0]); b4[1] = bf2f((bf16_t)(bb[0] >> 16));
+        b4[2] = bf2f((bf16_t)bb[1]); b4[3] = bf2f((bf16_t)(bb[1] >> 16));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ml = wm * 64 + j * 16 + (lane & 15);
+      u32x2 pk;
+      pk[0] = pack2(acc[i][j][0] + b4[0], acc[i][j][1] + b4[1]);
+      pk[1] = pack2(acc[i][j][2] + b4[2], acc[i][j][3] + b4[3]);
+      *(u32x2*)(cimg + ml * C_STRIDE2 + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+  const int cgrp = tid & 31;
+  for (int rr = tid >> 5; rr < BM2; rr += 512 / 32) {
+    const int m = m0 + rr;
+    const int n = n0 + cgrp * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const u32x2 lo = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16);
+    const u32x2 hi = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16 + 8);
+    bf16_t cv[8] = {(bf16_t)lo[0], (bf16_t)(lo[0] >> 16), (bf16_t)lo[1], (bf16_t)(lo[1] >> 16),
+                    (bf16_t)hi[0], (bf16_t)(hi[0] >> 16), (bf16_t)hi[1], (bf16_t)(hi[1] >> 16)};
+    float o[8];
+    epilogue_row8<EPI, R>(p, m, n, cv, o);
+    u32x4 pk;
+    pk[0] = pack2(o[0], o[1]);
+    pk[1] = pack2(o[2], o[3]);
+    pk[2] = pack2(o[4], o[5]);
+    pk[3] = pack2(o[6], o[7]);
+    *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
+  }
+}
+
+static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
+static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 split DMA burst (default), 1 single burst
+
 template <int EPI, int R = 0>
 static int launch(const GemmParams& p, hipStream_t s) {
-  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(ntm * ntn), dim3(GEMM_THREADS), LDS_BYTES, s, p);
+  if (g_force_small < 0) {
+    const char* e = getenv("LTX_GEMM_SMALL");
+    g_force_small = (e && e[0] == '1') ? 1 : 0;
+  }
+  // large tile once the grid still fills the chip with 256-row tiles
+  const int64_t big_tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + BN2 - 1) / BN2);
+  if (!g_force_small && p.M >= BM2 && big_tiles >= 256) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      attr_set = true;
+    }
+    if (g_variant == 0)  // default: DMA issue split over two quarters
+      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 1>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else
+      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 0>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+  } else {
+    const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(ntm * ntn), dim3(GEMM_THREADS), LDS_BYTES, s, p);
+  }
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
@@ -303,6 +521,11 @@ static int launch_lora(const GemmParams& p, hipStream_t s) {
 }  // namespace ltx
 
 using namespace ltx;
+
+extern "C" int ltx_gemm_set_variant(int variant) {
+  g_variant = variant;
+  return LTX_OK;
+}
 
 extern "C" int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
                                 int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue,
