@@ -157,6 +157,16 @@ int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, voi
                      int64_t ld1, const void* aux2, int64_t ld2, float alpha, int64_t rank,
                      int64_t rows_per_batch, void* stream);
 
+/* Same GEMM with a K extension: C = epilogue(A[M,K].W[N,K]^T + A2[M,K2].W2[N,K2]^T), K2 % 64 == 0
+ * (0 = none). Used to fuse the peft LoRA branch into the K loop with ltx_lora_split_bf16 operands:
+ * y = x.W^T + b + s*(x.A^T).B^T (training.py:50-68) in one f32 accumulation. */
+int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, int64_t ldw, const void* A2,
+                         int64_t lda2, const void* W2, int64_t ldw2, int64_t K2, void* C,
+                         int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue,
+                         const void* bias, const void* aux0, int64_t ld0, const void* aux1,
+                         int64_t ld1, const void* aux2, int64_t ld2, float alpha, int64_t rank,
+                         int64_t rows_per_batch, void* stream);
+
 /* Tuning knob for A/B measurements of GEMM schedules (0: per-tile DMA split over two quarters,
  * the default; 1: one burst). Process-global. */
 int ltx_gemm_set_variant(int variant);
@@ -168,6 +178,12 @@ int ltx_gemm_set_variant(int variant);
 int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk,
                   float* out, int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha,
                   void* stream);
+/* 3-term bf16 split of an f32 [R, r] matrix (element (i,j) at src[i*rs + j*cs], times scale) into
+ * a K-extension operand out [R, K2] (K2 = round_up(3r, 64)): role 0 (activation) rows
+ * [hi|hi|lo|0], role 1 (weight) rows [hi|lo|hi|0]; their dot product reproduces the f32 product
+ * to ~2^-16 relative. */
+int ltx_lora_split_bf16(const float* src, int64_t rs, int64_t cs, float scale, int64_t R,
+                        int64_t r, int role, void* out, int64_t ldo, int64_t K2, void* stream);
 /* dW(n,j) = alpha * sum_m Y[m,n] * U[m,j], stored at dw[n*on + j*oj] (f32, overwritten):
  * lora_B grad (Y = dY, U = u: on = r, oj = 1) and lora_A grad (Y = x, U = w: on = 1, oj = K).
  * Y bf16 [M,N] (ldy), U f32 [M,r] (ldu). Split-M partial sums are combined with f32 atomics. */

@@ -343,3 +343,29 @@ def test_mse_and_adamw():
             assert rel(mine, pt.detach()) < 1e-6
         else:
             assert ulps_bad(mine, pt.detach(), 1) < 1e-3
+
+
+def test_gemm_k_extension_lora_fusion():
+    """LoRA fused into the K loop: [x | split(u)] . [W | split(s*B)]^T == x.W^T + b + s*u.B^T
+    with u = x.A^T in f32 (peft), for both tile kernels and for the dgrad orientation."""
+    from ltx_amd import ops
+    for M, N, K in ((512, 256, 256), (14336 // 2, 2048, 2048)):
+        r, s = 16, 0.5
+        x, w, b = g(M, K, seed=21), g(N, K, seed=22, scale=K ** -0.5), g(N, seed=23)
+        A = torch.randn(r, K, device=DEV) / K ** 0.5
+        Bm = torch.randn(N, r, device=DEV) * 0.1
+        u = ops.lora_down(x, A)
+        out = ops.gemm(x, w, bias=b, ext=(ops.lora_split(u, "act"), ops.lora_split(Bm, "weight", s)))
+        ref = x.float() @ w.float().t() + b.float() + s * (u @ Bm.t())
+        assert rel(out, ref) < 1e-2
+        assert ulps_bad(out, ref.to(torch.bfloat16), 2) < 2e-3
+        # dgrad orientation: dy . W + w . A with w = s * dy . B  (A^T split as the weight side)
+        dy = g(M, N, seed=24)
+        wd = ops.lora_down(dy, Bm, alpha=s, transposed=True)
+        wT = ops.transpose(w)
+        dx = ops.gemm(dy, wT, ext=(ops.lora_split(wd, "act"), ops.lora_split(A, "weight", transposed=True)))
+        ref = dy.float() @ w.float() + wd @ A
+        assert rel(dx, ref) < 1e-2
+        # the 3-term split reproduces the f32 rank-r product to ~1e-5
+        sa, sw = ops.lora_split(u, "act").float(), ops.lora_split(Bm, "weight", s).float()
+        assert rel(sa @ sw.t(), s * (u @ Bm.t())) < 1e-4

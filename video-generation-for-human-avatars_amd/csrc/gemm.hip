@@ -44,6 +44,11 @@ struct GemmParams {
   float alpha;
   int rank;
   int rows_per_batch;
+  // optional K extension (LoRA fused into the K loop): C += A2[M,K2] . W2[N,K2]^T
+  const bf16_t* A2;
+  const bf16_t* W2;
+  int64_t lda2, ldw2;
+  int K2;
 };
 
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
@@ -185,13 +190,26 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
     asrc[i] = p.A + (int64_t)am * p.lda + lchunk * 8;
     wsrc[i] = p.W + (int64_t)wn * p.ldw + lchunk * 8;
   }
+  const int nk_main = p.K / BK;
   auto stage = [&](int buf, int kt) {
     char* base = smem + buf * STAGE_BYTES;
-    const int koff = kt * BK;
+    if (kt < nk_main) {
+      const int koff = kt * BK;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      glds16(asrc[i] + koff, base + (wave * 4 + i) * 1024);
-      glds16(wsrc[i] + koff, base + TILE_BYTES + (wave * 4 + i) * 1024);
+      for (int i = 0; i < 4; ++i) {
+        glds16(asrc[i] + koff, base + (wave * 4 + i) * 1024);
+        glds16(wsrc[i] + koff, base + TILE_BYTES + (wave * 4 + i) * 1024);
+      }
+    } else {  // K extension tile(s)
+      const int koff = (kt - nk_main) * BK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = (wave * 4 + i) * 8 + lrow;
+        const int lchunk = pchunk ^ (row & 7);
+        glds16(p.A2 + (int64_t)min(m0 + row, p.M - 1) * p.lda2 + koff + lchunk * 8, base + (wave * 4 + i) * 1024);
+        glds16(p.W2 + (int64_t)min(n0 + row, p.N - 1) * p.ldw2 + koff + lchunk * 8,
+               base + TILE_BYTES + (wave * 4 + i) * 1024);
+      }
     }
   };
 
@@ -203,7 +221,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / BK;
+  const int nk = nk_main + p.K2 / BK;
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -325,23 +343,31 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
     xsrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + ((pchunk ^ (row & 7)) * 8);
     wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.ldw + ((pchunk ^ (row & 7)) * 8);
   }
-  auto stage = [&](int st, int kt) {
-    char* base = smem + st * ST2;
-    const int koff = kt * BK;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + koff, base + (wave * 4 + i) * 1024);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(wsrc[i] + koff, base + XT2 + (wave * 4 + i) * 1024);
+  const int nk_main = p.K / BK;
+  // K-extension tiles (LoRA fused into the K loop) read A2/W2 instead of A/W
+  auto xptr = [&](int i, int kt) -> const bf16_t* {
+    if (kt < nk_main) return xsrc[i] + kt * BK;
+    const int row = (wave * 4 + i) * 8 + lrow;
+    return p.A2 + (int64_t)min(m0 + row, p.M - 1) * p.lda2 + (kt - nk_main) * BK + ((pchunk ^ (row & 7)) * 8);
+  };
+  auto wptr = [&](int i, int kt) -> const bf16_t* {
+    if (kt < nk_main) return wsrc[i] + kt * BK;
+    const int row = (wave * 4 + i) * 8 + lrow;
+    return p.W2 + (int64_t)min(n0 + row, p.N - 1) * p.ldw2 + (kt - nk_main) * BK + ((pchunk ^ (row & 7)) * 8);
   };
   auto stage_x = [&](int st, int kt) {
     char* base = smem + st * ST2;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(xsrc[i] + kt * BK, base + (wave * 4 + i) * 1024);
+    for (int i = 0; i < 4; ++i) glds16(xptr(i, kt), base + (wave * 4 + i) * 1024);
   };
   auto stage_w = [&](int st, int kt) {
     char* base = smem + st * ST2;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(wsrc[i] + kt * BK, base + XT2 + (wave * 4 + i) * 1024);
+    for (int i = 0; i < 4; ++i) glds16(wptr(i, kt), base + XT2 + (wave * 4 + i) * 1024);
+  };
+  auto stage = [&](int st, int kt) {
+    stage_x(st, kt);
+    stage_w(st, kt);
   };
 
   const int wm = wave >> 1, wn = wave & 1;
@@ -363,7 +389,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh) aoff[2 * h + nh][i] = XT2 + swz(wn * 128 + nh * 64 + i * 16 + frow, h * 4 + fchunk);
     }
-  const int nk = p.K / BK;
+  const int nk = nk_main + p.K2 / BK;
   stage(0, 0);
   if (nk > 1) {
     stage(1, 1);
@@ -527,11 +553,31 @@ extern "C" int ltx_gemm_set_variant(int variant) {
   return LTX_OK;
 }
 
+extern "C" int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, int64_t ldw,
+                                    const void* A2, int64_t lda2, const void* W2, int64_t ldw2,
+                                    int64_t K2, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                    int epilogue, const void* bias, const void* aux0, int64_t ld0,
+                                    const void* aux1, int64_t ld1, const void* aux2, int64_t ld2,
+                                    float alpha, int64_t rank, int64_t rows_per_batch, void* stream);
+
 extern "C" int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
                                 int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue,
                                 const void* bias, const void* aux0, int64_t ld0, const void* aux1,
                                 int64_t ld1, const void* aux2, int64_t ld2, float alpha,
                                 int64_t rank, int64_t rows_per_batch, void* stream) {
+  return ltx_gemm_bf16_nt_ext(A, lda, W, ldw, nullptr, 0, nullptr, 0, 0, C, ldc, M, N, K, epilogue, bias, aux0,
+                              ld0, aux1, ld1, aux2, ld2, alpha, rank, rows_per_batch, stream);
+}
+
+extern "C" int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, int64_t ldw,
+                                    const void* A2, int64_t lda2, const void* W2, int64_t ldw2,
+                                    int64_t K2, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                    int epilogue, const void* bias, const void* aux0, int64_t ld0,
+                                    const void* aux1, int64_t ld1, const void* aux2, int64_t ld2,
+                                    float alpha, int64_t rank, int64_t rows_per_batch, void* stream) {
+  LTX_CHECK_ARG(K2 == 0 || (A2 && W2 && K2 % BK == 0 && lda2 >= K2 && ldw2 >= K2 && lda2 % 8 == 0 &&
+                            ldw2 % 8 == 0 && ((uintptr_t)A2 | (uintptr_t)W2) % 16 == 0),
+                "gemm: K extension needs 16-B aligned A2/W2 with K2 % 64 == 0");
   LTX_CHECK_ARG(A && W && C, "gemm: null operand");
   LTX_CHECK_ARG(M > 0 && N > 0 && K > 0, "gemm: empty shape");
   LTX_CHECK_ARG(K % BK == 0, "gemm: K must be a multiple of 64");
@@ -549,6 +595,7 @@ extern "C" int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64
   p.bias = (const bf16_t*)bias;
   p.aux0 = aux0; p.ld0 = ld0; p.aux1 = aux1; p.ld1 = ld1; p.aux2 = aux2; p.ld2 = ld2;
   p.alpha = alpha; p.rank = (int)rank; p.rows_per_batch = (int)(rows_per_batch > 0 ? rows_per_batch : M);
+  p.A2 = (const bf16_t*)A2; p.W2 = (const bf16_t*)W2; p.lda2 = lda2; p.ldw2 = ldw2; p.K2 = (int)K2;
   hipStream_t s = (hipStream_t)stream;
   switch (epilogue) {
     case LTX_EPI_STORE: return launch<LTX_EPI_STORE>(p, s);

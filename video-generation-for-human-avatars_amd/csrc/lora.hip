@@ -144,9 +144,45 @@ __global__ __launch_bounds__(256) void lora_wgrad_kernel(const bf16_t* __restric
     }
 }
 
+// 3-term bf16 split of an f32 [R, r] operand for the K-extension LoRA fusion: with
+// v = hi + lo (hi = bf16(v), lo = bf16(v - hi)), the activation row is [hi | hi | lo | 0..] and
+// the weight row [hi | lo | hi | 0..], so their dot product is a.hi*w.hi + a.hi*w.lo + a.lo*w.hi
+// (the lo*lo term, ~2^-16 relative, is the only thing dropped).
+__global__ void lora_split_kernel(const float* __restrict__ src, int64_t rs, int64_t cs, float scale, int R,
+                                  int r, int role, bf16_t* __restrict__ out, int64_t ldo, int K2) {
+  const int64_t total = (int64_t)R * K2;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / K2), c = (int)(i % K2);
+    const int seg = c / r, j = c % r;
+    float o = 0.f;
+    if (seg < 3) {
+      const float v = src[(int64_t)row * rs + (int64_t)j * cs] * scale;
+      const float hi = rbf(v);
+      const float lo = rbf(v - hi);
+      // activation: hi, hi, lo ; weight: hi, lo, hi
+      o = (role == 0) ? (seg < 2 ? hi : lo) : (seg == 1 ? lo : hi);
+    }
+    out[(int64_t)row * ldo + c] = f2bf(o);
+  }
+}
+
 }  // namespace ltx
 
 using namespace ltx;
+
+extern "C" int ltx_lora_split_bf16(const float* src, int64_t rs, int64_t cs, float scale, int64_t R, int64_t r,
+                                   int role, void* out, int64_t ldo, int64_t K2, void* stream) {
+  LTX_CHECK_ARG(src && out && R > 0 && r > 0 && (role == 0 || role == 1), "lora_split: bad args");
+  LTX_CHECK_ARG(K2 >= 3 * r && K2 % 64 == 0 && ldo >= K2, "lora_split: K2 must be >= 3r and a multiple of 64");
+  const int64_t total = R * K2;
+  int64_t g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(lora_split_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, src, rs, cs, scale,
+                     (int)R, (int)r, role, (bf16_t*)out, ldo, (int)K2);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
 
 extern "C" int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk, float* out,
                              int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha, void* stream) {

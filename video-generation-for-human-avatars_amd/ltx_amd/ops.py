@@ -297,8 +297,9 @@ def set_launch_timer(timer):
 
 
 def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2=None,
-         alpha=1.0, rank=0, rows_per_batch=0):
-    """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias)); see LTX_EPI_* in ltx_hip.h."""
+         alpha=1.0, rank=0, rows_per_batch=0, ext=None):
+    """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias) [+ a2 . w2^T]); see LTX_EPI_* in ltx_hip.h.
+    ext = (a2 [M,K2], w2 [N,K2]) appends K-extension tiles (the fused LoRA branch)."""
     _need(a, BF16, "gemm a")
     _need(w, BF16, "gemm w")
     M, K = a.shape
@@ -313,9 +314,12 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
     if timed:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    call("ltx_gemm_bf16_nt", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(out), _rows(out, "out"),
-         M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1), ld1, _p(aux2), ld2,
-         float(alpha), rank, rows_per_batch, _s())
+    a2, w2 = ext if ext is not None else (None, None)
+    K2 = a2.shape[1] if a2 is not None else 0
+    call("ltx_gemm_bf16_nt_ext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
+         _rows(a2, "a2") if a2 is not None else 0, _p(w2), _rows(w2, "w2") if w2 is not None else 0,
+         K2, _p(out), _rows(out, "out"), M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1),
+         ld1, _p(aux2), ld2, float(alpha), rank, rows_per_batch, _s())
     if timed:
         ev1.record()
         _timer.pairs.append((ev0, ev1))
@@ -335,6 +339,26 @@ def lora_down(x, wr, alpha=1.0, transposed=False, out=None):
     out = torch.empty(M, r, dtype=F32, device=x.device) if out is None else out
     call("ltx_lora_down", _p(x), _rows(x, "x"), _p(wr), wj, wk, _p(out), _rows(out, "out"), M, K, r,
          float(alpha), _s())
+    return out
+
+
+def lora_k2(r):
+    return (3 * r + 63) // 64 * 64
+
+
+def lora_split(src, role, scale=1.0, transposed=False, out=None):
+    """K-extension operand from an f32 [R, r] matrix (transposed=True reads src as [r, R], e.g.
+    lora_A [r, K] used as A^T): role 'act' -> rows [hi|hi|lo|0], 'weight' -> [hi|lo|hi|0]."""
+    if transposed:
+        r, R = src.shape
+        rs, cs = src.stride(1), src.stride(0)
+    else:
+        R, r = src.shape
+        rs, cs = src.stride(0), src.stride(1)
+    K2 = lora_k2(r)
+    out = torch.empty(R, K2, dtype=BF16, device=src.device) if out is None else out
+    call("ltx_lora_split_bf16", _p(src), rs, cs, float(scale), R, r, 0 if role == "act" else 1,
+         _p(out), _rows(out, "out"), K2, _s())
     return out
 
 

@@ -33,8 +33,9 @@ class HipAttnProcessor:
             if lora is None:
                 return ops.gemm(inp, w, bias=b)
             u = ops.lora_down(inp, lora.lora_A["default"].weight)
-            return ops.gemm(inp, w, bias=b, epilogue="lora", aux1=u,
-                            aux2=lora.lora_B["default"].weight, alpha=lora.scaling, rank=lora.r)
+            return ops.gemm(inp, w, bias=b, ext=(ops.lora_split(u, "act"),
+                                                 ops.lora_split(lora.lora_B["default"].weight,
+                                                                "weight", lora.scaling)))
 
         q_raw = proj(attn.to_q, x)
         k_raw = proj(attn.to_k, e)

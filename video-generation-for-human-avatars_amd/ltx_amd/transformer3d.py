@@ -348,13 +348,17 @@ class _BlockFn(torch.autograd.Function):
         wv, bv, _ = _lin(a2.to_v)
         wo, bo, _ = _lin(a2.to_out[0])
         if has_lora:
+            # peft LoRA fused into the K loop: [x | split(x.A^T)] . [W | split(s*B)]^T
             Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo = lora_ab
             u_q = ops.lora_down(h1, Aq)
-            q2raw = ops.gemm(h1, wq, bias=bq, epilogue="lora", aux1=u_q, aux2=Bq, alpha=s, rank=r)
+            q2raw = ops.gemm(h1, wq, bias=bq,
+                             ext=(ops.lora_split(u_q, "act"), ops.lora_split(Bq, "weight", s)))
             u_k = ops.lora_down(enc2, Ak)
-            k2raw = ops.gemm(enc2, wk, bias=bk, epilogue="lora", aux1=u_k, aux2=Bk, alpha=s, rank=r)
+            k2raw = ops.gemm(enc2, wk, bias=bk,
+                             ext=(ops.lora_split(u_k, "act"), ops.lora_split(Bk, "weight", s)))
             u_v = ops.lora_down(enc2, Av)
-            v2 = ops.gemm(enc2, wv, bias=bv, epilogue="lora", aux1=u_v, aux2=Bv, alpha=s, rank=r)
+            v2 = ops.gemm(enc2, wv, bias=bv,
+                          ext=(ops.lora_split(u_v, "act"), ops.lora_split(Bv, "weight", s)))
         else:
             u_q = u_k = u_v = None
             q2raw = ops.gemm(h1, wq, bias=bq)
@@ -365,8 +369,8 @@ class _BlockFn(torch.autograd.Function):
         o2, lse2 = ops.attn_fwd(q2, k2, v2, B, H, d, a2.scale, key_bias=sh.enc_bias)
         if has_lora:
             u_o = ops.lora_down(o2, Ao)
-            h2 = ops.gemm(o2, wo, bias=bo, epilogue="lora_residual", aux0=h1, aux1=u_o, aux2=Bo,
-                          alpha=s, rank=r)
+            h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1,
+                          ext=(ops.lora_split(u_o, "act"), ops.lora_split(Bo, "weight", s)))
         else:
             u_o = None
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1)
@@ -418,8 +422,8 @@ class _BlockFn(torch.autograd.Function):
             dBo = ops.lora_wgrad(dh2, u_o, alpha=s)
             w_o = ops.lora_down(dh2, Bo, alpha=s, transposed=True)
             dAo = ops.lora_wgrad(o2, w_o, transpose_out=True)
-            do2 = ops.gemm(dh2, W["o2_wT"], epilogue="lora_dgrad_accum", aux1=w_o, aux2=Ao,
-                           rank=r)
+            do2 = ops.gemm(dh2, W["o2_wT"], ext=(ops.lora_split(w_o, "act"),
+                                                 ops.lora_split(Ao, "weight", transposed=True)))
         else:
             do2 = ops.gemm(dh2, W["o2_wT"])
         dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
@@ -432,18 +436,18 @@ class _BlockFn(torch.autograd.Function):
             dBq = ops.lora_wgrad(dq2raw, u_q, alpha=s)
             w_q = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True)
             dAq = ops.lora_wgrad(h1, w_q, transpose_out=True)
-            dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="lora_dgrad_accum", aux0=dh2, aux1=w_q,
-                           aux2=Aq, rank=r)
+            dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
+                           ext=(ops.lora_split(w_q, "act"), ops.lora_split(Aq, "weight", transposed=True)))
             dBk = ops.lora_wgrad(dk2raw, u_k, alpha=s)
             w_k = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True)
             dAk = ops.lora_wgrad(enc2, w_k, transpose_out=True)
-            denc = ops.gemm(dk2raw, W["k2_wT"], epilogue="lora_dgrad_accum", aux1=w_k, aux2=Ak,
-                            rank=r)
+            denc = ops.gemm(dk2raw, W["k2_wT"], ext=(ops.lora_split(w_k, "act"),
+                                                     ops.lora_split(Ak, "weight", transposed=True)))
             dBv = ops.lora_wgrad(dv2, u_v, alpha=s)
             w_v = ops.lora_down(dv2, Bv, alpha=s, transposed=True)
             dAv = ops.lora_wgrad(enc2, w_v, transpose_out=True)
-            ops.gemm(dv2, W["v2_wT"], epilogue="lora_dgrad_accum", aux0=denc, aux1=w_v, aux2=Av,
-                     rank=r, out=denc)
+            ops.gemm(dv2, W["v2_wT"], epilogue="accum", aux0=denc, out=denc,
+                     ext=(ops.lora_split(w_v, "act"), ops.lora_split(Av, "weight", transposed=True)))
             grads_lora = [dAq, dBq, dAk, dBk, dAv, dBv, dAo, dBo]
         else:
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2)
