@@ -133,16 +133,23 @@ __device__ __forceinline__ void key_bias_tile(float* kb, const AttnParams& p, in
 }
 
 // =============================================================================================
-// forward (MODE 0) and dQ (MODE 1): queries on lanes, keys in registers
+// forward (MODE 0) and dQ (MODE 1): queries on lanes, keys in registers.
+// BIAS: keys carry an additive term (encoder mask bias, or -inf past a ragged Nk); without it
+// (self-attention, Nk % 64 == 0) the per-key LDS reads and adds disappear.
+// VALU diet (the forward is VALU-bound at head dim 64): the running max is taken on the raw
+// scores (scale > 0), each probability is one v_fma + one v_exp_f32, and the O rescale is skipped
+// whenever no lane's max grew (exact: alpha would be 1).
 // =============================================================================================
-template <int HD, int MODE>
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int HD, int MODE, bool BIAS>
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams p) {
   constexpr int KT = 64;                 // keys per tile
   constexpr int KS = HD / 16;            // 16-deep k-steps over the head dim
   constexpr int DS = HD / 32;            // 32-wide d subtiles
   constexpr int TILE = KT * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
-  __shared__ float kb[KT];
+  __shared__ __attribute__((aligned(16))) float kb[KT];
   char* ktile = smem;
   char* vtile = smem + TILE;
 
@@ -156,31 +163,29 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
   const bf16_t* kbase = p.k + (int64_t)b * p.Nk * p.ldk + hh * HD;
   const bf16_t* vbase = p.v + (int64_t)b * p.Nk * p.ldv + hh * HD;
 
-  // Q^T fragments (B operand): lane holds Q[qc][ks*16 + 8h .. +7]
   s16x8 qf[KS];
   {
     const bf16_t* qr = p.q + ((int64_t)b * p.Nq + qc) * p.ldq + hh * HD;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[ks] = *(const s16x8*)(qr + ks * 16 + 8 * h);
   }
-  // dO^T fragments (dQ mode), same layout; lse / delta per lane (one query)
   s16x8 of[KS];
-  float lse2 = 0.f, dlt = 0.f;
+  float nlse = 0.f, dlt = 0.f;  // -lse2, delta (dQ mode)
   if constexpr (MODE == 1) {
     const bf16_t* dr = p.dout + ((int64_t)b * p.Nq + qc) * p.lddo + hh * HD;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) of[ks] = *(const s16x8*)(dr + ks * 16 + 8 * h);
     const int64_t si = ((int64_t)b * p.H + hh) * p.Nq + qc;
-    lse2 = p.lse[si];
+    nlse = -p.lse[si];
     dlt = p.delta[si];
   }
 
-  f32x16 acc[DS];  // O^T (fwd) or dQ^T (dq): rows = d, lanes = queries
+  f32x16 acc[DS];
 #pragma unroll
   for (int d = 0; d < DS; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
-  float m_run = -1e30f, l_run = 0.f;
+  float m_run = -1e30f, l_run = 0.f;  // m_run in scaled log2 units
 
   TileStage<HD, KT> ks_, vs_;
   const int ntiles = (p.Nk + KT - 1) / KT;
@@ -188,7 +193,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
   vs_.load(vbase, p.ldv, 0, p.Nk, tid);
   ks_.store(ktile, tid);
   vs_.store(vtile, tid);
-  key_bias_tile(kb, p, b, 0, KT, tid);
+  if (BIAS) key_bias_tile(kb, p, b, 0, KT, tid);
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
@@ -197,7 +202,6 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
       ks_.load(kbase, p.ldk, key0 + KT, p.Nk, tid);
       vs_.load(vbase, p.ldv, key0 + KT, p.Nk, tid);
     }
-    // S^T[key][q] for the two 32-key halves of the tile
     f32x16 s[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -208,33 +212,49 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
     }
     if constexpr (MODE == 0) {
       float mt = -1e30f;
+      if constexpr (BIAS) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float x = s[u][r] * c2 + kb[u * 32 + acc_row(r, h)];
-          s[u][r] = x;
-          mt = fmaxf(mt, x);
-        }
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 kb4 = *(const f32x4*)&kb[u * 32 + 8 * g + 4 * h];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float x = fmaf(s[u][4 * g + i], c2, kb4[i]);
+              s[u][4 * g + i] = x;
+              mt = fmaxf(mt, x);
+            }
+          }
+      } else {
+        float mr = -3.0e38f;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mr = fmaxf(mr, s[u][r]);
+        mt = mr * c2;
+      }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
       const float m_new = fmaxf(m_run, mt);
-      const float alpha = exp2f(m_run - m_new);
-      m_run = m_new;
+      if (__any(m_new > m_run)) {
+        const float alpha = fast_exp2(m_run - m_new);
+        l_run *= alpha;
+#pragma unroll
+        for (int d = 0; d < DS; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[d][r] *= alpha;
+        m_run = m_new;
+      }
+      const float nm = -m_run;
       float ls = 0.f;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float e = exp2f(s[u][r] - m_new);
+          const float e = BIAS ? fast_exp2(s[u][r] + nm) : fast_exp2(fmaf(s[u][r], c2, nm));
           s[u][r] = e;
           ls += e;
         }
-      l_run = l_run * alpha + ls;
-#pragma unroll
-      for (int d = 0; d < DS; ++d)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[d][r] *= alpha;
-      // O^T[d][q] += V^T[d][key] . P^T[key][q]
+      l_run += ls;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -244,7 +264,6 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
           for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vtile, u * 32, ss, d * 32, lane), pb, acc[d]);
         }
     } else {
-      // P^T = 2^(s*c2 + kb - lse2); dP^T = V . dO^T; dS^T = P^T (dP^T - delta)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 dp;
@@ -252,12 +271,24 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
         for (int r = 0; r < 16; ++r) dp[r] = 0.f;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) dp = mfma32(row_frag<HD>(vtile, u * 32, ks, lane), of[ks], dp);
+        if constexpr (BIAS) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pr = exp2f(s[u][r] * c2 + kb[u * 32 + acc_row(r, h)] - lse2);
-          s[u][r] = pr * (dp[r] - dlt);
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 kb4 = *(const f32x4*)&kb[u * 32 + 8 * g + 4 * h];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = 4 * g + i;
+              const float pr = fast_exp2(fmaf(s[u][r], c2, kb4[i] + nlse));
+              s[u][r] = pr * (dp[r] - dlt);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pr = fast_exp2(fmaf(s[u][r], c2, nlse));
+            s[u][r] = pr * (dp[r] - dlt);
+          }
         }
-        // dQ^T[d][q] += K^T[d][key] . dS^T[key][q]
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
           const s16x8 db = acc_frag(s[u], ss);
@@ -270,7 +301,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
       __syncthreads();
       ks_.store(ktile, tid);
       vs_.store(vtile, tid);
-      key_bias_tile(kb, p, b, key0 + KT, KT, tid);
+      if (BIAS) key_bias_tile(kb, p, b, key0 + KT, KT, tid);
       __syncthreads();
     }
   }
@@ -317,11 +348,12 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
 }
 
 // =============================================================================================
-// dK / dV: keys on lanes, queries in registers; workgroup = 4 waves x 32 keys
+// dK / dV: keys on lanes, queries in registers; workgroup = 4 waves x 32 keys. Query tiles of 64
+// (two 32-row halves) between barrier pairs, so each wave runs 32 MFMAs per LDS refill.
 // =============================================================================================
-template <int HD>
+template <int HD, bool BIAS>
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnParams p) {
-  constexpr int QT = 32;
+  constexpr int QT = 64;
   constexpr int KS = HD / 16;
   constexpr int DS = HD / 32;
   constexpr int TILE = QT * HD * 2;
@@ -336,10 +368,12 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   const int key = blockIdx.x * 128 + wave * 32 + (lane & 31);
   const int kc = min(key, p.Nk - 1);
   const float c2 = p.scale * LOG2E;
-  float kbias = -INFINITY;
-  if (key < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.Nk + key] * LOG2E : 0.f;
+  float kbias = 0.f;
+  if (BIAS) {
+    kbias = -INFINITY;
+    if (key < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.Nk + key] * LOG2E : 0.f;
+  }
 
-  // K^T / V^T fragments (B operands): lane holds K[kc][ks*16 + 8h .. +7]
   s16x8 kf[KS], vf[KS];
   {
     const bf16_t* kr = p.k + ((int64_t)b * p.Nk + kc) * p.ldk + hh * HD;
@@ -350,7 +384,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
       vf[ks] = *(const s16x8*)(vr + ks * 16 + 8 * h);
     }
   }
-  f32x16 dka[DS], dva[DS];  // dK^T / dV^T: rows = d, lanes = keys
+  f32x16 dka[DS], dva[DS];
 #pragma unroll
   for (int d = 0; d < DS; ++d)
 #pragma unroll
@@ -368,7 +402,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   auto stage_stats = [&](int qb) {
     if (tid < QT) {
       const int qq = qb + tid;
-      st_lse[tid] = qq < p.Nq ? lbase[qq] : INFINITY;  // rows past Nq contribute P = 0
+      st_lse[tid] = qq < p.Nq ? -lbase[qq] : -INFINITY;  // -lse2 (rows past Nq: P = 0)
       st_dl[tid] = qq < p.Nq ? dbase[qq] : 0.f;
     }
   };
@@ -385,34 +419,40 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
       qs_.load(qbase, p.ldq, qb + QT, p.Nq, tid);
       os_.load(obase, p.lddo, qb + QT, p.Nq, tid);
     }
-    f32x16 s, dp;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s[r] = 0.f;
-      dp[r] = 0.f;
-    }
-    // S[q][key] = Q.K^T ; dP[q][key] = dO.V^T
+    for (int u = 0; u < 2; ++u) {
+      f32x16 s, dp;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      s = mfma32(row_frag<HD>(qtile, 0, ks, lane), kf[ks], s);
-      dp = mfma32(row_frag<HD>(otile, 0, ks, lane), vf[ks], dp);
-    }
+      for (int r = 0; r < 16; ++r) {
+        s[r] = 0.f;
+        dp[r] = 0.f;
+      }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qr = acc_row(r, h);
-      const float pr = exp2f(s[r] * c2 + kbias - st_lse[qr]);
-      s[r] = pr;                           // P
-      dp[r] = pr * (dp[r] - st_dl[qr]);    // dS
-    }
-    // dV^T[d][key] += dO^T[d][q] . P[q][key] ; dK^T[d][key] += Q^T[d][q] . dS[q][key]
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma32(row_frag<HD>(qtile, u * 32, ks, lane), kf[ks], s);
+        dp = mfma32(row_frag<HD>(otile, u * 32, ks, lane), vf[ks], dp);
+      }
 #pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const s16x8 pb = acc_frag(s, ss);
-      const s16x8 sb = acc_frag(dp, ss);
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 nl4 = *(const f32x4*)&st_lse[u * 32 + 8 * g + 4 * h];
+        const f32x4 dl4 = *(const f32x4*)&st_dl[u * 32 + 8 * g + 4 * h];
 #pragma unroll
-      for (int d = 0; d < DS; ++d) {
-        dva[d] = mfma32(tr_frag<HD>(otile, 0, ss, d * 32, lane), pb, dva[d]);
-        dka[d] = mfma32(tr_frag<HD>(qtile, 0, ss, d * 32, lane), sb, dka[d]);
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i;
+          const float pr = fast_exp2(fmaf(s[r], c2, BIAS ? kbias + nl4[i] : nl4[i]));
+          s[r] = pr;
+          dp[r] = pr * (dp[r] - dl4[i]);
+        }
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const s16x8 pb = acc_frag(s, ss);
+        const s16x8 sb = acc_frag(dp, ss);
+#pragma unroll
+        for (int d = 0; d < DS; ++d) {
+          dva[d] = mfma32(tr_frag<HD>(otile, u * 32, ss, d * 32, lane), pb, dva[d]);
+          dka[d] = mfma32(tr_frag<HD>(qtile, u * 32, ss, d * 32, lane), sb, dka[d]);
+        }
       }
     }
     if (t + 1 < ntiles) {
@@ -466,10 +506,15 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const AttnParams p, flo
   }
 }
 
+static inline bool needs_bias(const AttnParams& p) { return p.key_bias != nullptr || (p.Nk % 64) != 0; }
+
 template <int HD>
 static int launch_fwd(const AttnParams& p, hipStream_t s) {
   dim3 grid((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
-  hipLaunchKernelGGL((attn_q_kernel<HD, 0>), grid, dim3(ATT_THREADS), 0, s, p);
+  if (needs_bias(p))
+    hipLaunchKernelGGL((attn_q_kernel<HD, 0, true>), grid, dim3(ATT_THREADS), 0, s, p);
+  else
+    hipLaunchKernelGGL((attn_q_kernel<HD, 0, false>), grid, dim3(ATT_THREADS), 0, s, p);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
@@ -481,10 +526,16 @@ static int launch_bwd(AttnParams p, float* delta, hipStream_t s) {
   LTX_LAUNCH_CHECK();
   p.delta = delta;
   dim3 gq((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
-  hipLaunchKernelGGL((attn_q_kernel<HD, 1>), gq, dim3(ATT_THREADS), 0, s, p);
-  LTX_LAUNCH_CHECK();
   dim3 gk((unsigned)((p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
-  hipLaunchKernelGGL(attn_dkdv_kernel<HD>, gk, dim3(ATT_THREADS), 0, s, p);
+  if (needs_bias(p)) {
+    hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
+    LTX_LAUNCH_CHECK();
+    hipLaunchKernelGGL((attn_dkdv_kernel<HD, true>), gk, dim3(ATT_THREADS), 0, s, p);
+  } else {
+    hipLaunchKernelGGL((attn_q_kernel<HD, 1, false>), gq, dim3(ATT_THREADS), 0, s, p);
+    LTX_LAUNCH_CHECK();
+    hipLaunchKernelGGL((attn_dkdv_kernel<HD, false>), gk, dim3(ATT_THREADS), 0, s, p);
+  }
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
