@@ -1,0 +1,279 @@
+"""CPU tests of the host-side mirror (no GPU, no kernel launches): config loading, scheduler
+timestep shifts, t sampling, PEFT-compatible module/parameter naming, checkpoint loading and LoRA
+merge, and the data-parallel gradient all-reduce over gloo with world_size 2.
+
+Parity anchors: tests/golden/train_config.json (the reference's own load_train_config_from_yaml on
+configs/train-avatars.yaml), tests/golden/rf_sched.* (reference RectifiedFlowScheduler), the
+tiny_train_step golden's parameter/grad key sets (reference model wrapped by peft)."""
+import json
+import math
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+from safetensors.torch import load_file, save_file
+
+from params import canonical_name
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF_YAML = "/root/reference/configs/train-avatars.yaml"
+
+TINY = None
+
+
+def _tiny():
+    global TINY
+    if TINY is None:
+        with open(os.path.join(GOLD, "tiny_train_step.json")) as f:
+            meta = json.load(f)
+        TINY = (load_file(os.path.join(GOLD, "tiny_train_step.safetensors")), meta)
+    return TINY
+
+
+# ---------------------------------------------------------------------------------- config
+def test_train_config_golden_fields():
+    """TrainConfig keeps every field name of ltx_video/config.py:6-64 with the golden's values
+    type-compatible (the golden is the reference parse of train-avatars.yaml)."""
+    from dataclasses import fields
+
+    from ltx_amd.config import TrainConfig
+    with open(os.path.join(GOLD, "train_config.json")) as f:
+        gold = json.load(f)
+    names = {f.name for f in fields(TrainConfig)}
+    assert names == set(gold), names ^ set(gold)
+    cfg = TrainConfig(**gold)
+    assert cfg.gradient_accumulation_steps == 16 and cfg.lora_rank == 32
+
+
+@pytest.mark.skipif(not os.path.exists(REF_YAML), reason="reference tree not present")
+def test_train_config_matches_reference_parse():
+    from dataclasses import asdict
+
+    from ltx_amd.config import load_train_config_from_yaml
+    with open(os.path.join(GOLD, "train_config.json")) as f:
+        gold = json.load(f)
+    assert asdict(load_train_config_from_yaml(REF_YAML)) == gold
+
+
+def test_train_config_quirks(tmp_path):
+    """config.py:109-154: sampler aliases, falsy rf floats read as None, checkpoint required."""
+    from ltx_amd.config import load_train_config_from_yaml
+    p = tmp_path / "c.yaml"
+    p.write_text("checkpoint_path: x.safetensors\nsampler: LinearQuadratic\nprecision: bf16\n"
+                 "train:\n  rf_log_normal_mu: 0\n  rf_log_normal_sigma: 1.5\n  batch_size: 4\n"
+                 "  rf_shifting: SD3\n")
+    c = load_train_config_from_yaml(str(p))
+    assert c.rf_sampler == "LinearQuadratic"
+    assert c.rf_log_normal_mu is None and c.rf_log_normal_sigma == 1.5
+    assert c.batch_size == 4 and c.num_epochs is None and c.precision == "bf16"
+    assert c.rf_shifting == "SD3" and c.lora_rank == 8
+    p.write_text("train: {}\n")
+    with pytest.raises(ValueError):
+        load_train_config_from_yaml(str(p))
+
+
+# ------------------------------------------------------------------------------- scheduler
+def test_scheduler_shifts_match_reference():
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    d = load_file(os.path.join(GOLD, "rf_sched.safetensors"))
+    t = d["t"]
+    none = RectifiedFlowScheduler(num_train_timesteps=1000, shifting=None, base_resolution=1024)
+    assert torch.equal(none.shift_timesteps(d["x0"].shape, t), d["shift_none"])
+    sd3 = RectifiedFlowScheduler(shifting="SD3", target_shift_terminal=0.1)
+    assert torch.allclose(sd3.shift_timesteps(torch.Size([3, 4096, 128]), t), d["shift_sd3"],
+                          rtol=1e-6, atol=1e-7)
+    sdf = RectifiedFlowScheduler(shifting="SimpleDiffusion", base_resolution=1024)
+    assert torch.allclose(sdf.shift_timesteps(torch.Size([3, 4096, 128]), t), d["shift_simple"],
+                          rtol=1e-6, atol=1e-7)
+
+
+def test_sample_timesteps_matches_reference():
+    """training.py:124-132 with the golden's seed: identical draws and quantile clamp."""
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.training import sample_timesteps
+    d = load_file(os.path.join(GOLD, "rf_sched.safetensors"))
+    with open(os.path.join(GOLD, "rf_sched.json")) as f:
+        meta = json.load(f)
+    cfg = TrainConfig(checkpoint_path="-", rf_log_normal_mu=-0.5, rf_log_normal_sigma=1.0)
+    torch.manual_seed(meta["tsample_seed"])
+    t = sample_timesteps(8, cfg, "cpu")
+    assert torch.equal(t, d["tsample_t"])
+    assert float(t.min()) >= 0.0 and float(t.max()) <= 1.0
+
+
+# --------------------------------------------------------------------- module tree / naming
+def _meta_model(cfg, r):
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.lora import apply_training_strategy
+    from ltx_amd.transformer3d import Transformer3DModel
+    with torch.device("meta"):
+        m = Transformer3DModel.from_config(cfg)
+        if r:
+            apply_training_strategy(m, TrainConfig(checkpoint_path="-", lora_rank=r, lora_alpha=r),
+                                    "lora_audio")
+    return m
+
+
+def test_tiny_param_names_match_reference_peft_model():
+    d, meta = _tiny()
+    m = _meta_model(meta["config"], meta["lora_rank"])
+    ours = {canonical_name(n): tuple(p.shape) for n, p in m.named_parameters()}
+    ref = {k[2:]: tuple(v.shape) for k, v in d.items() if k.startswith("w.")}
+    assert ours == ref
+    trainable = {canonical_name(n) for n, p in m.named_parameters() if p.requires_grad}
+    assert trainable == {k[5:] for k in d if k.startswith("grad.")}
+    # raw (un-canonicalised) names keep peft's layout
+    raw = [n for n, _ in m.named_parameters() if "attn2.to_out.0" in n]
+    assert any(n.endswith("attn2.to_out.0.base_layer.weight") for n in raw)
+    assert any(n.endswith("attn2.to_out.0.lora_B.default.weight") for n in raw)
+
+
+def test_ltx2b_param_counts():
+    """1,923,385,472 base parameters + 7,340,032 LoRA (r=16); 19,927,040 trainable."""
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    m = _meta_model(OURS_TRANSFORMER_CONFIG, 16)
+    total = sum(p.numel() for p in m.parameters())
+    train = sum(p.numel() for p in m.parameters() if p.requires_grad)
+    lora = sum(p.numel() for n, p in m.named_parameters() if "lora_" in n)
+    assert train == 19_927_040
+    assert total - lora == 1_923_385_472
+    assert lora == 28 * 4 * 16 * (2048 + 2048)
+
+
+def test_full_strategy_trainable_set():
+    """training.py:75-91 substring rule ('full' mode): FF and patchify_proj stay frozen."""
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.lora import apply_training_strategy
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    m = _meta_model(OURS_TRANSFORMER_CONFIG, 0)
+    apply_training_strategy(m, TrainConfig(checkpoint_path="-"), "full")
+    train = {n for n, p in m.named_parameters() if p.requires_grad}
+    assert not any(".ff." in n or n.startswith("patchify_proj") for n in train)
+    assert "scale_shift_table" in train and "proj_out.weight" in train
+    assert any("attn1.to_q" in n for n in train) and any("attn2.k_norm" in n for n in train)
+    assert abs(sum(p.numel() for n, p in m.named_parameters() if n in train) - 983.3e6) < 0.05e6
+
+
+def test_skip_layer_mask():
+    """transformer3d.py:187-203."""
+    d, meta = _tiny()
+    m = _meta_model(meta["config"], 0)
+    assert m.create_skip_layer_mask(2, 3, 1, None) is None
+    m = m.to_empty(device="cpu")
+    mask = m.create_skip_layer_mask(2, 3, 1, [0])
+    assert mask.shape == (len(m.transformer_blocks), 6)
+    assert mask[0].tolist() == [1, 0, 1, 1, 0, 1] and mask[1].eq(1).all()
+
+
+# -------------------------------------------------------------------- checkpoints / merging
+def _tiny_state(d):
+    return {k[2:]: v for k, v in d.items() if k.startswith("w.") and "lora_" not in k}
+
+
+def test_from_pretrained_single_file_roundtrip(tmp_path):
+    """Single-file safetensors with metadata['config'] (transformer3d.py:337-352), including the
+    ComfyUI 'model.diffusion_model.' prefix (transformer3d.py:279-292)."""
+    from ltx_amd.patchifier import SymmetricPatchifier
+    from ltx_amd.transformer3d import Transformer3DModel
+    d, meta = _tiny()
+    state = {k: v.contiguous() for k, v in _tiny_state(d).items()}
+    md = {"config": json.dumps({"transformer": meta["config"]})}
+    for prefix in ("", "model.diffusion_model."):
+        path = tmp_path / f"ckpt{len(prefix)}.safetensors"
+        save_file({prefix + k: v for k, v in state.items()}, str(path), metadata=md)
+        m = Transformer3DModel.from_pretrained(str(path), patchifier=SymmetricPatchifier(1))
+        got = m.state_dict()
+        assert set(got) == set(state)
+        for k, v in state.items():
+            assert torch.equal(got[k], v), k
+        assert m.dtype == torch.bfloat16 and m.device.type == "cpu"
+        assert isinstance(m.patchifier, SymmetricPatchifier)
+
+
+def test_merged_state_dict_folds_lora():
+    """peft merge_and_unload as save_training_checkpoint exports it (torch_utils.py:66-102)."""
+    from ltx_amd.lora import merged_state_dict
+    d, meta = _tiny()
+    m = _meta_model(meta["config"], meta["lora_rank"])
+    sd = {}
+    for n, _ in m.named_parameters():
+        sd[n] = d["w." + canonical_name(n)].clone()
+    m.load_state_dict(sd, assign=True, strict=True)
+    out = merged_state_dict(m)
+    assert not any("lora_" in k or "base_layer" in k for k in out)
+    ref_keys = {k for k in _tiny_state(d)}
+    assert set(out) == ref_keys
+    blk = "transformer_blocks.0.attn2.to_q"
+    w = d[f"w.{blk}.weight"].float()
+    a = d[f"w.{blk}.lora_A.default.weight"].float()
+    b = d[f"w.{blk}.lora_B.default.weight"].float()
+    s = meta.get("lora_alpha", meta["lora_rank"]) / meta["lora_rank"]
+    assert torch.equal(out[f"{blk}.weight"], (w + s * (b @ a)).to(torch.bfloat16))
+
+
+def test_product_ops_refuse_cpu_tensors():
+    """No CPU fallback: the product path raises instead of computing on the host."""
+    from ltx_amd import ops
+    with pytest.raises(Exception):
+        ops.patchify(torch.zeros(1, 4, 1, 2, 2, dtype=torch.bfloat16))
+
+
+# ------------------------------------------------------------------------ DP all-reduce (gloo)
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _dp_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ltx_amd.training import GradAllReduce
+        torch.manual_seed(0)
+        params = [torch.nn.Parameter(torch.zeros(s, dtype=dt)) for s, dt in
+                  [((16, 64), torch.float32), ((64, 16), torch.float32), ((300,), torch.bfloat16),
+                   ((7, 5), torch.float32), ((1000,), torch.bfloat16)]]
+        g = torch.Generator().manual_seed(100 + rank)
+        for i, p in enumerate(params):
+            if i == 3 and rank == 0:
+                continue  # a missing grad on one rank counts as zeros
+            p.grad = torch.randn(p.shape, generator=g).to(p.dtype)
+        red = GradAllReduce(params, bucket_mb=0.004)  # several buckets
+        assert len(red.buckets) > 1
+        red()
+        torch.save({i: p.grad for i, p in enumerate(params)}, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_gloo_world2():
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        mp.start_processes(_dp_worker, args=(world, _free_port(), td), nprocs=world,
+                           start_method="spawn", join=True)
+        res = [torch.load(os.path.join(td, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    shapes = [((16, 64), torch.float32), ((64, 16), torch.float32), ((300,), torch.bfloat16),
+              ((7, 5), torch.float32), ((1000,), torch.bfloat16)]
+    expect = []
+    for i, (s, dt) in enumerate(shapes):
+        acc = torch.zeros(s, dtype=torch.float32)
+        for r in range(world):
+            g = torch.Generator().manual_seed(100 + r)
+            for j, (s2, dt2) in enumerate(shapes[:i + 1]):
+                if j == 3 and r == 0:
+                    continue
+                v = torch.randn(s2, generator=g).to(dt2)
+            if not (i == 3 and r == 0):
+                acc += v.float()
+        expect.append((acc / world).to(dt))
+    for r in range(world):
+        for i, e in enumerate(expect):
+            got = res[r][i]
+            assert got.dtype == e.dtype
+            assert torch.equal(got, e), (r, i)
+    assert math.isfinite(float(expect[0].sum()))
