@@ -92,11 +92,11 @@ def synthetic_batch(device, rank):
     return batch, prompt, mask
 
 
-def cpu_baseline(budget_layers=4):
+def cpu_baseline(budget_layers=28, timed=2):
     """The oracle restatement (oracle/ltx_oracle.py) on the host cores: config A at B=1,
-    N = 1792, `budget_layers` of the 28 blocks, one warm-up + one timed fwd+bwd; per-sample
-    time extrapolated x(28/budget_layers) (the non-block prologue/head is scaled too, which
-    makes the CPU figure slightly pessimistic)."""
+    N = 1792, `budget_layers` of the 28 blocks (all of them by default), one warm-up + `timed`
+    timed fwd+bwd steps (~10-20 s of CPU work); per-sample time = mean timed step
+    x(28/budget_layers)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import ltx_oracle as O
     from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
@@ -120,19 +120,19 @@ def cpu_baseline(budget_layers=4):
     prompt = torch.randn(1, L_TXT, 4096, generator=g)
     mask = (torch.arange(L_TXT) < 16).long().view(1, L_TXT)
     times = []
-    for _ in range(2):
+    for _ in range(1 + timed):
         t0 = time.perf_counter()
         r = O.train_step(p, cfg, lat, ref, pose, prompt, mask)
         r["loss"].backward()
         times.append(time.perf_counter() - t0)
         for v in p.values():
             v.grad = None
-    per_sample = times[-1] * (28.0 / budget_layers)
+    per_sample = sum(times[1:]) / timed * (28.0 / budget_layers)
     return {"value": 1.0 / per_sample, "unit": "samples/s", "cores": threads, "kind": "port",
             "tokens_per_s": F_LAT * H_LAT * W_LAT / per_sample,
             "sample": (f"oracle/ltx_oracle.py train_step fwd+bwd, B=1, N={F_LAT*H_LAT*W_LAT}, "
-                       f"{budget_layers}/28 LTX-2B blocks timed (1 warm-up + 1 timed step, "
-                       f"{times[-1]:.1f} s) and scaled x{28/budget_layers:g}; torch "
+                       f"{budget_layers}/28 LTX-2B blocks, 1 warm-up + {timed} timed steps "
+                       f"({sum(times[1:]):.1f} s timed), scaled x{28/budget_layers:g}; torch "
                        f"{torch.__version__} CPU, {threads} threads, cpu_count={os.cpu_count()}")}
 
 

@@ -321,8 +321,17 @@ constexpr int ST2 = XT2 + WT2;      // 64 KiB per stage
 constexpr int C_STRIDE2 = BN2 * 2 + 8;
 constexpr int LDS2 = (2 * ST2 > BM2 * C_STRIDE2) ? 2 * ST2 : BM2 * C_STRIDE2;
 
-template <int EPI, int R, int SPLIT>
+// VAR bit 0: split the tile-(t+2) DMA issue over Q3 (X) and the next Q0 (W); bit 1: static
+// priority (waves 4-7 at s_setprio 1 for the whole loop, no per-quarter flips;
+// MI355X_MICROARCH.md "Two waves per SIMD" item 4).
+template <int EPI, int R, int VAR>
 __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
+  constexpr bool SPLIT = (VAR & 1) != 0;
+  constexpr bool SPRIO = (VAR & 2) != 0;
+  constexpr bool DBG_NODMA = (VAR & 4) != 0;   // measurement only (wrong results): no DMA past the prologue
+  constexpr bool DBG_NOBAR = (VAR & 8) != 0;   // measurement only: and no mid-loop wait/barrier
+  constexpr bool DBG_NOWAIT = (VAR & 16) != 0; // measurement only: DMA issued, never waited for in the loop
+  constexpr bool ASMDMA = (VAR & 32) != 0;     // scalar-base + 32-bit offset LDS-DMA (inline asm)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -335,15 +344,51 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
   // DMA: wave w moves rows [32w, 32w+32) of the X tile and of the W tile (4 + 4 x 1 KiB)
   const int lrow = lane >> 3;
   const int pchunk = lane & 7;
+  const int nk_main = p.K / BK;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  // ASMDMA: global_load_lds_dwordx4 with a scalar (per-block, per-K-tile) base and a per-lane
+  // 32-bit offset (row clamp + source-side swizzle), M0 written in the same asm statement: one
+  // SALU add pair + the DMA per piece instead of 64-bit VALU address math + v_readfirstlane.
+  uint32_t xo[4], wo[4];
+  const char* xb = nullptr;
+  const char* wb = nullptr;
+  auto set_x = [&](bool ext) {
+    const int64_t ld = ext ? p.lda2 : p.lda;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wave * 4 + i) * 8 + lrow;
+      xo[i] = (uint32_t)(((int64_t)(min(m0 + row, p.M - 1) - m0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
+    }
+    xb = (const char*)(ext ? p.A2 : p.A) + (int64_t)m0 * ld * 2;
+  };
+  auto set_w = [&](bool ext) {
+    const int64_t ld = ext ? p.ldw2 : p.ldw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wave * 4 + i) * 8 + lrow;
+      wo[i] = (uint32_t)(((int64_t)(min(n0 + row, p.N - 1) - n0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
+    }
+    wb = (const char*)(ext ? p.W2 : p.W) + (int64_t)n0 * ld * 2;
+  };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  auto glds_s = [&](uint32_t voff, const char* sbase, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+  };
   const bf16_t* xsrc[4];
   const bf16_t* wsrc[4];
+  if constexpr (ASMDMA) {
+    set_x(nk_main == 0);
+    set_w(nk_main == 0);
+  } else {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = (wave * 4 + i) * 8 + lrow;
-    xsrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + ((pchunk ^ (row & 7)) * 8);
-    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.ldw + ((pchunk ^ (row & 7)) * 8);
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wave * 4 + i) * 8 + lrow;
+      xsrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + ((pchunk ^ (row & 7)) * 8);
+      wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.ldw + ((pchunk ^ (row & 7)) * 8);
+    }
   }
-  const int nk_main = p.K / BK;
   // K-extension tiles (LoRA fused into the K loop) read A2/W2 instead of A/W
   auto xptr = [&](int i, int kt) -> const bf16_t* {
     if (kt < nk_main) return xsrc[i] + kt * BK;
@@ -356,14 +401,30 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
     return p.W2 + (int64_t)min(n0 + row, p.N - 1) * p.ldw2 + (kt - nk_main) * BK + ((pchunk ^ (row & 7)) * 8);
   };
   auto stage_x = [&](int st, int kt) {
-    char* base = smem + st * ST2;
+    if constexpr (ASMDMA) {
+      if (kt == nk_main && nk_main > 0) set_x(true);  // ext tiles come last, in issue order
+      const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
+      const uint32_t l = lds0 + st * ST2 + wv * 4096;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(xptr(i, kt), base + (wave * 4 + i) * 1024);
+      for (int i = 0; i < 4; ++i) glds_s(xo[i], sb, l + i * 1024);
+    } else {
+      char* base = smem + st * ST2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds16(xptr(i, kt), base + (wave * 4 + i) * 1024);
+    }
   };
   auto stage_w = [&](int st, int kt) {
-    char* base = smem + st * ST2;
+    if constexpr (ASMDMA) {
+      if (kt == nk_main && nk_main > 0) set_w(true);
+      const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
+      const uint32_t l = lds0 + st * ST2 + XT2 + wv * 4096;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(wptr(i, kt), base + XT2 + (wave * 4 + i) * 1024);
+      for (int i = 0; i < 4; ++i) glds_s(wo[i], sb, l + i * 1024);
+    } else {
+      char* base = smem + st * ST2;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) glds16(wptr(i, kt), base + XT2 + (wave * 4 + i) * 1024);
+    }
   };
   auto stage = [&](int st, int kt) {
     stage_x(st, kt);
@@ -405,12 +466,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
   }
 #define LTX_MFMA_Q(AS, BS, NH)                                                                        \
   __builtin_amdgcn_sched_barrier(0);                                                                  \
-  __builtin_amdgcn_s_setprio(1);                                                                      \
+  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(1);                                                \
   _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
   _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
     acc[(NH) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * 4 + i][j], 0, 0, 0); \
-  __builtin_amdgcn_s_setprio(0);                                                                      \
+  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(0);                                                \
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (SPRIO) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
 
   int cur = 0;
   bool pend_w = false;  // SPLIT: W half of tile kt+1's DMA still to issue in Q0
@@ -419,7 +483,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
     // Q0 (h0, n0): prefetch A(Q1)
 #pragma unroll
     for (int i = 0; i < 4; ++i) aO[i] = *(const s16x8*)(st + aoff[1][i]);
-    if (SPLIT && pend_w) {
+    if (SPLIT && pend_w && !DBG_NODMA) {
       stage_w(cur ^ 1, kt + 1);
       pend_w = false;
     }
@@ -437,8 +501,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
     LTX_MFMA_Q(aE, b1, 0)
     // all reads of tile t issued: wait tile t+1, free tile t's stage, DMA tile t+2 into it
     if (kt + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (kt + 2 < nk) {
+      if constexpr (DBG_NOBAR)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      else if constexpr (DBG_NOWAIT)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + 2 < nk && !DBG_NODMA) {
         if (SPLIT) {
           stage_x(cur, kt + 2);
           pend_w = true;
@@ -505,7 +574,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
 }
 
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
-static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 split DMA burst (default), 1 single burst
+static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (asm DMA + split + static prio),
+                                // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split;
+                                // 4-7 measurement-only (wrong results)
 
 template <int EPI, int R = 0>
 static int launch(const GemmParams& p, hipStream_t s) {
@@ -520,10 +591,39 @@ static int launch(const GemmParams& p, hipStream_t s) {
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 33>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 35>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       attr_set = true;
     }
-    if (g_variant == 0)  // default: DMA issue split over two quarters
+    if (g_variant == 0)  // default: scalar-base asm DMA, issue split over two quarters, static priority
+      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else if (g_variant == 10)  // previous default: builtin DMA, split issue
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 1>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else if (g_variant == 2)
+      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 3>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else if (g_variant == 8)
+      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 33>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else if (g_variant == 9)
+      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else if (g_variant >= 4) {
+      if constexpr (EPI == LTX_EPI_STORE && R == 0) {  // measurement-only variants
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 13>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 17>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        if (g_variant == 4)
+          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 5>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+        else if (g_variant == 6)
+          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 17>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+        else if (g_variant == 7)
+          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 16>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+        else
+          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 13>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+      } else {
+        return fail(LTX_ERR_BAD_ARG, "gemm: measurement variants exist for the plain store epilogue only");
+      }
+    }
     else
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 0>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
   } else {
