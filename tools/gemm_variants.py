@@ -31,6 +31,7 @@ ap.add_argument("--shape", default=None)
 ap.add_argument("--shapes", default=None)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--torch", action="store_true")
+ap.add_argument("--check", action="store_true")
 args = ap.parse_args()
 lib = _lib.load()
 names = [args.shape] if args.shape else (args.shapes.split(",") if args.shapes else list(SHAPES))
@@ -51,6 +52,22 @@ for name in names:
             ms = timeit(lambda: ops.gemm(x, w, bias=bias, epilogue=epi, aux0=pre, out=c), args.iters)
         print(f"{name} {'torch' if args.torch else 'v%d' % args.only} {fl / ms / 1e9:.1f} TF")
         continue
+    if args.check:
+        outs = {}
+        for v in [int(s2) for s2 in args.variants.split(",")]:
+            lib.ltx_gemm_set_variant(v)
+            c.fill_(0)
+            ops.gemm(x, w, bias=bias, epilogue=epi, aux0=pre, out=c)
+            torch.cuda.synchronize()
+            outs[v] = c.clone()
+        lib.ltx_gemm_set_variant(0)
+        ref = (x.float() @ w.float().t() + bias.float())
+        if epi == "gelu":
+            ref = torch.nn.functional.gelu(ref.bfloat16().float(), approximate="tanh")
+        v0 = list(outs)[0]
+        for v, o in outs.items():
+            rel = float((o.float() - ref).norm() / ref.norm())
+            print(f"check {name} v{v}: equal_to_v{v0}={torch.equal(o, outs[v0])} rel_vs_fp32={rel:.2e}", flush=True)
     row = {}
     for rnd in range(3):
         for v in [int(s) for s in args.variants.split(",")]:

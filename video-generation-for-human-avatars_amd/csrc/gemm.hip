@@ -573,6 +573,245 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong large-tile kernel: 256x256 tile, BK = 64, 8 waves in two groups G0 = waves 0-3 and
+// G1 = waves 4-7 (each SIMD holds one wave of each group). G1 runs one barrier behind G0, so on
+// every SIMD one wave computes (16 MFMAs) while its partner reads its LDS fragments and issues its
+// LDS-DMA (MI355X_MICROARCH.md "Two waves per SIMD"; cdna_hip_programming.md "The 256^2 8-phase
+// template"). A phase computes one 128x128 C quadrant of the block over the whole K-tile, each
+// wave a 64 (m) x 32 (n) piece of it. The quadrant order (0,0),(0,1),(1,1),(1,0) reuses fragments
+// from registers (X half 0 in phases 0-1, X half 1 in 2-3, W half 0 in 0 and 3, W half 1 in 1-2),
+// so each staged 16 KiB piece (X0, X1, W0, W1 of a K-tile) is read in ONE phase and refilled two
+// phases later: exactly one piece (2 DMA instructions per wave) per phase, issued 5-6 phases
+// before its first read; counted vmcnt (never 0 in the loop) + raw s_barrier.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ const char* sgpr_ptr(const char* ptr) {  // wave-uniform pointer -> SGPR pair
+  const uint64_t v = (uint64_t)ptr;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const char*)(((uint64_t)hi << 32) | lo);
+}
+
+constexpr int PIECE = 128 * BK * 2;  // 16 KiB: 128 rows x 64 k, swizzled like the 128x64 tiles
+constexpr int BUF_P = 4 * PIECE;     // one K-tile: [X0, X1, W0, W1]
+
+__device__ __forceinline__ void wait_vm_pieces(int n) {  // n = pieces allowed in flight (x2 DMA each)
+  switch (n) {
+    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+struct PPDma {
+  uint32_t xo[2][2], wo[2][2];    // main operands: per-lane byte offsets [half][j]
+  uint32_t xoe[2][2], woe[2][2];  // K-extension operands
+  const char* xb;
+  const char* wb;
+  const char* xbe;
+  const char* wbe;
+  uint32_t lds0;
+  int wv, nk_main;
+};
+
+__device__ __forceinline__ void pp_glds(uint32_t voff, const char* sbase, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+
+// piece T of K-tile kt: 0 X0, 1 W0, 2 W1, 3 X1 (the issue order within a K-tile)
+__device__ __forceinline__ void pp_issue(const PPDma& d, int kt, int T) {
+  const bool is_x = (T == 0 || T == 3);
+  const int h = (T == 0 || T == 1) ? 0 : 1;
+  const bool ext = kt >= d.nk_main;
+  const int kk = ext ? kt - d.nk_main : kt;
+  const char* base = is_x ? (ext ? d.xbe : d.xb) : (ext ? d.wbe : d.wb);
+  const char* sb = sgpr_ptr(base + kk * (BK * 2));
+  const int slot = is_x ? h : 2 + h;
+  const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane(d.lds0 + (kt & 1) * BUF_P + slot * PIECE + d.wv * 2048);
+  uint32_t o0, o1;
+  if (is_x) {
+    o0 = ext ? (h ? d.xoe[1][0] : d.xoe[0][0]) : (h ? d.xo[1][0] : d.xo[0][0]);
+    o1 = ext ? (h ? d.xoe[1][1] : d.xoe[0][1]) : (h ? d.xo[1][1] : d.xo[0][1]);
+  } else {
+    o0 = ext ? (h ? d.woe[1][0] : d.woe[0][0]) : (h ? d.wo[1][0] : d.wo[0][0]);
+    o1 = ext ? (h ? d.woe[1][1] : d.woe[0][1]) : (h ? d.wo[1][1] : d.wo[0][1]);
+  }
+  pp_glds(o0, sb, l);
+  pp_glds(o1, sb, l + 1024);
+}
+
+template <int EPI, int R>
+__global__ __launch_bounds__(512, 1) void gemm_nt_kernel_p(const GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const bool g1 = wv >= 4;
+  const int ntm = (p.M + BM2 - 1) / BM2, ntn = (p.N + BN2 - 1) / BN2;
+  int tm, tn;
+  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
+  const int m0 = tm * BM2, n0 = tn * BN2;
+  const int nk_main = __builtin_amdgcn_readfirstlane(p.K / BK);
+  const int nk = __builtin_amdgcn_readfirstlane(p.K / BK + p.K2 / BK);
+
+  // ---- DMA bookkeeping: wave w moves piece rows h*128 + 16w + 8j + (lane>>3), j = 0, 1
+  PPDma d;
+  {
+    const int lrow = lane >> 3, pchunk = lane & 7;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = h * 128 + wave * 16 + j * 8 + lrow;
+        const int sw = (pchunk ^ (row & 7)) * 8;
+        const int64_t xr = min(m0 + row, p.M - 1) - m0, wr = min(n0 + row, p.N - 1) - n0;
+        d.xo[h][j] = (uint32_t)((xr * p.lda + sw) * 2);
+        d.wo[h][j] = (uint32_t)((wr * p.ldw + sw) * 2);
+        d.xoe[h][j] = (uint32_t)((xr * p.lda2 + sw) * 2);
+        d.woe[h][j] = (uint32_t)((wr * p.ldw2 + sw) * 2);
+      }
+    d.xb = (const char*)p.A + (int64_t)m0 * p.lda * 2;
+    d.wb = (const char*)p.W + (int64_t)n0 * p.ldw * 2;
+    d.xbe = (const char*)p.A2 + (int64_t)m0 * p.lda2 * 2;
+    d.wbe = (const char*)p.W2 + (int64_t)n0 * p.ldw2 * 2;
+    d.lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+    d.wv = wv;
+    d.nk_main = nk_main;
+  }
+  // phase q issues piece (q + 6) & 3 of K-tile (q + 6) >> 2 while that tile exists
+  auto issue_phase = [&](int q) {
+    const int kt = (q + 6) >> 2;
+    if (kt < nk) pp_issue(d, kt, (q + 6) & 3);
+  };
+  // pieces allowed in flight after phase q's issue: those of phases q-3..q that issued
+  auto inflight = [&](int q) { return min(4, max(0, 4 * nk - 6 - (q - 3))); };
+
+  const int wm = wave >> 2, wn = wave & 3;
+  const int frow = lane & 15, fchunk = lane >> 4;
+  f32x4 acc[4][2][4];  // [quadrant phase][n-frag j][m-frag i]
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[a][j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  s16x8 xf[4][2], wf0[2][2], wf1[2][2];  // [frag][k-step]
+  auto read_x = [&](const char* piece) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) xf[i][ks] = *(const s16x8*)(piece + swz(wm * 64 + i * 16 + frow, ks * 4 + fchunk));
+  };
+  auto read_w = [&](const char* piece, s16x8 (&wf)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) wf[j][ks] = *(const s16x8*)(piece + swz(wn * 32 + j * 16 + frow, ks * 4 + fchunk));
+  };
+#define LTX_PP_MFMA(QA, WF)                                                                           \
+  __builtin_amdgcn_sched_barrier(0);                                                                  \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                  \
+  __builtin_amdgcn_s_setprio(1);                                                                      \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                    \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                       \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
+    acc[QA][j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WF[j][ks], xf[i][ks], acc[QA][j][i], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);                                                                      \
+  __builtin_amdgcn_sched_barrier(0);
+#define LTX_PP_BAR() asm volatile("s_barrier" ::: "memory")
+
+  // ---- prologue: the pieces of phases -6..-1 (X0, W0, W1, X1 of tile 0; X0, W0 of tile 1)
+  for (int q = -6; q < 0; ++q) issue_phase(q);
+  wait_vm_pieces(inflight(-1));
+  LTX_PP_BAR();
+  if (g1) LTX_PP_BAR();  // the stagger: G1 runs one barrier behind G0
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF_P;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = 4 * t + r;
+      // load segment: this phase's fragments, then its DMA piece
+      if (r == 0) {
+        read_x(buf);
+        read_w(buf + 2 * PIECE, wf0);
+      } else if (r == 1) {
+        read_w(buf + 3 * PIECE, wf1);
+      } else if (r == 2) {
+        read_x(buf + PIECE);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      issue_phase(q);
+      if (g1) wait_vm_pieces(inflight(q));
+      LTX_PP_BAR();
+      // compute segment: quadrant r
+      if (r == 0) { LTX_PP_MFMA(0, wf0) }
+      else if (r == 1) { LTX_PP_MFMA(1, wf1) }
+      else if (r == 2) { LTX_PP_MFMA(2, wf1) }
+      else { LTX_PP_MFMA(3, wf0) }
+      if (!g1) wait_vm_pieces(inflight(q));
+      LTX_PP_BAR();
+    }
+  }
+  if (!g1) LTX_PP_BAR();  // match G1's stagger barrier
+#undef LTX_PP_MFMA
+#undef LTX_PP_BAR
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // epilogue stage 1: bf16(acc + bias) -> LDS image [256 m][256 n]
+  char* cimg = smem;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int qm = (a >= 2) ? 1 : 0;
+    const int qn = (a == 1 || a == 2) ? 1 : 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int nl = qn * 128 + wn * 32 + j * 16 + (lane >> 4) * 4;
+      float b4[4] = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias) {
+        const int gn = n0 + nl;
+        if (gn + 3 < p.N) {
+          const u32x2 bb = *(const u32x2*)(p.bias + gn);
+          b4[0] = bf2f((bf16_t)bb[0]); b4[1] = bf2f((bf16_t)(bb[0] >> 16));
+          b4[2] = bf2f((bf16_t)bb[1]); b4[3] = bf2f((bf16_t)(bb[1] >> 16));
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ml = qm * 128 + wm * 64 + i * 16 + (lane & 15);
+        u32x2 pk;
+        pk[0] = pack2(acc[a][j][i][0] + b4[0], acc[a][j][i][1] + b4[1]);
+        pk[1] = pack2(acc[a][j][i][2] + b4[2], acc[a][j][i][3] + b4[3]);
+        *(u32x2*)(cimg + ml * C_STRIDE2 + nl * 2) = pk;
+      }
+    }
+  }
+  __syncthreads();
+  const int cgrp = tid & 31;
+  for (int rr = tid >> 5; rr < BM2; rr += 512 / 32) {
+    const int m = m0 + rr;
+    const int n = n0 + cgrp * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const u32x2 lo = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16);
+    const u32x2 hi = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16 + 8);
+    bf16_t cv[8] = {(bf16_t)lo[0], (bf16_t)(lo[0] >> 16), (bf16_t)lo[1], (bf16_t)(lo[1] >> 16),
+                    (bf16_t)hi[0], (bf16_t)(hi[0] >> 16), (bf16_t)hi[1], (bf16_t)(hi[1] >> 16)};
+    float o[8];
+    epilogue_row8<EPI, R>(p, m, n, cv, o);
+    u32x4 pk;
+    pk[0] = pack2(o[0], o[1]);
+    pk[1] = pack2(o[2], o[3]);
+    pk[2] = pack2(o[4], o[5]);
+    pk[3] = pack2(o[6], o[7]);
+    *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
+  }
+}
+
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
 static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (asm DMA + split + static prio),
                                 // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split;
@@ -598,7 +837,14 @@ static int launch(const GemmParams& p, hipStream_t s) {
     }
     if (g_variant == 0)  // default: scalar-base asm DMA, issue split over two quarters, static priority
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant == 10)  // previous default: builtin DMA, split issue
+    else if (g_variant == 11) {  // ping-pong 8-phase kernel
+      static bool pp_set = false;
+      if (!pp_set) {
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_p<EPI, R>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        pp_set = true;
+      }
+      hipLaunchKernelGGL((gemm_nt_kernel_p<EPI, R>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    } else if (g_variant == 10)  // previous default: builtin DMA, split issue
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 1>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
     else if (g_variant == 2)
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 3>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
