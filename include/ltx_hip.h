@@ -108,18 +108,24 @@ int ltx_layernorm_modulate_bwd(const void* dy, const void* x, const float* mean,
                                int64_t M, int64_t D, int64_t rows_per_batch, void* stream);
 
 /* ---- K9 tail: q/k RMSNorm (affine, eps 1e-5, across all heads) + 3-D RoPE ------------------- */
+/* RoPE cos/sin table (precompute_freqs_cis, transformer3d.py:209-277): omega [D/6] f32 is the
+ * reference's `theta ** linspace(0,1,D//6) * pi/2` (computed once on the host),
+ * phi = omega[j] * (grid[b,a,n]/max_pos[a]*2 - 1), D%6 leading pad dims (cos 1, sin 0), both
+ * rounded to bf16 as the reference's tables are; grid is [B,3,N] int64 (grid_is_float == 0) or
+ * f32. Output cs [B*N, D/2] u32 = bf16 cos | bf16 sin << 16 per element pair (16-B aligned).
+ * Pass B = 1 when all batches share their coordinates (then cs_batch_rows = 0 below). */
+int ltx_rope_table(const void* indices_grid, int grid_is_float, int64_t B, int64_t N, int64_t D,
+                   const float* omega, float max_pos_t, float max_pos_h, float max_pos_w, uint32_t* cs,
+                   void* stream);
 /* q_out = rope(bf16(bf16(q_in * rstd) * q_weight)) (attention.py:996-1012, RoPE :917-932), same
- * for k. cos/sin of transformer3d.py:221-277 are formed in-kernel: omega [D/6] f32 is the
- * reference's `theta ** linspace(0,1,D//6) * pi/2` table (computed once on the host),
- * phi = omega[j] * (grid[b,a,n]/max_pos[a]*2 - 1), D%6 leading pad dims (cos 1, sin 0); grid is
- * [B,3,N] int64 (grid_is_float == 0) or f32. rope == 0 skips the rotation (cross-attention).
+ * for k; token m = b*N + n reads table row b*cs_batch_rows + n (cs_batch_rows = N, or 0 for a
+ * batch-shared table). rope == 0 skips the rotation (cross-attention; rope_cs may be null).
  * k_in / k_out may be null (q only). Saves f32 rstd_q / rstd_k [M] (M = B*N rows). */
 int ltx_qk_norm_rope_fwd(const void* q_in, int64_t ldq_in, const void* k_in, int64_t ldk_in,
                          void* q_out, int64_t ldq_out, void* k_out, int64_t ldk_out,
                          const void* q_weight, const void* k_weight, float* rstd_q,
-                         float* rstd_k, const void* indices_grid, int grid_is_float, int64_t B,
-                         int64_t N, int64_t D, const float* omega, float max_pos_t,
-                         float max_pos_h, float max_pos_w, int rope, float eps, void* stream);
+                         float* rstd_k, const uint32_t* rope_cs, int64_t cs_batch_rows, int64_t B,
+                         int64_t N, int64_t D, int rope, float eps, void* stream);
 /* Backward: incoming dq (f32 when dq_is_f32, else bf16; it is rounded to bf16 first, as SDPA's
  * backward returns bf16) -> dq_raw bf16, the gradient w.r.t. q_in; same for k. */
 int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const void* dk_in,
@@ -127,9 +133,8 @@ int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const
                          const void* k_raw, int64_t ldk_raw, const void* q_weight,
                          const void* k_weight, const float* rstd_q, const float* rstd_k,
                          void* dq_out, int64_t ldq_out, void* dk_out, int64_t ldk_out,
-                         const void* indices_grid, int grid_is_float, int64_t B, int64_t N,
-                         int64_t D, const float* omega, float max_pos_t, float max_pos_h,
-                         float max_pos_w, int rope, void* stream);
+                         const uint32_t* rope_cs, int64_t cs_batch_rows, int64_t B, int64_t N,
+                         int64_t D, int rope, void* stream);
 
 /* ---- K10/K14: flash attention (F.scaled_dot_product_attention, attention.py:1057-1064) ------- */
 /* Q [B,Nq,H,d] (row stride ldq per token, head h at column h*d), K/V [B,Nk,H,d], O likewise;

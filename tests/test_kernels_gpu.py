@@ -241,6 +241,14 @@ def test_qk_norm_rope_fwd_bwd(D, grid_float):
     (kr * dk.view(B, N, D)).sum().backward()
     assert rel(dq_raw, qi.grad.reshape(B * N, D)) < 1e-2
     assert rel(dk_raw, ki.grad.reshape(B * N, D)) < 1e-2
+    # batch-broadcast coordinates -> one shared cos/sin table: bit-identical to per-batch tables
+    shared = ops.RopeSpec(coords[:1].expand(B, -1, -1), D, 10000.0, [20, 2048, 2048])
+    assert shared.cs_batch_rows == 0 and shared.cs.shape[0] == N
+    assert torch.equal(shared.cs, rope.cs[:N])
+    q_s, k_s, _, _ = ops.qk_norm_rope_fwd(qkv[:, :D], qkv[:, D:2 * D], qw, kw, shared)
+    assert torch.equal(q_s, q_out) and torch.equal(k_s, k_out)
+    dq_s, dk_s = ops.qk_norm_rope_bwd(dq, qkv[:, :D], qw, rq, dk, qkv[:, D:2 * D], kw, rk, shared)
+    assert torch.equal(dq_s, dq_raw) and torch.equal(dk_s, dk_raw)
     # q-only / no-rope variant (attn2 q_norm) + f32 incoming gradient
     q2, _, rq2, _ = ops.qk_norm_rope_fwd(qkv[:, :D], None, qw, None, None, B=B, N=N)
     assert ulps_bad(q2, O.rmsnorm(qkv[:, :D], 1e-5, qw), 1) < 1e-3

@@ -263,13 +263,39 @@ __device__ __forceinline__ void rope_cs(const RopeRow& rr, const float* __restri
   s = rbf(sv);
 }
 
+// cos/sin table, one packed u32 (bf16 cos | bf16 sin << 16) per element pair: rows = tokens of
+// Bt batches (Bt = 1 when every batch shares its coordinates), D/2 pairs per row. Built once per
+// forward and read by all 28 blocks' q/k kernels (fwd and bwd) instead of a sincosf per element.
+__global__ __launch_bounds__(256) void rope_table_kernel(const void* grid, int is_float, int N, int D, int64_t total,
+                                                         const float* __restrict__ omega, float mp0, float mp1,
+                                                         float mp2, uint32_t* __restrict__ cs) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int half = D / 2;
+  const int64_t row = idx / half;
+  const int i = (int)(idx - row * half);
+  const RopeRow rr = rope_row(grid, is_float, (int)(row / N), (int)(row % N), N, mp0, mp1, mp2);
+  float c, s;
+  rope_cs(rr, omega, 2 * i, D % 6, c, s);
+  cs[idx] = (uint32_t)f2bf(c) | ((uint32_t)f2bf(s) << 16);
+}
+
+__device__ __forceinline__ void cs4(const uint32_t* __restrict__ cs, int64_t rowbase, int e, float* c, float* s) {
+  const u32x4 v = *(const u32x4*)(cs + rowbase + (e >> 1));
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    c[t] = bf2f((bf16_t)(v[t] & 0xffff));
+    s[t] = bf2f((bf16_t)(v[t] >> 16));
+  }
+}
+
 // one wave = one (row, q|k) item
 __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
     const bf16_t* __restrict__ q_in, int64_t ldq_in, const bf16_t* __restrict__ k_in, int64_t ldk_in,
     bf16_t* __restrict__ q_out, int64_t ldq_out, bf16_t* __restrict__ k_out, int64_t ldk_out,
     const bf16_t* __restrict__ qw, const bf16_t* __restrict__ kw, float* __restrict__ rstd_q,
-    float* __restrict__ rstd_k, const void* grid, int grid_is_float, int N, int M, int D,
-    const float* __restrict__ omega, float mp0, float mp1, float mp2, int rope, int nsel, float eps) {
+    float* __restrict__ rstd_k, const uint32_t* __restrict__ cs, int64_t cs_batch_rows, int N, int M, int D,
+    int rope, int nsel, float eps) {
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
   const int m = item / nsel;
@@ -292,9 +318,7 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)D + eps);
   if (lane == 0) (which ? rstd_k : rstd_q)[m] = r;
-  RopeRow rr;
-  const int pad = D % 6;
-  if (rope) rr = rope_row(grid, grid_is_float, m / N, m % N, N, mp0, mp1, mp2);
+  const int64_t csrow = ((int64_t)(m / N) * cs_batch_rows + (m % N)) * (D / 2);
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
@@ -304,10 +328,11 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) nv[j] = rbf(rbf(v[p][j] * r) * w8[j]);
       if (rope) {
+        float c4[4], s4[4];
+        cs4(cs, csrow, e, c4, s4);
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
-          float c, s;
-          rope_cs(rr, omega, e + j, pad, c, s);
+          const float c = c4[j >> 1], s = s4[j >> 1];
           // out = bf16(bf16(x * cos) + bf16(rot(x) * sin)), rot = (-x1, x0)
           o[j] = rbf(nv[j] * c) + rbf(-nv[j + 1] * s);
           o[j + 1] = rbf(nv[j + 1] * c) + rbf(nv[j] * s);
@@ -329,8 +354,8 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
     int dk_f32, const bf16_t* __restrict__ q_raw, int64_t ldq_raw, const bf16_t* __restrict__ k_raw,
     int64_t ldk_raw, const bf16_t* __restrict__ qw, const bf16_t* __restrict__ kw,
     const float* __restrict__ rstd_q, const float* __restrict__ rstd_k, bf16_t* __restrict__ dq_out,
-    int64_t ldq_out, bf16_t* __restrict__ dk_out, int64_t ldk_out, const void* grid, int grid_is_float, int N,
-    int M, int D, const float* __restrict__ omega, float mp0, float mp1, float mp2, int rope, int nsel) {
+    int64_t ldq_out, bf16_t* __restrict__ dk_out, int64_t ldk_out, const uint32_t* __restrict__ cs,
+    int64_t cs_batch_rows, int N, int M, int D, int rope, int nsel) {
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
   const int m = item / nsel;
@@ -343,9 +368,7 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
   bf16_t* out = which ? dk_out + (int64_t)m * ldk_out : dq_out + (int64_t)m * ldq_out;
   const bf16_t* w = which ? kw : qw;
   const float r = (which ? rstd_k : rstd_q)[m];
-  RopeRow rr;
-  const int pad = D % 6;
-  if (rope) rr = rope_row(grid, grid_is_float, m / N, m % N, N, mp0, mp1, mp2);
+  const int64_t csrow = ((int64_t)(m / N) * cs_batch_rows + (m % N)) * (D / 2);
   float gx[MAXP][8], xv[MAXP][8];
   float dr = 0.f;
 #pragma unroll
@@ -361,10 +384,11 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
         load8((const bf16_t*)gin + (int64_t)m * ldg + e, g8);
       }
       if (rope) {
+        float c4[4], s4[4];
+        cs4(cs, csrow, e, c4, s4);
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
-          float c, s;
-          rope_cs(rr, omega, e + j, pad, c, s);
+          const float c = c4[j >> 1], s = s4[j >> 1];
           const float da0 = rbf(g8[j] * c), da1 = rbf(g8[j + 1] * c);
           const float dr0 = rbf(g8[j] * s), dr1 = rbf(g8[j + 1] * s);  // d(rot)
           // rot[2i] = -x[2i+1], rot[2i+1] = x[2i]
@@ -454,14 +478,25 @@ int ltx_layernorm_modulate_bwd(const void* dy, const void* x, const float* mean,
   return LTX_OK;
 }
 
+int ltx_rope_table(const void* indices_grid, int grid_is_float, int64_t B, int64_t N, int64_t D,
+                   const float* omega, float max_pos_t, float max_pos_h, float max_pos_w, uint32_t* cs,
+                   void* stream) {
+  LTX_CHECK_ARG(indices_grid && omega && cs && B > 0 && N > 0, "rope_table: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "rope_table: D must be %8 and <= 2048");
+  const int64_t total = B * N * (D / 2);
+  hipLaunchKernelGGL(rope_table_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     indices_grid, grid_is_float, (int)N, (int)D, total, omega, max_pos_t, max_pos_h, max_pos_w, cs);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
 int ltx_qk_norm_rope_fwd(const void* q_in, int64_t ldq_in, const void* k_in, int64_t ldk_in, void* q_out,
                          int64_t ldq_out, void* k_out, int64_t ldk_out, const void* q_weight, const void* k_weight,
-                         float* rstd_q, float* rstd_k, const void* indices_grid, int grid_is_float, int64_t B,
-                         int64_t N, int64_t D, const float* omega, float max_pos_t, float max_pos_h,
-                         float max_pos_w, int rope, float eps, void* stream) {
+                         float* rstd_q, float* rstd_k, const uint32_t* rope_cs, int64_t cs_batch_rows, int64_t B,
+                         int64_t N, int64_t D, int rope, float eps, void* stream) {
   LTX_CHECK_ARG(q_in && q_out && q_weight && rstd_q && B > 0 && N > 0, "qk_norm_rope_fwd: bad args");
   LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "qk_norm_rope_fwd: D must be %8 and <= 2048");
-  LTX_CHECK_ARG(!rope || (indices_grid && omega), "qk_norm_rope_fwd: rope needs indices_grid and omega");
+  LTX_CHECK_ARG(!rope || (rope_cs && ((uintptr_t)rope_cs % 16) == 0), "qk_norm_rope_fwd: rope needs a 16-B aligned table");
   const bool has_k = k_in != nullptr;
   LTX_CHECK_ARG(!has_k || (k_out && k_weight && rstd_k), "qk_norm_rope_fwd: k needs k_out, k_weight, rstd_k");
   LTX_CHECK_ARG(ldq_in % 8 == 0 && ldq_out % 8 == 0 && (!has_k || (ldk_in % 8 == 0 && ldk_out % 8 == 0)),
@@ -471,8 +506,7 @@ int ltx_qk_norm_rope_fwd(const void* q_in, int64_t ldq_in, const void* k_in, int
   hipLaunchKernelGGL(qk_norm_rope_fwd_kernel, dim3(row_blocks(M * nsel)), dim3(ROW_THREADS), 0,
                      (hipStream_t)stream, (const bf16_t*)q_in, ldq_in, (const bf16_t*)k_in, ldk_in, (bf16_t*)q_out,
                      ldq_out, (bf16_t*)k_out, ldk_out, (const bf16_t*)q_weight, (const bf16_t*)k_weight, rstd_q,
-                     rstd_k, indices_grid, grid_is_float, (int)N, (int)M, (int)D, omega, max_pos_t, max_pos_h,
-                     max_pos_w, rope, nsel, eps);
+                     rstd_k, rope_cs, cs_batch_rows, (int)N, (int)M, (int)D, rope, nsel, eps);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
@@ -480,12 +514,11 @@ int ltx_qk_norm_rope_fwd(const void* q_in, int64_t ldq_in, const void* k_in, int
 int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const void* dk_in, int64_t ldk_in,
                          int dk_is_f32, const void* q_raw, int64_t ldq_raw, const void* k_raw, int64_t ldk_raw,
                          const void* q_weight, const void* k_weight, const float* rstd_q, const float* rstd_k,
-                         void* dq_out, int64_t ldq_out, void* dk_out, int64_t ldk_out, const void* indices_grid,
-                         int grid_is_float, int64_t B, int64_t N, int64_t D, const float* omega, float max_pos_t,
-                         float max_pos_h, float max_pos_w, int rope, void* stream) {
+                         void* dq_out, int64_t ldq_out, void* dk_out, int64_t ldk_out, const uint32_t* rope_cs,
+                         int64_t cs_batch_rows, int64_t B, int64_t N, int64_t D, int rope, void* stream) {
   LTX_CHECK_ARG(dq_in && q_raw && q_weight && rstd_q && dq_out && B > 0 && N > 0, "qk_norm_rope_bwd: bad args");
   LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "qk_norm_rope_bwd: D must be %8 and <= 2048");
-  LTX_CHECK_ARG(!rope || (indices_grid && omega), "qk_norm_rope_bwd: rope needs indices_grid and omega");
+  LTX_CHECK_ARG(!rope || (rope_cs && ((uintptr_t)rope_cs % 16) == 0), "qk_norm_rope_bwd: rope needs a 16-B aligned table");
   const bool has_k = dk_in != nullptr;
   LTX_CHECK_ARG(!has_k || (k_raw && k_weight && rstd_k && dk_out), "qk_norm_rope_bwd: incomplete k operands");
   const int nsel = has_k ? 2 : 1;
@@ -493,8 +526,8 @@ int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const
   hipLaunchKernelGGL(qk_norm_rope_bwd_kernel, dim3(row_blocks(M * nsel)), dim3(ROW_THREADS), 0,
                      (hipStream_t)stream, dq_in, ldq_in, dq_is_f32, dk_in, ldk_in, dk_is_f32, (const bf16_t*)q_raw,
                      ldq_raw, (const bf16_t*)k_raw, ldk_raw, (const bf16_t*)q_weight, (const bf16_t*)k_weight,
-                     rstd_q, rstd_k, (bf16_t*)dq_out, ldq_out, (bf16_t*)dk_out, ldk_out, indices_grid,
-                     grid_is_float, (int)N, (int)M, (int)D, omega, max_pos_t, max_pos_h, max_pos_w, rope, nsel);
+                     rstd_q, rstd_k, (bf16_t*)dq_out, ldq_out, (bf16_t*)dk_out, ldk_out, rope_cs, cs_batch_rows,
+                     (int)N, (int)M, (int)D, rope, nsel);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

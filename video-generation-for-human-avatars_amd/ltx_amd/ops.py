@@ -177,24 +177,35 @@ def layernorm_modulate_bwd(dy, x, mean, rstd, onep, ld_mod, rows_per_batch):
 
 
 class RopeSpec:
-    """Per-forward RoPE description: indices_grid + the reference's frequency table.
+    """Per-forward RoPE state: the bf16 cos/sin table of precompute_freqs_cis
+    (transformer3d.py:209-277), built once on the device by ltx_rope_table and read by every
+    block's q/k kernels, forward and backward.
 
-    ``omega`` is computed exactly as precompute_freqs_cis does (transformer3d.py:231-250):
+    ``omega`` is computed exactly as the reference does (transformer3d.py:231-250):
     ``theta ** linspace(log(1,theta), log(theta,theta), dim//6) * pi / 2`` in f32 -- a 341-entry
-    constant, computed once on the host and copied to the device."""
+    constant, computed on the host. When ``indices_grid`` is a batch-broadcast view (stride 0 on
+    dim 0, as train_step passes it), one table serves every batch (cs_batch_rows = 0)."""
 
     def __init__(self, indices_grid, dim, theta, max_pos):
         import math
-        self.grid = indices_grid.contiguous()
-        self.is_float = 0 if indices_grid.dtype == torch.int64 else 1
-        if self.is_float and self.grid.dtype != F32:
-            self.grid = self.grid.to(F32)
+        self.B, _, self.N = indices_grid.shape
+        self.D = dim
+        shared = self.B > 1 and indices_grid.stride(0) == 0
+        grid = (indices_grid[:1] if shared else indices_grid).contiguous()
+        self.is_float = 0 if grid.dtype == torch.int64 else 1
+        if self.is_float and grid.dtype != F32:
+            grid = grid.to(F32)
+        self.grid = grid
         idx = theta ** torch.linspace(math.log(1, theta), math.log(theta, theta), dim // 6,
                                       dtype=torch.float32)
         idx = idx.to(torch.float32) * math.pi / 2
         self.omega = idx.to(indices_grid.device)
         self.max_pos = [float(m) for m in max_pos]
-        self.B, _, self.N = indices_grid.shape
+        bt = grid.shape[0]
+        self.cs_batch_rows = 0 if shared else self.N
+        self.cs = torch.empty(bt * self.N, dim // 2, dtype=torch.int32, device=indices_grid.device)
+        call("ltx_rope_table", _p(grid), self.is_float, bt, self.N, dim, _p(self.omega),
+             self.max_pos[0], self.max_pos[1], self.max_pos[2], _p(self.cs), _s())
 
 
 def qk_norm_rope_fwd(q_in, k_in, q_w, k_w, rope: RopeSpec = None, B=None, N=None, eps=1e-5,
@@ -211,12 +222,11 @@ def qk_norm_rope_fwd(q_in, k_in, q_w, k_w, rope: RopeSpec = None, B=None, N=None
     if rope is not None:
         B, N = rope.B, rope.N
     assert B * N == M
-    mp = rope.max_pos if rope is not None else [1.0, 1.0, 1.0]
     call("ltx_qk_norm_rope_fwd", _p(q_in), _rows(q_in, "q_in"), _p(k_in),
          _rows(k_in, "k_in") if k_in is not None else 0, _p(q_out), _rows(q_out, "q_out"),
          _p(k_out), _rows(k_out, "k_out") if k_in is not None else 0, _p(q_w), _p(k_w), _p(rq),
-         _p(rk), _p(rope.grid) if rope else None, rope.is_float if rope else 0, B, N, D,
-         _p(rope.omega) if rope else None, mp[0], mp[1], mp[2], 1 if rope else 0, eps, _s())
+         _p(rk), _p(rope.cs) if rope else None, rope.cs_batch_rows if rope else 0, B, N, D,
+         1 if rope else 0, eps, _s())
     return q_out, (k_out if k_in is not None else None), rq, rk
 
 
@@ -229,15 +239,13 @@ def qk_norm_rope_bwd(dq, q_raw, q_w, rq, dk=None, k_raw=None, k_w=None, rk=None,
         dk_out = torch.empty(M, D, dtype=BF16, device=dev)
     if rope is not None:
         B, N = rope.B, rope.N
-    mp = rope.max_pos if rope is not None else [1.0, 1.0, 1.0]
     call("ltx_qk_norm_rope_bwd", _p(dq), _rows(dq, "dq"), 1 if dq.dtype == F32 else 0, _p(dk),
          _rows(dk, "dk") if dk is not None else 0,
          1 if (dk is not None and dk.dtype == F32) else 0, _p(q_raw), _rows(q_raw, "q_raw"),
          _p(k_raw), _rows(k_raw, "k_raw") if k_raw is not None else 0, _p(q_w), _p(k_w), _p(rq),
          _p(rk), _p(dq_out), _rows(dq_out, "dq_out"), _p(dk_out),
-         _rows(dk_out, "dk_out") if dk is not None else 0, _p(rope.grid) if rope else None,
-         rope.is_float if rope else 0, B, N, D, _p(rope.omega) if rope else None, mp[0], mp[1],
-         mp[2], 1 if rope else 0, _s())
+         _rows(dk_out, "dk_out") if dk is not None else 0, _p(rope.cs) if rope else None,
+         rope.cs_batch_rows if rope else 0, B, N, D, 1 if rope else 0, _s())
     return dq_out, (dk_out if dk is not None else None)
 
 

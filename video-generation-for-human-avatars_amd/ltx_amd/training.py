@@ -46,7 +46,8 @@ def train_step(model, batch, scheduler, patchifier, config, prompt_embeds, promp
     N = F * H * W
     enc = prompt_embeds.expand(B, -1, -1).to(device=device, dtype=dt)
     enc_mask = prompt_attention_mask.expand(B, -1).to(device)
-    coords = patchifier.get_latent_coords(F, H, W, B, device)
+    # one coordinate set broadcast over the batch (identical per sample): one shared RoPE table
+    coords = patchifier.get_latent_coords(F, H, W, 1, device).expand(B, -1, -1)
     if t is None:
         t = sample_timesteps(B, config, "cpu").to(device)
         t = scheduler.shift_timesteps(torch.Size([B, N, C]), t)
