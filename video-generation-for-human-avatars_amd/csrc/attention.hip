@@ -76,32 +76,31 @@ __device__ __forceinline__ f32x16 mfma32(const s16x8& a, const s16x8& b, const f
 // row (in the register axis) of accumulator register r for lane half h
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// global 16-B loads of a [ROWS][HD] tile (rows clamped), staged in registers, written swizzled
+// global 16-B loads of a [ROWS][HD] tile, staged in registers, written swizzled. A thread moves
+// chunk c = tid % CH of rows tid / CH + i * RSTEP: its byte offsets inside a tile are constant,
+// so a tile is one scalar base (row0 * ld) + a 24-bit-multiply lane offset per load (no per-tile
+// 64-bit address math, no lane predicates); rows past a ragged end re-read the last row.
 template <int HD, int ROWS>
 struct TileStage {
   static constexpr int CH = HD / 8;
-  static constexpr int PER = (ROWS * CH + ATT_THREADS - 1) / ATT_THREADS;
+  static constexpr int PER = ROWS * CH / ATT_THREADS;
+  static constexpr int RSTEP = ATT_THREADS / CH;
+  static_assert(ROWS * CH % ATT_THREADS == 0, "a tile must split evenly over the workgroup");
   u32x4 v[PER];
   __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int row0, int nrows, int tid) {
+    const int r = tid / CH, c = tid % CH;
+    const char* tb = (const char*)(base + (int64_t)row0 * ld);  // wave-uniform
+    const int lim = nrows - 1 - row0;                             // rows past the end re-read the last
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int idx = tid + i * ATT_THREADS;
-      if (idx < ROWS * CH) {
-        const int r = idx / CH, c = idx % CH;
-        const int gr = min(row0 + r, nrows - 1);
-        v[i] = *(const u32x4*)(base + (int64_t)gr * ld + c * 8);
-      }
+      const uint32_t off = __umul24((uint32_t)min(r + i * RSTEP, lim), (uint32_t)(ld * 2)) + (uint32_t)(c * 16);
+      v[i] = *(const u32x4*)(tb + off);
     }
   }
   __device__ __forceinline__ void store(char* tile, int tid) const {
+    const int r = tid / CH, c = tid % CH;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int idx = tid + i * ATT_THREADS;
-      if (idx < ROWS * CH) {
-        const int r = idx / CH, c = idx % CH;
-        *(u32x4*)(tile + toff<HD>(r, c)) = v[i];
-      }
-    }
+    for (int i = 0; i < PER; ++i) *(u32x4*)(tile + toff<HD>(r + i * RSTEP, c)) = v[i];
   }
 };
 
@@ -141,6 +140,17 @@ __device__ __forceinline__ void key_bias_tile(float* kb, const AttnParams& p, in
 // whenever no lane's max grew (exact: alpha would be 1).
 // =============================================================================================
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// lane l and lane l ^ 32 combined without an LDS round trip (v_permlane32_swap): both halves
+// get the bit-identical result (same operand order in every lane)
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 template <int HD, int MODE, bool BIAS>
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams p) {
@@ -196,19 +206,38 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
   if (BIAS) key_bias_tile(kb, p, b, 0, KT, tid);
   __syncthreads();
 
+  // Retire every pre-loop global load (Q/dO/K/V fragments) with a counter wait hipcc can see:
+  // otherwise its loop-header merge keeps them "pending" and each in-loop use waits with a
+  // vmcnt that also drains the freshly issued tile prefetch.
+  __builtin_amdgcn_s_waitcnt(0);
   for (int t = 0; t < ntiles; ++t) {
     const int key0 = t * KT;
-    if (t + 1 < ntiles) {
+    if (t + 1 < ntiles) {  // next K/V tile -> registers, written to LDS after this tile
       ks_.load(kbase, p.ldk, key0 + KT, p.Nk, tid);
       vs_.load(vbase, p.ldv, key0 + KT, p.Nk, tid);
     }
     f32x16 s[2];
+    if constexpr (MODE == 1) {
+      s16x8 kf[2][KS];  // dQ: all K fragments in flight before the first MFMA
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
+        for (int ks = 0; ks < KS; ++ks) kf[u][ks] = row_frag<HD>(ktile, u * 32, ks, lane);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(ktile, u * 32, ks, lane), qf[ks], s[u]);
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(kf[u][ks], qf[ks], s[u]);
+      }
+    } else {  // forward: stay at <= 128 VGPRs (4 waves / SIMD)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(ktile, u * 32, ks, lane), qf[ks], s[u]);
+      }
     }
     if constexpr (MODE == 0) {
       float mt = -1e30f;
@@ -226,14 +255,14 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
             }
           }
       } else {
-        float mr = -3.0e38f;
+        float mr[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};  // 4 chains: ILP for v_max3
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) mr = fmaxf(mr, s[u][r]);
-        mt = mr * c2;
+          for (int r = 0; r < 16; ++r) mr[r & 3] = fmaxf(mr[r & 3], s[u][r]);
+        mt = fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3])) * c2;
       }
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      mt = xor32_max(mt);
       const float m_new = fmaxf(m_run, mt);
       if (__any(m_new > m_run)) {
         const float alpha = fast_exp2(m_run - m_new);
@@ -245,16 +274,16 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
         m_run = m_new;
       }
       const float nm = -m_run;
-      float ls = 0.f;
+      float ls[4] = {0.f, 0.f, 0.f, 0.f};  // 4 chains instead of one 32-deep dependent add chain
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float e = BIAS ? fast_exp2(s[u][r] + nm) : fast_exp2(fmaf(s[u][r], c2, nm));
           s[u][r] = e;
-          ls += e;
+          ls[r & 3] += e;
         }
-      l_run += ls;
+      l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -267,10 +296,13 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         f32x16 dp;
+        s16x8 vfr[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) vfr[ks] = row_frag<HD>(vtile, u * 32, ks, lane);
 #pragma unroll
         for (int r = 0; r < 16; ++r) dp[r] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) dp = mfma32(row_frag<HD>(vtile, u * 32, ks, lane), of[ks], dp);
+        for (int ks = 0; ks < KS; ++ks) dp = mfma32(vfr[ks], of[ks], dp);
         if constexpr (BIAS) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
@@ -308,7 +340,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
 
   if (qi >= p.Nq) return;
   if constexpr (MODE == 0) {
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float l_tot = xor32_sum(l_run);
     const float inv = 1.0f / l_tot;
     bf16_t* orow = p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD;
 #pragma unroll
@@ -413,6 +445,10 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   stage_stats(0);
   __syncthreads();
 
+  // Retire every pre-loop global load (Q/dO/K/V fragments) with a counter wait hipcc can see:
+  // otherwise its loop-header merge keeps them "pending" and each in-loop use waits with a
+  // vmcnt that also drains the freshly issued tile prefetch.
+  __builtin_amdgcn_s_waitcnt(0);
   for (int t = 0; t < ntiles; ++t) {
     const int qb = t * QT;
     if (t + 1 < ntiles) {
@@ -427,10 +463,16 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
         s[r] = 0.f;
         dp[r] = 0.f;
       }
+      s16x8 qfr[KS], ofr[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        s = mfma32(row_frag<HD>(qtile, u * 32, ks, lane), kf[ks], s);
-        dp = mfma32(row_frag<HD>(otile, u * 32, ks, lane), vf[ks], dp);
+        qfr[ks] = row_frag<HD>(qtile, u * 32, ks, lane);
+        ofr[ks] = row_frag<HD>(otile, u * 32, ks, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma32(qfr[ks], kf[ks], s);
+        dp = mfma32(ofr[ks], vf[ks], dp);
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
