@@ -179,22 +179,25 @@ int ltx_gemm_set_variant(int variant);
 /* ---- LoRA skinny contractions in f32 (peft lora_A / lora_B, training.py:50-68) --------------- */
 /* out[m,j] = alpha * sum_k x[m,k] * Wr[j,k], Wr element (j,k) at Wr[j*wj + k*wk]; x bf16 [M,K]
  * (ldx), out f32 [M,r] (ldo). lora_A forward (u = x.A^T: wj = K, wk = 1) and the lora_B dgrad
- * (w = s*dY.B with B f32 [N,r]: wj = 1, wk = r). r <= 32. */
+ * (w = s*dY.B with B f32 [N,r]: wj = 1, wk = r). r in {8, 16, 32}. When split != null the rows
+ * are also written as the activation K-extension operand (bf16 [M, K2], ld_split: role 0 of
+ * ltx_lora_split_bf16 with scale 1), saving that launch. */
 int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk,
                   float* out, int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha,
-                  void* stream);
+                  void* split, int64_t ld_split, int64_t K2, void* stream);
 /* 3-term bf16 split of an f32 [R, r] matrix (element (i,j) at src[i*rs + j*cs], times scale) into
  * a K-extension operand out [R, K2] (K2 = round_up(3r, 64)): role 0 (activation) rows
  * [hi|hi|lo|0], role 1 (weight) rows [hi|lo|hi|0]; their dot product reproduces the f32 product
  * to ~2^-16 relative. */
 int ltx_lora_split_bf16(const float* src, int64_t rs, int64_t cs, float scale, int64_t R,
                         int64_t r, int role, void* out, int64_t ldo, int64_t K2, void* stream);
-/* dW(n,j) = alpha * sum_m Y[m,n] * U[m,j], stored at dw[n*on + j*oj] (f32, overwritten):
+/* dW(n,j) (+)= alpha * sum_m Y[m,n] * U[m,j] at dw[n*on + j*oj] (f32; overwritten, or added to
+ * when accumulate != 0, e.g. straight into a .grad buffer across micro-steps):
  * lora_B grad (Y = dY, U = u: on = r, oj = 1) and lora_A grad (Y = x, U = w: on = 1, oj = K).
  * Y bf16 [M,N] (ldy), U f32 [M,r] (ldu). Split-M partial sums are combined with f32 atomics. */
 int ltx_lora_wgrad(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw,
                    int64_t on, int64_t oj, int64_t M, int64_t N, int64_t r, float alpha,
-                   void* stream);
+                   int accumulate, void* stream);
 
 /* ---- small ops -------------------------------------------------------------------------------- */
 /* AdaLayerNormSingle sinusoid: out[b,:] = bf16([cos(s*t*f), sin(s*t*f)]) (256 ch), s = scale */

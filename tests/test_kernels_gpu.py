@@ -306,14 +306,16 @@ def test_timestep_silu_transpose_colsum():
     assert rel(cs, x.float().sum(0)) < 5e-3
 
 
-def test_lora_kernels():
+@pytest.mark.parametrize("M,r", [(1000, 16), (2048, 16), (333, 8), (517, 32)])
+def test_lora_kernels(M, r):
     from ltx_amd import ops
-    M, K, N, r = 1000, 2048, 2048, 16
+    K, N = 2048, 2048
     x = g(M, K, seed=1)
     A = torch.randn(r, K, device=DEV) / K ** 0.5
     Bm = torch.randn(N, r, device=DEV) * 0.05
-    u = ops.lora_down(x, A)
+    u, su = ops.lora_down(x, A, split=True)
     assert rel(u, x.float() @ A.t()) < 1e-5
+    assert torch.equal(su, ops.lora_split(u, "act"))  # fused split == standalone split
     dy = g(M, N, seed=2)
     w = ops.lora_down(dy, Bm, alpha=0.5, transposed=True)
     assert rel(w, 0.5 * dy.float() @ Bm) < 1e-5
@@ -321,6 +323,11 @@ def test_lora_kernels():
     assert rel(dB, 0.5 * dy.float().t() @ u) < 1e-5
     dA = ops.lora_wgrad(x, w, transpose_out=True)
     assert rel(dA, w.t() @ x.float()) < 1e-5
+    # accumulate into an existing buffer (the .grad path): buf + product
+    buf = torch.randn(N, r, device=DEV)
+    ref = buf + 0.5 * dy.float().t() @ u
+    ops.lora_wgrad(dy, u, alpha=0.5, out=buf, accumulate=True)
+    assert rel(buf, ref) < 1e-5
 
 
 def test_mse_and_adamw():

@@ -5,6 +5,8 @@
 // which keeps the adapters' f32 semantics while freeing the VALU for address math.
 // The up-projection (B) and its input-gradient half are fused into the bf16 GEMM epilogues
 // (gemm.hip: LTX_EPI_LORA / LTX_EPI_LORA_DGRAD_ACCUM).
+#include <type_traits>
+
 #include "common.h"
 #include "ltx_hip.h"
 
@@ -14,134 +16,193 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// out[m,j] = alpha * sum_k x[m,k] * Wr[j*wj + k*wk]
-// Block = 4 waves on the same 16 rows, K split 4 ways (grid = M/16 blocks); per 32-deep k chunk
-// a lane loads 8 consecutive k of its row (one 16-B load) and of its j row, and issues 8 MFMAs
-// whose k index g = lane>>4 stands for k = kb + 8g + i (the same permutation on both operands).
-// The 4 partial 16 x r tiles are summed through LDS.
-template <int R>
-__global__ __launch_bounds__(256) void lora_down_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+// out[m,j] = alpha * sum_k x[m,k] * Wr[j*wj + k*wk]   (+ optional activation split, below)
+// Block = 4 waves on the same 32 rows (two 16-row groups), K split 4 ways; for small M (text
+// tokens) 8 waves on 16 rows, K split 8 ways, to fill the chip (K % 128 / % 256; the
+// loads of 4 k steps go out together). Per 32-deep k step a
+// lane loads 8 consecutive k of its row (one 16-B load per row group) and the 8 matching weights
+// of its j, and issues 8 MFMAs whose k index g = lane>>4 stands for k = kb + 8g + i (the same
+// permutation on both operands); one weight fetch serves both row groups. The 4 partial 32 x r
+// tiles are summed through LDS. With split != null the row is also written as the K-extension
+// activation operand [hi | hi | lo | 0..] (bf16, K2 columns) of the LoRA-fused GEMM.
+template <int R, int RG, int KW>
+__global__ __launch_bounds__(64 * KW) void lora_down_kernel(const bf16_t* __restrict__ x, int64_t ldx,
                                                         const float* __restrict__ Wr, int64_t wj, int64_t wk,
                                                         float* __restrict__ out, int64_t ldo, int M, int K,
-                                                        float alpha) {
-  constexpr int JT = R / 16;  // 16-wide j tiles (R in {16, 32}); R = 8 runs as a padded tile
-  constexpr int JTT = JT > 0 ? JT : 1;
-  __shared__ float part[4][16][R >= 16 ? R : 16];
+                                                        float alpha, bf16_t* __restrict__ split, int64_t lds,
+                                                        int K2) {
+  constexpr int RP = R >= 16 ? R : 16;  // R = 8 runs as a padded 16-wide tile
+  constexpr int JT = RP / 16;
+  // RG = 16-row groups per block: 2 (one weight fetch serves 32 rows) when there are rows enough
+  // to fill the chip, else 1
+  __shared__ float part[KW][16 * RG][RP + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m0 = blockIdx.x * 16;
-  const int row = min(m0 + (lane & 15), M - 1);
+  const int m0 = blockIdx.x * 16 * RG;
   const int g = lane >> 4;
-  const int kper = K / 4;
+  const int kper = K / KW;
   const int kbeg = wave * kper, kend = kbeg + kper;
-  f32x4 acc[JTT];
+  f32x4 acc[RG][JT];
 #pragma unroll
-  for (int t = 0; t < JTT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const bf16_t* xr = x + (int64_t)row * ldx;
-  for (int kb = kbeg; kb < kend; kb += 32) {
-    const int k = kb + 8 * g;
-    const u32x4 xv = *(const u32x4*)(xr + k);
-    float xf[8];
+  for (int q = 0; q < RG; ++q)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xf[i] = bf2f((bf16_t)(xv[i >> 1] >> ((i & 1) * 16)));
+    for (int t = 0; t < JT; ++t) acc[q][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const bf16_t* xr[RG];
 #pragma unroll
-    for (int t = 0; t < JTT; ++t) {
-      const int j = t * 16 + (lane & 15);
-      float wv[8];
-      if (j < R) {
-        const float* wp = Wr + (int64_t)j * wj + (int64_t)k * wk;
-        if (wk == 1) {
-          const f32x4 a = *(const f32x4*)wp, b = *(const f32x4*)(wp + 4);
+  for (int q = 0; q < RG; ++q) xr[q] = x + (int64_t)min(m0 + 16 * q + (lane & 15), M - 1) * ldx;
+  // NS x 32 k per call: all x and weight loads of the NS sub-steps issued before their MFMAs
+  auto kstep = [&](auto ns_tag, int kb) {
+    constexpr int NS = decltype(ns_tag)::value;
+    u32x4 xv[NS][RG];
+    float wv[NS][JT][8];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) { wv[i] = a[i]; wv[4 + i] = b[i]; }
+    for (int st = 0; st < NS; ++st) {
+      const int k = kb + 32 * st + 8 * g;
+#pragma unroll
+      for (int q = 0; q < RG; ++q) xv[st][q] = *(const u32x4*)(xr[q] + k);
+#pragma unroll
+      for (int t = 0; t < JT; ++t) {
+        const int j = t * 16 + (lane & 15);
+        if (j < R) {
+          const float* wp = Wr + (int64_t)j * wj + (int64_t)k * wk;
+          if (wk == 1) {
+            const f32x4 a = *(const f32x4*)wp, b = *(const f32x4*)(wp + 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { wv[st][t][i] = a[i]; wv[st][t][4 + i] = b[i]; }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) wv[st][t][i] = wp[(int64_t)i * wk];
+          }
         } else {
 #pragma unroll
-          for (int i = 0; i < 8; ++i) wv[i] = wp[(int64_t)i * wk];
+          for (int i = 0; i < 8; ++i) wv[st][t][i] = 0.f;
         }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wv[i] = 0.f;
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[t] = mfma4(xf[i], wv[i], acc[t]);
     }
-  }
+#pragma unroll
+    for (int st = 0; st < NS; ++st)
+#pragma unroll
+      for (int q = 0; q < RG; ++q)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float xf = bf2f((bf16_t)(xv[st][q][i >> 1] >> ((i & 1) * 16)));
+#pragma unroll
+          for (int t = 0; t < JT; ++t) acc[q][t] = mfma4(xf, wv[st][t][i], acc[q][t]);
+        }
+  };
+  int kb = kbeg;
+  for (; kb + 128 <= kend; kb += 128) kstep(std::integral_constant<int, 4>{}, kb);
+  for (; kb < kend; kb += 32) kstep(std::integral_constant<int, 1>{}, kb);
   // C layout: col j = lane & 15 (+16t), row m = (lane >> 4) * 4 + reg
 #pragma unroll
-  for (int t = 0; t < JTT; ++t)
+  for (int q = 0; q < RG; ++q)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int j = t * 16 + (lane & 15);
-      if (j < (R >= 16 ? R : 16)) part[wave][(lane >> 4) * 4 + rr][j] = acc[t][rr];
-    }
+    for (int t = 0; t < JT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) part[wave][16 * q + (lane >> 4) * 4 + rr][t * 16 + (lane & 15)] = acc[q][t][rr];
   __syncthreads();
-  for (int e = threadIdx.x; e < 16 * R; e += 256) {
+  for (int e = threadIdx.x; e < 16 * RG * R; e += 64 * KW) {
     const int rr = e / R, j = e % R;
     const int m = m0 + rr;
-    if (m < M) out[(int64_t)m * ldo + j] = (part[0][rr][j] + part[1][rr][j] + part[2][rr][j] + part[3][rr][j]) * alpha;
+    if (m >= M) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < KW; ++w) sum += part[w][rr][j];
+    const float v = sum * alpha;
+    out[(int64_t)m * ldo + j] = v;
+    if (split) {
+      const bf16_t hi = f2bf(v);
+      const bf16_t lo = f2bf(v - bf2f(hi));
+      bf16_t* sr = split + (int64_t)m * lds;
+      sr[j] = hi;
+      sr[R + j] = hi;
+      sr[2 * R + j] = lo;
+    }
+  }
+  if (split) {  // zero padding columns 3R .. K2
+    const int pad = K2 - 3 * R;
+    for (int e = threadIdx.x; e < 16 * RG * pad; e += 64 * KW) {
+      const int rr = e / pad, c = 3 * R + e % pad;
+      const int m = m0 + rr;
+      if (m < M) split[(int64_t)m * lds + c] = (bf16_t)0;
+    }
   }
 }
 
-// dw(n,j) += alpha * sum_{m in split} y[m,n] * u[m,j]  (f32 atomics across splits)
-// Block = 4 waves x 16 columns n; rows streamed in 64-row tiles through LDS (y as bf16, u as
-// f32); per 4 rows one MFMA per 16-wide j tile: A = y^T [16 n x 4 m], B = u [4 m x 16 j].
+// dw(n,j) (+)= alpha * sum_m y[m,n] * u[m,j]   (f32 atomics across row splits)
+// Computed as C[j][n] += U^T[j][m] . Y[m][n] on v_mfma_f32_16x16x4_f32: per 4 rows a lane loads
+// u[m][j] (4 B) and 8 consecutive columns of y (one 16-B load; 16 lanes = 128 columns, 256 B
+// per row), and MFMA t (t = 0..7) takes element t, so its output column c stands for
+// n0 + 8c + t (a fixed permutation undone at the store). Block = 8 waves on the same 128
+// columns, interleaved row quads; the wave partials are reduced through LDS, then one atomic
+// per output element and block.
 template <int R>
-__global__ __launch_bounds__(256) void lora_wgrad_kernel(const bf16_t* __restrict__ y, int64_t ldy,
+__global__ __launch_bounds__(512) void lora_wgrad_kernel(const bf16_t* __restrict__ y, int64_t ldy,
                                                          const float* __restrict__ u, int64_t ldu,
                                                          float* __restrict__ dw, int64_t on, int64_t oj, int M,
                                                          int N, int rows_per_split, float alpha) {
   constexpr int RP = R >= 16 ? R : 16;
   constexpr int JT = RP / 16;
-  __shared__ bf16_t ys[64][64 + 2];
-  __shared__ float us[64][RP + 1];
+  constexpr int NW = 8;  // waves per block, interleaved over row quads
+  __shared__ float red[NW][RP][128 + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * 64;
+  const int n0 = blockIdx.x * 128;
   const int mb = blockIdx.y * rows_per_split;
   const int me = min(M, mb + rows_per_split);
-  f32x4 acc[JT];
-#pragma unroll
-  for (int t = 0; t < JT; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int m0 = mb; m0 < me; m0 += 64) {
-    // stage y[64 rows][64 cols]: 256 threads x 16 elements (two 16-B loads)
-    {
-      const int r = tid >> 2, c = (tid & 3) * 16;
-      const int m = m0 + r;
-      u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-      if (m < me && n0 + c < N) {
-        const bf16_t* p = y + (int64_t)m * ldy + n0 + c;
-        a = *(const u32x4*)p;
-        if (n0 + c + 8 < N) b = *(const u32x4*)(p + 8);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        ys[r][c + 2 * i] = (bf16_t)a[i];
-        ys[r][c + 2 * i + 1] = (bf16_t)(a[i] >> 16);
-        ys[r][c + 8 + 2 * i] = (bf16_t)b[i];
-        ys[r][c + 8 + 2 * i + 1] = (bf16_t)(b[i] >> 16);
-      }
-    }
-    for (int e = tid; e < 64 * RP; e += 256) {
-      const int r = e / RP, j = e % RP;
-      const int m = m0 + r;
-      us[r][j] = (m < me && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll 4
-    for (int mm = 0; mm < 64; mm += 4) {
-      const float a = bf2f(ys[mm + (lane >> 4)][wave * 16 + (lane & 15)]);
-#pragma unroll
-      for (int t = 0; t < JT; ++t) acc[t] = mfma4(a, us[mm + (lane >> 4)][t * 16 + (lane & 15)], acc[t]);
-    }
-    __syncthreads();
-  }
-  // C: row n = wave*16 + (lane>>4)*4 + reg, col j = t*16 + (lane&15)
+  const int c8 = n0 + 8 * (lane & 15);  // this lane's 8 columns
+  const bool colok = c8 < N;            // N % 8 == 0: all 8 in or all out
+  f32x4 acc[JT][8];
 #pragma unroll
   for (int t = 0; t < JT; ++t)
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int n = n0 + wave * 16 + (lane >> 4) * 4 + rr;
-      const int j = t * 16 + (lane & 15);
-      if (n < N && j < R) atomicAdd(dw + (int64_t)n * on + (int64_t)j * oj, acc[t][rr] * alpha);
+    for (int i = 0; i < 8; ++i) acc[t][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // each wave takes row quads mb + 4*wave + 32*i; four quads' loads are issued before their
+  // 32 MFMAs so every wave keeps 4 x 1 KiB of y in flight
+  for (int m16 = mb + 4 * wave; m16 < me; m16 += 4 * 4 * NW) {
+    u32x4 yv[4];
+    float uv[4][JT];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = m16 + 4 * NW * q + (lane >> 4);
+      const bool rowok = m < me;
+      yv[q] = (u32x4){0, 0, 0, 0};
+      if (rowok && colok) yv[q] = *(const u32x4*)(y + (int64_t)m * ldy + c8);
+#pragma unroll
+      for (int t = 0; t < JT; ++t) {
+        const int j = t * 16 + (lane & 15);
+        uv[q][t] = (rowok && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
+      }
     }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float yf = bf2f((bf16_t)(yv[q][i >> 1] >> ((i & 1) * 16)));
+#pragma unroll
+        for (int t = 0; t < JT; ++t) acc[t][i] = mfma4(uv[q][t], yf, acc[t][i]);
+      }
+  }
+  // C_t,i: row j = t*16 + (lane>>4)*4 + rr, col c = lane & 15 -> n = n0 + 8c + i
+#pragma unroll
+  for (int t = 0; t < JT; ++t)
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[wave][t * 16 + (lane >> 4) * 4 + rr][8 * (lane & 15) + i] = acc[t][i][rr];
+  __syncthreads();
+  // consecutive threads -> consecutive output addresses (j fastest when the output is [N, r])
+  const bool jfast = (oj == 1);
+  for (int e = tid; e < R * 128; e += 64 * NW) {
+    const int j = jfast ? e % R : e / 128;
+    const int c = jfast ? e / R : e % 128;
+    const int n = n0 + c;
+    if (n < N) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) sum += red[w][j][c];
+      const float v = sum * alpha;
+      atomicAdd(dw + (int64_t)n * on + (int64_t)j * oj, v);
+    }
+  }
 }
 
 // 3-term bf16 split of an f32 [R, r] operand for the K-extension LoRA fusion: with
@@ -185,42 +246,63 @@ extern "C" int ltx_lora_split_bf16(const float* src, int64_t rs, int64_t cs, flo
 }
 
 extern "C" int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk, float* out,
-                             int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha, void* stream) {
+                             int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha, void* split,
+                             int64_t ld_split, int64_t K2, void* stream) {
   LTX_CHECK_ARG(x && Wr && out && M > 0 && K > 0, "lora_down: bad args");
+  LTX_CHECK_ARG(!split || (K2 >= 3 * r && K2 % 64 == 0 && ld_split >= K2), "lora_down: split needs K2 >= 3r, %64");
   LTX_CHECK_ARG(K % 128 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0, "lora_down: K %128, 16-B rows");
   LTX_CHECK_ARG(wk != 1 || (wj % 4 == 0 && ((uintptr_t)Wr % 16) == 0), "lora_down: W rows must be 16-B aligned");
-  const dim3 grid((unsigned)((M + 15) / 16));
+  const bool big = M >= 8192;
+  const dim3 grid((unsigned)(big ? (M + 31) / 32 : (M + 15) / 16));
   hipStream_t s = (hipStream_t)stream;
+  bf16_t* sp = (bf16_t*)split;
+#define LTX_LORA_DOWN(RR)                                                                                      \
+  if (big)                                                                                                     \
+    hipLaunchKernelGGL((lora_down_kernel<RR, 2, 4>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk,  \
+                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);                                \
+  else if (K % 256 == 0)                                                                                       \
+    hipLaunchKernelGGL((lora_down_kernel<RR, 1, 8>), grid, dim3(512), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk,  \
+                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);                                \
+  else                                                                                                         \
+    hipLaunchKernelGGL((lora_down_kernel<RR, 1, 4>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk,  \
+                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);
   switch (r) {
-    case 8: hipLaunchKernelGGL(lora_down_kernel<8>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk, out, ldo, (int)M, (int)K, alpha); break;
-    case 16: hipLaunchKernelGGL(lora_down_kernel<16>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk, out, ldo, (int)M, (int)K, alpha); break;
-    case 32: hipLaunchKernelGGL(lora_down_kernel<32>, grid, dim3(256), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk, out, ldo, (int)M, (int)K, alpha); break;
+    case 8: LTX_LORA_DOWN(8) break;
+    case 16: LTX_LORA_DOWN(16) break;
+    case 32: LTX_LORA_DOWN(32) break;
     default: return fail(LTX_ERR_BAD_ARG, "lora_down: rank must be 8, 16 or 32");
   }
+#undef LTX_LORA_DOWN
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
 
 extern "C" int ltx_lora_wgrad(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw, int64_t on,
-                              int64_t oj, int64_t M, int64_t N, int64_t r, float alpha, void* stream) {
+                              int64_t oj, int64_t M, int64_t N, int64_t r, float alpha, int accumulate,
+                              void* stream) {
   LTX_CHECK_ARG(y && u && dw && M > 0 && N > 0, "lora_wgrad: bad args");
   LTX_CHECK_ARG((on == r && oj == 1) || (on == 1 && oj == N), "lora_wgrad: output must be a dense [N,r] or [r,N]");
   LTX_CHECK_ARG(N % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0, "lora_wgrad: y rows must be 16-B aligned");
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(dw, 0, (size_t)N * r * sizeof(float), s);
-  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
-  const int nb = (int)((N + 63) / 64);
-  int splits = (int)((1024 + nb - 1) / nb);
-  const int max_splits = (int)((M + 63) / 64);
+  if (!accumulate) {
+    hipError_t e = hipMemsetAsync(dw, 0, (size_t)N * r * sizeof(float), s);
+    if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  }
+  // <= ~256 blocks of 128 columns x >= 512 rows (8 waves x 4-quad steps): enough waves to stream
+  // y while keeping the f32 atomics (128 * r per block) small
+  const int nb = (int)((N + 127) / 128);
+  int splits = (int)((256 + nb - 1) / nb);
+  const int max_splits = (int)((M + 511) / 512);
   if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
   int rps = (int)((M + splits - 1) / splits);
-  rps = (rps + 63) / 64 * 64;
+  rps = (rps + 127) / 128 * 128;
   splits = (int)((M + rps - 1) / rps);
   const dim3 grid((unsigned)nb, (unsigned)splits);
   switch (r) {
-    case 8: hipLaunchKernelGGL(lora_wgrad_kernel<8>, grid, dim3(256), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
-    case 16: hipLaunchKernelGGL(lora_wgrad_kernel<16>, grid, dim3(256), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
-    case 32: hipLaunchKernelGGL(lora_wgrad_kernel<32>, grid, dim3(256), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
+    case 8: hipLaunchKernelGGL(lora_wgrad_kernel<8>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
+    case 16: hipLaunchKernelGGL(lora_wgrad_kernel<16>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
+    case 32: hipLaunchKernelGGL(lora_wgrad_kernel<32>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
     default: return fail(LTX_ERR_BAD_ARG, "lora_wgrad: rank must be 8, 16 or 32");
   }
   LTX_LAUNCH_CHECK();

@@ -49,8 +49,9 @@ _SIGNATURES = {
     "ltx_gemm_bf16_nt_ext": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64,
                              _i64, _i32, _p, _p, _i64, _p, _i64, _p, _i64, _f32, _i64, _i64, _p],
     "ltx_lora_split_bf16": [_p, _i64, _i64, _f32, _i64, _i64, _i32, _p, _i64, _i64, _p],
-    "ltx_lora_down": [_p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _f32, _p],
-    "ltx_lora_wgrad": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p],
+    "ltx_lora_down": [_p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _f32, _p, _i64, _i64,
+                      _p],
+    "ltx_lora_wgrad": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f32, _i32, _p],
     "ltx_timestep_embedding": [_p, _f32, _p, _i64, _i64, _p],
     "ltx_silu_bf16": [_p, _p, _i64, _p],
     "ltx_transpose_bf16": [_p, _i64, _p, _i64, _i64, _i64, _p],

@@ -334,9 +334,11 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
     return out
 
 
-def lora_down(x, wr, alpha=1.0, transposed=False, out=None):
+def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False):
     """out[m,j] = alpha * x[m,:] . Wr[j,:]; Wr = lora_A [r,K]; transposed=True takes lora_B [K,r]
-    (i.e. uses B^T) for the dgrad w = s * dY . B."""
+    (i.e. uses B^T) for the dgrad w = s * dY . B. split=True also returns the activation
+    K-extension operand of the rows (what lora_split(out, "act") makes), written by the same
+    kernel."""
     M, K = x.shape
     if transposed:
         r = wr.shape[1]
@@ -345,9 +347,27 @@ def lora_down(x, wr, alpha=1.0, transposed=False, out=None):
         r = wr.shape[0]
         wj, wk = wr.stride(0), 1
     out = torch.empty(M, r, dtype=F32, device=x.device) if out is None else out
+    sp, K2 = None, 0
+    if split:
+        K2 = lora_k2(r)
+        sp = torch.empty(M, K2, dtype=BF16, device=x.device)
     call("ltx_lora_down", _p(x), _rows(x, "x"), _p(wr), wj, wk, _p(out), _rows(out, "out"), M, K, r,
-         float(alpha), _s())
-    return out
+         float(alpha), _p(sp), K2, K2, _s())
+    return (out, sp) if split else out
+
+
+_WEIGHT_GENERATION = [0]
+
+
+def weight_generation():
+    """Counter bumped by every FusedAdamW step: its kernel updates parameters in place without
+    touching torch's version counters, so caches keyed on weights (LoRA operand splits) also
+    key on this."""
+    return _WEIGHT_GENERATION[0]
+
+
+def bump_weight_generation():
+    _WEIGHT_GENERATION[0] += 1
 
 
 def lora_k2(r):
@@ -370,19 +390,20 @@ def lora_split(src, role, scale=1.0, transposed=False, out=None):
     return out
 
 
-def lora_wgrad(y, u, alpha=1.0, transpose_out=False):
-    """dW[n,j] = alpha * sum_m y[m,n] u[m,j] -> [N,r] (or [r,N] when transpose_out)."""
+def lora_wgrad(y, u, alpha=1.0, transpose_out=False, out=None, accumulate=False):
+    """dW[n,j] = alpha * sum_m y[m,n] u[m,j] -> [N,r] (or [r,N] when transpose_out). With
+    out/accumulate the product is added into an existing dense f32 buffer (e.g. p.grad)."""
     M, N = y.shape
     r = u.shape[1]
-    if transpose_out:
-        dw = torch.empty(r, N, dtype=F32, device=y.device)
-        on, oj = 1, N
-    else:
-        dw = torch.empty(N, r, dtype=F32, device=y.device)
-        on, oj = r, 1
-    call("ltx_lora_wgrad", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(dw), on, oj, M, N, r,
-         float(alpha), _s())
-    return dw
+    shape = (r, N) if transpose_out else (N, r)
+    if out is None:
+        out = torch.empty(shape, dtype=F32, device=y.device)
+        accumulate = False
+    assert tuple(out.shape) == shape and out.dtype == F32 and out.is_contiguous()
+    on, oj = (1, N) if transpose_out else (r, 1)
+    call("ltx_lora_wgrad", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(out), on, oj, M, N, r,
+         float(alpha), 1 if accumulate else 0, _s())
+    return out
 
 
 # ---------------------------------------------------------------------------------------------

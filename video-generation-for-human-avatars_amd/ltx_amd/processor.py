@@ -32,10 +32,8 @@ class HipAttnProcessor:
             w, b, lora = _lin(lin)
             if lora is None:
                 return ops.gemm(inp, w, bias=b)
-            u = ops.lora_down(inp, lora.lora_A["default"].weight)
-            return ops.gemm(inp, w, bias=b, ext=(ops.lora_split(u, "act"),
-                                                 ops.lora_split(lora.lora_B["default"].weight,
-                                                                "weight", lora.scaling)))
+            _, su = ops.lora_down(inp, lora.lora_A["default"].weight, split=True)
+            return ops.gemm(inp, w, bias=b, ext=(su, lora.weight_split("B")))
 
         q_raw = proj(attn.to_q, x)
         k_raw = proj(attn.to_k, e)

@@ -94,6 +94,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 st["step"] += 1
                 ops.adamw_step(p, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], group["lr"],
                                b1, b2, group["eps"], group["weight_decay"], st["step"])
+        ops.bump_weight_generation()  # in-place kernel updates: invalidate weight-derived caches
 
 
 class GradAllReduce:

@@ -101,6 +101,23 @@ class LoraLinear(nn.Module):
                                                           device=dev, dtype=torch.float32)})
         nn.init.kaiming_uniform_(self.lora_A["default"].weight, a=math.sqrt(5))
         nn.init.zeros_(self.lora_B["default"].weight)
+        self._split_cache = {}
+
+    def weight_split(self, which):
+        """Cached K-extension weight operands (3-term bf16 split, ltx_lora_split_bf16):
+        'B' -> s*B for the forward GEMM, 'A' -> A^T for the input-gradient GEMM. Rebuilt when
+        the adapter changes: new storage, an in-place torch update (version counter) or a
+        FusedAdamW step (ops.weight_generation())."""
+        p = self.lora_B["default"].weight if which == "B" else self.lora_A["default"].weight
+        key = (p.data_ptr(), p._version, ops.weight_generation())
+        hit = self._split_cache.get(which)
+        if hit is None or hit[0] != key:
+            with torch.no_grad():
+                t = (ops.lora_split(p, "weight", self.scaling) if which == "B"
+                     else ops.lora_split(p, "weight", transposed=True))
+            hit = (key, t)
+            self._split_cache[which] = hit
+        return hit[1]
 
     @property
     def weight(self):
@@ -317,6 +334,15 @@ def _lora_params(blk):
     return lins
 
 
+def _grad_buf(lin, which):
+    """The .grad of a LoraLinear adapter weight ('A' or 'B'), created zeroed on first use: the
+    LoRA wgrad kernels add into it directly (no per-micro-step buffer, memset or add)."""
+    p = lin.lora_A["default"].weight if which == "A" else lin.lora_B["default"].weight
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+    return p.grad
+
+
 class _BlockFn(torch.autograd.Function):
     """One BasicTransformerBlock.forward (attention.py:198-321) + its backward."""
 
@@ -350,15 +376,13 @@ class _BlockFn(torch.autograd.Function):
         if has_lora:
             # peft LoRA fused into the K loop: [x | split(x.A^T)] . [W | split(s*B)]^T
             Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo = lora_ab
-            u_q = ops.lora_down(h1, Aq)
-            q2raw = ops.gemm(h1, wq, bias=bq,
-                             ext=(ops.lora_split(u_q, "act"), ops.lora_split(Bq, "weight", s)))
-            u_k = ops.lora_down(enc2, Ak)
-            k2raw = ops.gemm(enc2, wk, bias=bk,
-                             ext=(ops.lora_split(u_k, "act"), ops.lora_split(Bk, "weight", s)))
-            u_v = ops.lora_down(enc2, Av)
-            v2 = ops.gemm(enc2, wv, bias=bv,
-                          ext=(ops.lora_split(u_v, "act"), ops.lora_split(Bv, "weight", s)))
+            u_q, su = ops.lora_down(h1, Aq, split=True)
+            q2raw = ops.gemm(h1, wq, bias=bq, ext=(su, lora[0].weight_split("B")))
+            u_k, su = ops.lora_down(enc2, Ak, split=True)
+            k2raw = ops.gemm(enc2, wk, bias=bk, ext=(su, lora[1].weight_split("B")))
+            u_v, su = ops.lora_down(enc2, Av, split=True)
+            v2 = ops.gemm(enc2, wv, bias=bv, ext=(su, lora[2].weight_split("B")))
+            del su
         else:
             u_q = u_k = u_v = None
             q2raw = ops.gemm(h1, wq, bias=bq)
@@ -368,9 +392,10 @@ class _BlockFn(torch.autograd.Function):
         k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, a2.k_norm.weight, None, None, B=B, N=L)
         o2, lse2 = ops.attn_fwd(q2, k2, v2, B, H, d, a2.scale, key_bias=sh.enc_bias)
         if has_lora:
-            u_o = ops.lora_down(o2, Ao)
+            u_o, su = ops.lora_down(o2, Ao, split=True)
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1,
-                          ext=(ops.lora_split(u_o, "act"), ops.lora_split(Bo, "weight", s)))
+                          ext=(su, lora[3].weight_split("B")))
+            del su
         else:
             u_o = None
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1)
@@ -419,11 +444,11 @@ class _BlockFn(torch.autograd.Function):
         del dx2
         # ---- attn2: h2 = h1 + to_out(o2)   (LoRA grads: peft f32 adapters)
         if has_lora:
-            dBo = ops.lora_wgrad(dh2, u_o, alpha=s)
-            w_o = ops.lora_down(dh2, Bo, alpha=s, transposed=True)
-            dAo = ops.lora_wgrad(o2, w_o, transpose_out=True)
-            do2 = ops.gemm(dh2, W["o2_wT"], ext=(ops.lora_split(w_o, "act"),
-                                                 ops.lora_split(Ao, "weight", transposed=True)))
+            lq, lk, lv, lo = lora
+            ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
+            w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True)
+            ops.lora_wgrad(o2, w_o, transpose_out=True, out=_grad_buf(lo, "A"), accumulate=True)
+            do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")))
         else:
             do2 = ops.gemm(dh2, W["o2_wT"])
         dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
@@ -433,22 +458,24 @@ class _BlockFn(torch.autograd.Function):
         dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=B, N=L)
         del dq2, dk2
         if has_lora:
-            dBq = ops.lora_wgrad(dq2raw, u_q, alpha=s)
-            w_q = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True)
-            dAq = ops.lora_wgrad(h1, w_q, transpose_out=True)
+            ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
+            w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True)
+            ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
-                           ext=(ops.lora_split(w_q, "act"), ops.lora_split(Aq, "weight", transposed=True)))
-            dBk = ops.lora_wgrad(dk2raw, u_k, alpha=s)
-            w_k = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True)
-            dAk = ops.lora_wgrad(enc2, w_k, transpose_out=True)
-            denc = ops.gemm(dk2raw, W["k2_wT"], ext=(ops.lora_split(w_k, "act"),
-                                                     ops.lora_split(Ak, "weight", transposed=True)))
-            dBv = ops.lora_wgrad(dv2, u_v, alpha=s)
-            w_v = ops.lora_down(dv2, Bv, alpha=s, transposed=True)
-            dAv = ops.lora_wgrad(enc2, w_v, transpose_out=True)
+                           ext=(sw, lq.weight_split("A")))
+            ops.lora_wgrad(dk2raw, u_k, alpha=s, out=_grad_buf(lk, "B"), accumulate=True)
+            w_k, sw = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True, split=True)
+            ops.lora_wgrad(enc2, w_k, transpose_out=True, out=_grad_buf(lk, "A"), accumulate=True)
+            denc = ops.gemm(dk2raw, W["k2_wT"], ext=(sw, lk.weight_split("A")))
+            ops.lora_wgrad(dv2, u_v, alpha=s, out=_grad_buf(lv, "B"), accumulate=True)
+            w_v, sw = ops.lora_down(dv2, Bv, alpha=s, transposed=True, split=True)
+            ops.lora_wgrad(enc2, w_v, transpose_out=True, out=_grad_buf(lv, "A"), accumulate=True)
             ops.gemm(dv2, W["v2_wT"], epilogue="accum", aux0=denc, out=denc,
-                     ext=(ops.lora_split(w_v, "act"), ops.lora_split(Av, "weight", transposed=True)))
-            grads_lora = [dAq, dBq, dAk, dBk, dAv, dBv, dAo, dBo]
+                     ext=(sw, lv.weight_split("A")))
+            del sw
+            # the adapter gradients went straight into .grad (accumulated across micro-steps by
+            # the kernels' atomics); autograd gets None for them
+            grads_lora = [None] * 8
         else:
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2)
             denc = ops.gemm(dk2raw, W["k2_wT"])
