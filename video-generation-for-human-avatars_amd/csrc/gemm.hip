@@ -332,6 +332,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
   constexpr bool DBG_NOBAR = (VAR & 8) != 0;   // measurement only: and no mid-loop wait/barrier
   constexpr bool DBG_NOWAIT = (VAR & 16) != 0; // measurement only: DMA issued, never waited for in the loop
   constexpr bool ASMDMA = (VAR & 32) != 0;     // scalar-base + 32-bit offset LDS-DMA (inline asm)
+  constexpr bool INTERLEAVE = ASMDMA && SPLIT && (VAR & 64) != 0;  // one DMA piece per 4 MFMAs
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -426,6 +427,17 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
       for (int i = 0; i < 4; ++i) glds16(wptr(i, kt), base + XT2 + (wave * 4 + i) * 1024);
     }
   };
+  // one 1 KiB piece of a stage (ASMDMA): INTERLEAVE spreads a stage's 4 pieces between MFMA rows
+  auto piece_x = [&](int st, int kt, int i) {
+    if (i == 0 && kt == nk_main && nk_main > 0) set_x(true);
+    const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
+    glds_s(xo[i], sb, lds0 + st * ST2 + wv * 4096 + i * 1024);
+  };
+  auto piece_w = [&](int st, int kt, int i) {
+    if (i == 0 && kt == nk_main && nk_main > 0) set_w(true);
+    const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
+    glds_s(wo[i], sb, lds0 + st * ST2 + XT2 + wv * 4096 + i * 1024);
+  };
   auto stage = [&](int st, int kt) {
     stage_x(st, kt);
     stage_w(st, kt);
@@ -472,6 +484,18 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
     acc[(NH) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * 4 + i][j], 0, 0, 0); \
   if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(0);                                                \
   __builtin_amdgcn_sched_barrier(0);
+#define LTX_MFMA_QI(AS, BS, NH, PIECE)                                                                \
+  __builtin_amdgcn_sched_barrier(0);                                                                  \
+  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(1);                                                \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                     \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                     \
+      acc[(NH) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * 4 + i][j], 0, 0, 0); \
+    __builtin_amdgcn_sched_barrier(0);                                                                \
+    PIECE(i);                                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                                                \
+  }                                                                                                   \
+  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(0);                                                \
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (SPRIO) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   }
@@ -483,11 +507,20 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
     // Q0 (h0, n0): prefetch A(Q1)
 #pragma unroll
     for (int i = 0; i < 4; ++i) aO[i] = *(const s16x8*)(st + aoff[1][i]);
-    if (SPLIT && pend_w && !DBG_NODMA) {
-      stage_w(cur ^ 1, kt + 1);
+    if constexpr (INTERLEAVE) {
+      const bool pw_on = pend_w;
+      auto pw = [&](int i) {
+        if (pw_on) piece_w(cur ^ 1, kt + 1, i);
+      };
+      LTX_MFMA_QI(aE, b0, 0, pw)
       pend_w = false;
+    } else {
+      if (SPLIT && pend_w && !DBG_NODMA) {
+        stage_w(cur ^ 1, kt + 1);
+        pend_w = false;
+      }
+      LTX_MFMA_Q(aE, b0, 0)
     }
-    LTX_MFMA_Q(aE, b0, 0)
     // Q1 (h0, n1): prefetch A(Q2), B(h1)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -508,7 +541,9 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
       else
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (kt + 2 < nk && !DBG_NODMA) {
-        if (SPLIT) {
+        if (INTERLEAVE) {
+          pend_w = true;  // X pieces go out between Q3's MFMA rows below, W in Q0
+        } else if (SPLIT) {
           stage_x(cur, kt + 2);
           pend_w = true;
         } else {
@@ -523,10 +558,19 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
         b0[i] = *(const s16x8*)(sn + boff[0][i]);
       }
     }
-    LTX_MFMA_Q(aO, b1, 1)
+    if constexpr (INTERLEAVE) {
+      const bool px_on = kt + 2 < nk;
+      auto px = [&](int i) {
+        if (px_on) piece_x(cur, kt + 2, i);
+      };
+      LTX_MFMA_QI(aO, b1, 1, px)
+    } else {
+      LTX_MFMA_Q(aO, b1, 1)
+    }
     cur ^= 1;
   }
 #undef LTX_MFMA_Q
+#undef LTX_MFMA_QI
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // epilogue stage 1: bf16(acc + bias) -> LDS image [256 m][256 n]
@@ -555,6 +599,225 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
   __syncthreads();
   const int cgrp = tid & 31;
   for (int rr = tid >> 5; rr < BM2; rr += 512 / 32) {
+    const int m = m0 + rr;
+    const int n = n0 + cgrp * 8;
+    if (m >= p.M || n >= p.N) continue;
+    const u32x2 lo = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16);
+    const u32x2 hi = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16 + 8);
+    bf16_t cv[8] = {(bf16_t)lo[0], (bf16_t)(lo[0] >> 16), (bf16_t)lo[1], (bf16_t)(lo[1] >> 16),
+                    (bf16_t)hi[0], (bf16_t)(hi[0] >> 16), (bf16_t)hi[1], (bf16_t)(hi[1] >> 16)};
+    float o[8];
+    epilogue_row8<EPI, R>(p, m, n, cv, o);
+    u32x4 pk;
+    pk[0] = pack2(o[0], o[1]);
+    pk[1] = pack2(o[2], o[3]);
+    pk[2] = pack2(o[4], o[5]);
+    pk[3] = pack2(o[6], o[7]);
+    *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Production large-tile kernel, templated on the tile height BMT (256 or 224) so that the tile
+// count fills whole rounds of the 256 CUs: M = 14336 (= 64 x 224) gives 448 tiles of 256 x 256
+// for N = 2048 (1.75 rounds -> 12.5 % of the chip idle in the tail) but 512 tiles of 224 x 256
+// (exactly 2). BMT = 256: 8 waves as 4 (m) x 2 (n), each 64 x 128 (4 x 8 fragments);
+// BMT = 224: 2 (m) x 4 (n), each 112 x 64 (7 x 4 fragments). Everything else is the l-kernel's
+// default schedule (VAR 35): scalar-base asm LDS-DMA, tile t+2's X pieces issued after the
+// mid-tile barrier and its W pieces in the next Q0, static priority for waves 4-7, quarters of
+// (k-half, n-half) with the next quarter's fragments prefetched, one barrier per K-tile.
+// X pieces (8 rows x 128 B) go to waves 4w..4w+3 (for BMT = 224 wave 7 moves only W pieces).
+// ---------------------------------------------------------------------------------------------
+template <int EPI, int R, int BMT>
+__global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
+  static_assert(BMT == 256 || BMT == 224, "tile height");
+  constexpr int WMW = (BMT == 256) ? 4 : 2;  // waves along m
+  constexpr int WNW = 8 / WMW;                // waves along n
+  constexpr int WTM = BMT / WMW;              // 64 | 112
+  constexpr int WTN = BN2 / WNW;              // 128 | 64
+  constexpr int MF = WTM / 16;                // 4 | 7
+  constexpr int NF = WTN / 16;                // 8 | 4
+  constexpr int NFH = NF / 2;                 // n-fragments per quarter
+  constexpr int XPIECES = BMT / 8;            // 32 | 28
+  constexpr int XT = BMT * BK * 2;            // X tile bytes
+  constexpr int ST = XT + WT2;                // stage bytes
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int ntm = (p.M + BMT - 1) / BMT, ntn = (p.N + BN2 - 1) / BN2;
+  int tm, tn;
+  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
+  const int m0 = tm * BMT, n0 = tn * BN2;
+  const int nk_main = p.K / BK;
+  const int nk = nk_main + p.K2 / BK;
+
+  // ---- DMA bookkeeping (see gemm_nt_kernel_l: per-lane 32-bit offsets, scalar bases)
+  const int lrow = lane >> 3, pchunk = lane & 7;
+  const int xp = min(4, max(0, XPIECES - 4 * wv));  // X pieces of this wave (uniform)
+  uint32_t xo[4], wo[4];
+  const char* xb = nullptr;
+  const char* wb = nullptr;
+  auto set_x = [&](bool ext) {
+    const int64_t ld = ext ? p.lda2 : p.lda;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = min((wave * 4 + i) * 8 + lrow, BMT - 1);
+      xo[i] = (uint32_t)(((int64_t)(min(m0 + row, p.M - 1) - m0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
+    }
+    xb = (const char*)(ext ? p.A2 : p.A) + (int64_t)m0 * ld * 2;
+  };
+  auto set_w = [&](bool ext) {
+    const int64_t ld = ext ? p.ldw2 : p.ldw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wave * 4 + i) * 8 + lrow;
+      wo[i] = (uint32_t)(((int64_t)(min(n0 + row, p.N - 1) - n0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
+    }
+    wb = (const char*)(ext ? p.W2 : p.W) + (int64_t)n0 * ld * 2;
+  };
+  set_x(nk_main == 0);
+  set_w(nk_main == 0);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
+  auto glds_s = [&](uint32_t voff, const char* sbase, uint32_t lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+  };
+  auto stage_x = [&](int st, int kt) {
+    if (kt == nk_main && nk_main > 0) set_x(true);  // ext tiles come last, in issue order
+    const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
+    const uint32_t l = lds0 + st * ST + wv * 4096;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < xp) glds_s(xo[i], sb, l + i * 1024);
+  };
+  auto stage_w = [&](int st, int kt) {
+    if (kt == nk_main && nk_main > 0) set_w(true);
+    const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
+    const uint32_t l = lds0 + st * ST + XT + wv * 4096;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds_s(wo[i], sb, l + i * 1024);
+  };
+
+  const int wm = (WMW == 4) ? (wave >> 1) : (wave >> 2);
+  const int wn = (WMW == 4) ? (wave & 1) : (wave & 3);
+  f32x4 acc[NF][MF];  // [n-fragment][m-fragment]
+#pragma unroll
+  for (int i = 0; i < NF; ++i)
+#pragma unroll
+    for (int j = 0; j < MF; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15;
+  const int fchunk = lane >> 4;
+  // A (W) fragment offsets per quarter q = 2h + nh, B (X) offsets per k-half h
+  int aoff[4][NFH], boff[2][MF];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int j = 0; j < MF; ++j) boff[h][j] = swz(wm * WTM + j * 16 + frow, h * 4 + fchunk);
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int i = 0; i < NFH; ++i)
+        aoff[2 * h + nh][i] = XT + swz(wn * WTN + nh * (WTN / 2) + i * 16 + frow, h * 4 + fchunk);
+  }
+  stage_x(0, 0);
+  stage_w(0, 0);
+  if (nk > 1) {
+    stage_x(1, 1);
+    stage_w(1, 1);
+    if (xp == 4)
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+    else if (xp == 0)
+      asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+  s16x8 aE[NFH], aO[NFH], b0[MF], b1[MF];  // A even/odd quarter sets, B per k-half
+#pragma unroll
+  for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(smem + aoff[0][i]);
+#pragma unroll
+  for (int j = 0; j < MF; ++j) b0[j] = *(const s16x8*)(smem + boff[0][j]);
+#define LTX_MFMA_T(AS, BS, NH)                                                                        \
+  __builtin_amdgcn_sched_barrier(0);                                                                  \
+  _Pragma("unroll") for (int i = 0; i < NFH; ++i)                                                     \
+  _Pragma("unroll") for (int j = 0; j < MF; ++j)                                                      \
+    acc[(NH) * NFH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * NFH + i][j], 0, 0, 0); \
+  __builtin_amdgcn_sched_barrier(0);
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+
+  int cur = 0;
+  bool pend_w = false;  // W half of tile kt+1's DMA still to issue in Q0
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* st = smem + cur * ST;
+    // Q0 (h0, n0): prefetch A(Q1)
+#pragma unroll
+    for (int i = 0; i < NFH; ++i) aO[i] = *(const s16x8*)(st + aoff[1][i]);
+    if (pend_w) {
+      stage_w(cur ^ 1, kt + 1);
+      pend_w = false;
+    }
+    LTX_MFMA_T(aE, b0, 0)
+    // Q1 (h0, n1): prefetch A(Q2), B(h1)
+#pragma unroll
+    for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(st + aoff[2][i]);
+#pragma unroll
+    for (int j = 0; j < MF; ++j) b1[j] = *(const s16x8*)(st + boff[1][j]);
+    LTX_MFMA_T(aO, b0, 1)
+    // Q2 (h1, n0): prefetch A(Q3)
+#pragma unroll
+    for (int i = 0; i < NFH; ++i) aO[i] = *(const s16x8*)(st + aoff[3][i]);
+    LTX_MFMA_T(aE, b1, 0)
+    // all reads of tile t issued: wait tile t+1, free tile t's stage, DMA tile t+2's X into it
+    if (kt + 1 < nk) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + 2 < nk) {
+        stage_x(cur, kt + 2);
+        pend_w = true;
+      }
+      const char* sn = smem + (cur ^ 1) * ST;
+      // Q3 (h1, n1) of tile t: prefetch A(Q0), B(h0) of tile t+1
+#pragma unroll
+      for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(sn + aoff[0][i]);
+#pragma unroll
+      for (int j = 0; j < MF; ++j) b0[j] = *(const s16x8*)(sn + boff[0][j]);
+    }
+    LTX_MFMA_T(aO, b1, 1)
+    cur ^= 1;
+  }
+#undef LTX_MFMA_T
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // epilogue stage 1: bf16(acc + bias) -> LDS image [BMT m][256 n]
+  char* cimg = smem;
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int nl = wn * WTN + i * 16 + (lane >> 4) * 4;
+    float b4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias) {
+      const int gn = n0 + nl;
+      if (gn + 3 < p.N) {
+        const u32x2 bb = *(const u32x2*)(p.bias + gn);
+        b4[0] = bf2f((bf16_t)bb[0]); b4[1] = bf2f((bf16_t)(bb[0] >> 16));
+        b4[2] = bf2f((bf16_t)bb[1]); b4[3] = bf2f((bf16_t)(bb[1] >> 16));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < MF; ++j) {
+      const int ml = wm * WTM + j * 16 + (lane & 15);
+      u32x2 pk;
+      pk[0] = pack2(acc[i][j][0] + b4[0], acc[i][j][1] + b4[1]);
+      pk[1] = pack2(acc[i][j][2] + b4[2], acc[i][j][3] + b4[3]);
+      *(u32x2*)(cimg + ml * C_STRIDE2 + nl * 2) = pk;
+    }
+  }
+  __syncthreads();
+  const int cgrp = tid & 31;
+  for (int rr = tid >> 5; rr < BMT; rr += 512 / 32) {
     const int m = m0 + rr;
     const int n = n0 + cgrp * 8;
     if (m >= p.M || n >= p.N) continue;
@@ -813,9 +1076,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_p(const GemmParams p) {
 }
 
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
-static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (asm DMA + split + static prio),
-                                // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split;
-                                // 4-7 measurement-only (wrong results)
+static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (t-kernel, auto tile height),
+                                // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split,
+                                // 11 ping-pong, 12 interleaved DMA, 13/14/15 t-kernel 256/224/auto,
+                                // 16 l-kernel default of before; 4-7 measurement-only (wrong results)
 
 template <int EPI, int R = 0>
 static int launch(const GemmParams& p, hipStream_t s) {
@@ -833,10 +1097,30 @@ static int launch(const GemmParams& p, hipStream_t s) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 33>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 35>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 99>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       attr_set = true;
     }
-    if (g_variant == 0)  // default: scalar-base asm DMA, issue split over two quarters, static priority
+    if (g_variant == 16)  // previous default: l-kernel, asm DMA, split issue, static priority
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else if (g_variant == 0 || (g_variant >= 13 && g_variant <= 15)) {
+      // default (0 = 15): gemm_nt_kernel_t with the tile height that fills the last round best;
+      // 13 forces BMT 256, 14 forces BMT 224
+      static bool t_set = false;
+      if (!t_set) {
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        t_set = true;
+      }
+      const int64_t ntn = (p.N + BN2 - 1) / BN2;
+      const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
+      // fraction of the last round of 256 CUs that has work, per tile height
+      auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
+      const bool use224 = g_variant == 14 || ((g_variant == 15 || g_variant == 0) && fill(t224) > fill(t256) + 0.02);
+      if (use224)
+        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
+      else
+        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
+    }
     else if (g_variant == 11) {  // ping-pong 8-phase kernel
       static bool pp_set = false;
       if (!pp_set) {
@@ -852,6 +1136,8 @@ static int launch(const GemmParams& p, hipStream_t s) {
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 33>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
     else if (g_variant == 9)
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+    else if (g_variant == 12)  // asm DMA pieces interleaved between MFMA rows
+      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 99>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
     else if (g_variant >= 4) {
       if constexpr (EPI == LTX_EPI_STORE && R == 0) {  // measurement-only variants
         (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
