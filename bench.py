@@ -243,7 +243,7 @@ def main():
                    "grad_accum": ACCUM, "parallelism": f"dp{world}"},
         "step_tflops_per_gpu": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-        "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel<GELU> FF-up [14336x2048].[8192x2048]^T",
+        "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel_t<GELU, 256> FF-up [14336x2048].[8192x2048]^T",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": load_traffic(),
                      "launch_ms": round(dom_ms, 4), "launches": len(timer.pairs)},

@@ -14,7 +14,7 @@ import json
 import sys
 from collections import defaultdict
 
-DOM_MATCH = "gemm_nt_kernel_l<1"
+DOM_MATCH = "gemm_nt_kernel_t<1"
 DOM_GRID = 56 * 32 * 512  # ceil(14336/256) * ceil(8192/256) workgroups x 512 threads
 
 
@@ -51,7 +51,7 @@ def traffic(fetch_csv, write_csv, out):
     write = write_kb * 1024.0
     M, N, K = 14336, 8192, 2048
     algo = 2 * (M * K + N * K) + 2 * 2 * M * N  # A, W read once; activation + pre-activation stored
-    res = {"kernel": "gemm_nt_kernel_l<GELU> FF-up [14336x2048].[8192x2048]^T (+pre-activation store)",
+    res = {"kernel": "gemm_nt_kernel_t<GELU, 256> FF-up [14336x2048].[8192x2048]^T (+pre-activation store)",
            "dispatches_fetch": nf, "dispatches_write": nw,
            "fetch_size_kb_raw": fetch_kb, "write_size_kb_raw": write_kb,
            "fetch_bytes_corrected": fetch, "write_bytes": write,
