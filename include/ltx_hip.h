@@ -139,10 +139,14 @@ int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const
 /* ---- K10/K14: flash attention (F.scaled_dot_product_attention, attention.py:1057-1064) ------- */
 /* Q [B,Nq,H,d] (row stride ldq per token, head h at column h*d), K/V [B,Nk,H,d], O likewise;
  * lse [B,H,Nq] f32 in log2 units (saved for the backward); key_bias [B,Nk] f32 added to the scaled scores
- * (encoder mask bias, transformer3d.py:441-445) or null. d in {32, 64}. */
+ * (encoder mask bias, transformer3d.py:441-445) or null. d in {32, 64}. kv_batch_rows = Nk, or 0
+ * when every batch attends to the same K/V/key_bias rows (the training step's one prompt
+ * expanded over the batch, training.py:415): then K/V/key_bias hold one batch. dK/dV (backward)
+ * stay per batch [B*Nk rows]; their batch sum is the gradient of the shared rows. */
 int ltx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
                  int64_t ldv, void* o, int64_t ldo, float* lse, const float* key_bias, int64_t B,
-                 int64_t H, int64_t Nq, int64_t Nk, int64_t d, float scale, void* stream);
+                 int64_t H, int64_t Nq, int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale,
+                 void* stream);
 /* Backward (deterministic, no atomics): delta[b,h,i] = sum_d dO*O (f32, caller workspace
  * [B,H,Nq]); dQ [B,Nq,H,d] (f32 if dq_is_f32 else bf16, row stride lddq), dK/dV bf16. lse as
  * written by ltx_attn_fwd (log2 units). */
@@ -150,8 +154,8 @@ int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
                  int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
                  const float* lse, const float* key_bias, float* delta_ws, void* dq,
                  int64_t lddq, int dq_is_f32, void* dk, int64_t lddk, void* dv, int64_t lddv,
-                 int64_t B, int64_t H, int64_t Nq, int64_t Nk, int64_t d, float scale,
-                 void* stream);
+                 int64_t B, int64_t H, int64_t Nq, int64_t Nk, int64_t kv_batch_rows, int64_t d,
+                 float scale, void* stream);
 
 /* ---- bf16 MFMA GEMM: C[M,N] = epilogue(A[M,K] . W[N,K]^T) ------------------------------------ */
 /* nn.Linear forward (W as stored) and dgrad (W^T packed once: frozen weights). K % 64 == 0,
@@ -209,6 +213,10 @@ int ltx_transpose_bf16(const void* in, int64_t ld_in, void* out, int64_t ld_out,
                        int64_t C, void* stream);
 /* column sums of bf16 [M,N] -> bf16 [N] (bias grads; f32 accumulation) */
 int ltx_colsum_bf16(const void* x, int64_t ldx, void* out, int64_t M, int64_t N, void* stream);
+/* out[r,:] = bf16(sum_b x[b*rows + r, :]) (f32 accumulation): gradient of rows shared by all
+ * batches (the expanded prompt, training.py:415 -- autograd's sum over the expanded dim). */
+int ltx_batch_sum_bf16(const void* x, int64_t ldx, int64_t B, int64_t rows, int64_t cols,
+                       void* out, int64_t ldo, void* stream);
 /* F.mse_loss(out, v) (mean) + its backward seed and std(v) (training.py:159-166):
  * stats[0] = sum (o-v)^2 in f32 over bf16-rounded squares, stats[1] = sum v, stats[2] = sum v^2
  * (f32 atomics into a zeroed 4-float buffer); dout = bf16(bf16(bf16(o-v) * 2/n) * gscale). */

@@ -95,6 +95,32 @@ def test_tiny_model_matches_reference_goldens():
             _check_noise_criterion(name, g[name], v.to(DEV), gref32[name], slack=5e-3)
 
 
+def test_shared_prompt_path_matches_per_sample_path():
+    """train_step hands the model one prompt expanded over the batch (stride-0 view): the text
+    side then runs once and the cross-attention reads shared K/V, with the text-side gradients
+    summed over the batch. It must agree with the per-sample path (a materialised copy)."""
+    d, meta = _load("tiny_train_step")
+    cfg = meta["config"]
+    params = {k[2:]: v for k, v in d.items() if k.startswith("w.")}
+    B = d["in.latents"].shape[0]
+    results = []
+    for shared in (True, False):
+        model = build_model(cfg, params, meta["lora_rank"])
+        x = d["out.hidden_states"].to(DEV).bfloat16()
+        enc = d["in.prompt_embeds"].to(DEV).bfloat16().expand(B, -1, -1)
+        mask = d["in.prompt_attention_mask"].to(DEV).expand(B, -1)
+        if not shared:
+            enc, mask = enc.contiguous(), mask.contiguous()
+        coords = model.patchifier.get_latent_coords(2, 8, 8, B, DEV)
+        out = model._forward_tokens(x, coords, enc, d["out.t"].to(DEV), mask)
+        out.backward(torch.ones_like(out) * 1e-2)
+        results.append((out.detach(), grads_by_canonical(model)))
+    (o1, g1), (o2, g2) = results
+    assert rel(o1, o2) < 1e-3
+    for k in g1:
+        assert rel(g1[k], g2[k]) < 2e-2, k
+
+
 def test_block2b_matches_reference_goldens():
     d, meta = _load("ltx2b_block")
     cfg = meta["config"]

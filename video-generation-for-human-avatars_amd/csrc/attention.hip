@@ -118,6 +118,7 @@ struct AttnParams {
   bf16_t* dk; int64_t lddk;
   bf16_t* dv; int64_t lddv;
   int B, H, Nq, Nk;
+  int kvb;                             // rows between batches of K, V and key_bias (Nk, or 0: shared)
   float scale;
 };
 
@@ -126,7 +127,7 @@ __device__ __forceinline__ void key_bias_tile(float* kb, const AttnParams& p, in
   if (tid < n) {
     const int key = key0 + tid;
     float v = -INFINITY;
-    if (key < p.Nk) v = p.key_bias ? p.key_bias[(int64_t)b * p.Nk + key] * LOG2E : 0.f;
+    if (key < p.Nk) v = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + key] * LOG2E : 0.f;
     kb[tid] = v;
   }
 }
@@ -170,8 +171,8 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
   const int qc = min(qi, p.Nq - 1);
   const float c2 = p.scale * LOG2E;
 
-  const bf16_t* kbase = p.k + (int64_t)b * p.Nk * p.ldk + hh * HD;
-  const bf16_t* vbase = p.v + (int64_t)b * p.Nk * p.ldv + hh * HD;
+  const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  const bf16_t* vbase = p.v + (int64_t)b * p.kvb * p.ldv + hh * HD;
 
   s16x8 qf[KS];
   {
@@ -403,13 +404,13 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   float kbias = 0.f;
   if (BIAS) {
     kbias = -INFINITY;
-    if (key < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.Nk + key] * LOG2E : 0.f;
+    if (key < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + key] * LOG2E : 0.f;
   }
 
   s16x8 kf[KS], vf[KS];
   {
-    const bf16_t* kr = p.k + ((int64_t)b * p.Nk + kc) * p.ldk + hh * HD;
-    const bf16_t* vr = p.v + ((int64_t)b * p.Nk + kc) * p.ldv + hh * HD;
+    const bf16_t* kr = p.k + ((int64_t)b * p.kvb + kc) * p.ldk + hh * HD;
+    const bf16_t* vr = p.v + ((int64_t)b * p.kvb + kc) * p.ldv + hh * HD;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       kf[ks] = *(const s16x8*)(kr + ks * 16 + 8 * h);
@@ -599,14 +600,15 @@ using namespace ltx;
 
 extern "C" int ltx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
                             void* o, int64_t ldo, float* lse, const float* key_bias, int64_t B, int64_t H,
-                            int64_t Nq, int64_t Nk, int64_t d, float scale, void* stream) {
+                            int64_t Nq, int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale, void* stream) {
   int rc = check_common(q, ldq, k, ldk, v, ldv, B, H, Nq, Nk, d);
   if (rc) return rc;
+  LTX_CHECK_ARG(kv_batch_rows == Nk || kv_batch_rows == 0, "attn_fwd: kv_batch_rows must be Nk or 0 (shared)");
   LTX_CHECK_ARG(o && lse && ldo >= H * d && ldo % 8 == 0, "attn_fwd: bad output");
   AttnParams p = {};
   p.q = (const bf16_t*)q; p.ldq = ldq; p.k = (const bf16_t*)k; p.ldk = ldk; p.v = (const bf16_t*)v; p.ldv = ldv;
   p.o_out = (bf16_t*)o; p.ldo = ldo; p.lse = lse; p.key_bias = key_bias;
-  p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.scale = scale;
+  p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.kvb = (int)kv_batch_rows; p.scale = scale;
   return d == 64 ? launch_fwd<64>(p, (hipStream_t)stream) : launch_fwd<32>(p, (hipStream_t)stream);
 }
 
@@ -614,9 +616,10 @@ extern "C" int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t l
                             const void* o, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
                             const float* key_bias, float* delta_ws, void* dq, int64_t lddq, int dq_is_f32,
                             void* dk, int64_t lddk, void* dv, int64_t lddv, int64_t B, int64_t H, int64_t Nq,
-                            int64_t Nk, int64_t d, float scale, void* stream) {
+                            int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale, void* stream) {
   int rc = check_common(q, ldq, k, ldk, v, ldv, B, H, Nq, Nk, d);
   if (rc) return rc;
+  LTX_CHECK_ARG(kv_batch_rows == Nk || kv_batch_rows == 0, "attn_bwd: kv_batch_rows must be Nk or 0 (shared)");
   LTX_CHECK_ARG(o && dout && lse && delta_ws && dq && dk && dv, "attn_bwd: null operand");
   LTX_CHECK_ARG((ldo | lddo | lddq | lddk | lddv) % 8 == 0, "attn_bwd: strides must be multiples of 8");
   AttnParams p = {};
@@ -625,6 +628,6 @@ extern "C" int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t l
   p.lse = (float*)lse; p.key_bias = key_bias;
   p.dq = dq; p.lddq = lddq; p.dq_f32 = dq_is_f32;
   p.dk = (bf16_t*)dk; p.lddk = lddk; p.dv = (bf16_t*)dv; p.lddv = lddv;
-  p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.scale = scale;
+  p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.kvb = (int)kv_batch_rows; p.scale = scale;
   return d == 64 ? launch_bwd<64>(p, delta_ws, (hipStream_t)stream) : launch_bwd<32>(p, delta_ws, (hipStream_t)stream);
 }

@@ -214,6 +214,28 @@ __global__ void silu_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y
 }
 
 // column sums with f32 accumulation (nn.Linear bias grad = grad_out.sum(0))
+// out[r, :] = bf16(sum_b x[b*rows + r, :]) with f32 accumulation, 8 columns per thread: the
+// gradient of rows shared by every batch (one prompt expanded over the batch, training.py:415).
+__global__ __launch_bounds__(256) void batch_sum_kernel(const bf16_t* __restrict__ x, int64_t ldx, int B,
+                                                        int64_t rows, int cols, bf16_t* __restrict__ out,
+                                                        int64_t ldo) {
+  const int c8 = cols / 8;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= rows * c8) return;
+  const int64_t r = idx / c8;
+  const int c = (int)(idx % c8) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < B; ++b) {
+    const u32x4 v = *(const u32x4*)(x + ((int64_t)b * rows + r) * ldx + c);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += bf2f((bf16_t)(v[i >> 1] >> ((i & 1) * 16)));
+  }
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = pack2(acc[2 * i], acc[2 * i + 1]);
+  *(u32x4*)(out + r * ldo + c) = o;
+}
+
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ x, int64_t ldx,
                                                      bf16_t* __restrict__ out, int M, int N) {
   __shared__ float part[4][64];
@@ -423,6 +445,17 @@ int ltx_colsum_bf16(const void* x, int64_t ldx, void* out, int64_t M, int64_t N,
   LTX_CHECK_ARG(x && out && M > 0 && N > 0 && ldx >= N, "colsum: bad args");
   hipLaunchKernelGGL(colsum_kernel, dim3((unsigned)((N + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)x, ldx, (bf16_t*)out, (int)M, (int)N);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_batch_sum_bf16(const void* x, int64_t ldx, int64_t B, int64_t rows, int64_t cols, void* out, int64_t ldo,
+                       void* stream) {
+  LTX_CHECK_ARG(x && out && B > 0 && rows > 0 && cols > 0 && cols % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0,
+                "batch_sum: bad args (cols and leading dims must be multiples of 8)");
+  const int64_t n = rows * (cols / 8);
+  hipLaunchKernelGGL(batch_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, ldx, (int)B, rows, (int)cols, (bf16_t*)out, ldo);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

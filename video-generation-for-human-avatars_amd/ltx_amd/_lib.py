@@ -40,9 +40,9 @@ _SIGNATURES = {
     "ltx_qk_norm_rope_bwd": [_p, _i64, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _p, _p, _p, _p,
                              _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i32, _p],
     "ltx_attn_fwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64,
-                     _f32, _p],
+                     _i64, _f32, _p],
     "ltx_attn_bwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i32,
-                     _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _p],
+                     _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _p],
     "ltx_gemm_bf16_nt": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i32, _p, _p, _i64, _p,
                          _i64, _p, _i64, _f32, _i64, _i64, _p],
     "ltx_gemm_set_variant": [_i32],
@@ -56,6 +56,7 @@ _SIGNATURES = {
     "ltx_silu_bf16": [_p, _p, _i64, _p],
     "ltx_transpose_bf16": [_p, _i64, _p, _i64, _i64, _i64, _p],
     "ltx_colsum_bf16": [_p, _i64, _p, _i64, _i64, _p],
+    "ltx_batch_sum_bf16": [_p, _i64, _i64, _i64, _i64, _p, _i64, _p],
     "ltx_mse_fwd_bwd": [_p, _p, _p, _p, _i64, _f32, _p],
     "ltx_adamw_step": [_p, _p, _p, _p, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i64, _p],
 }

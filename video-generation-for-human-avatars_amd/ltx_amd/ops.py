@@ -252,21 +252,24 @@ def qk_norm_rope_bwd(dq, q_raw, q_w, rq, dk=None, k_raw=None, k_w=None, rk=None,
 # ---------------------------------------------------------------------------------------------
 # attention
 # ---------------------------------------------------------------------------------------------
-def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None):
-    """q [B*Nq, >=H*d] row view, k/v [B*Nk, ...] -> (o [B*Nq, H*d], lse [B,H,Nq] f32 log2)."""
+def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
+    """q [B*Nq, >=H*d] row view, k/v [B*Nk, ...] -> (o [B*Nq, H*d], lse [B,H,Nq] f32 log2).
+    kv_shared: k/v/key_bias hold ONE batch ([Nk, ...], [1, Nk]) attended by every query batch."""
     Nq = q.shape[0] // B
-    Nk = k.shape[0] // B
+    Nk = k.shape[0] if kv_shared else k.shape[0] // B
     o = torch.empty(B * Nq, H * d, dtype=BF16, device=q.device) if out is None else out
     lse = torch.empty(B, H, Nq, dtype=F32, device=q.device)
     call("ltx_attn_fwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
-         _rows(o, "o"), _p(lse), _p(key_bias), B, H, Nq, Nk, d, scale, _s())
+         _rows(o, "o"), _p(lse), _p(key_bias), B, H, Nq, Nk, 0 if kv_shared else Nk, d, scale, _s())
     return o, lse
 
 
 def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, dq=None,
-             dk=None, dv=None):
+             dk=None, dv=None, kv_shared=False):
+    """Gradients (dq [B*Nq], dk/dv [B*Nk] per query batch -- with kv_shared their batch_sum is
+    the gradient of the shared rows)."""
     Nq = q.shape[0] // B
-    Nk = k.shape[0] // B
+    Nk = k.shape[0] if kv_shared else k.shape[0] // B
     dev = q.device
     dq = torch.empty(B * Nq, H * d, dtype=F32 if dq_f32 else BF16, device=dev) if dq is None else dq
     dk = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dk is None else dk
@@ -275,8 +278,17 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
     call("ltx_attn_bwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
          _rows(o, "o"), _p(do), _rows(do, "do"), _p(lse), _p(key_bias), _p(delta), _p(dq),
          _rows(dq, "dq"), 1 if dq.dtype == F32 else 0, _p(dk), _rows(dk, "dk"), _p(dv),
-         _rows(dv, "dv"), B, H, Nq, Nk, d, scale, _s())
+         _rows(dv, "dv"), B, H, Nq, Nk, 0 if kv_shared else Nk, d, scale, _s())
     return dq, dk, dv
+
+
+def batch_sum(x, B, out=None):
+    """x [B*rows, cols] bf16 -> [rows, cols]: sum over the batch (f32 accumulation)."""
+    rows = x.shape[0] // B
+    cols = x.shape[1]
+    out = torch.empty(rows, cols, dtype=BF16, device=x.device) if out is None else out
+    call("ltx_batch_sum_bf16", _p(x), _rows(x, "x"), B, rows, cols, _p(out), _rows(out, "out"), _s())
+    return out
 
 
 # ---------------------------------------------------------------------------------------------

@@ -44,8 +44,10 @@ def train_step(model, batch, scheduler, patchifier, config, prompt_embeds, promp
     pose = batch["pose_latents"].to(device=device, dtype=dt)
     B, C, F, H, W = latents.shape
     N = F * H * W
-    enc = prompt_embeds.expand(B, -1, -1).to(device=device, dtype=dt)
-    enc_mask = prompt_attention_mask.expand(B, -1).to(device)
+    # convert first, then expand: the batch stays a stride-0 view, which the model recognises as
+    # one prompt shared by the batch (caption projection and text K/V computed once)
+    enc = prompt_embeds.to(device=device, dtype=dt).expand(B, -1, -1)
+    enc_mask = prompt_attention_mask.to(device).expand(B, -1)
     # one coordinate set broadcast over the batch (identical per sample): one shared RoPE table
     coords = patchifier.get_latent_coords(F, H, W, 1, device).expand(B, -1, -1)
     if t is None:

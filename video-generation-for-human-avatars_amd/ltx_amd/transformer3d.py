@@ -311,8 +311,12 @@ class PixArtAlphaTextProjection(nn.Module):
 class _Shared:
     """Per-forward constants shared by all blocks."""
 
-    def __init__(self, B, N, L, heads, head_dim, rope, enc_bias, eps):
+    def __init__(self, B, N, L, heads, head_dim, rope, enc_bias, eps, text_shared=False):
         self.B, self.N, self.L = B, N, L
+        # text_shared: every sample attends to the same prompt (train_step expands one prompt
+        # over the batch, training.py:415), so the text side holds one batch (Bt = 1)
+        self.text_shared = text_shared
+        self.Bt = 1 if text_shared else B
         self.H, self.d = heads, head_dim
         self.D = heads * head_dim
         self.rope = rope
@@ -389,8 +393,9 @@ class _BlockFn(torch.autograd.Function):
             k2raw = ops.gemm(enc2, wk, bias=bk)
             v2 = ops.gemm(enc2, wv, bias=bv)
         q2, _, rq2, _ = ops.qk_norm_rope_fwd(q2raw, None, a2.q_norm.weight, None, None, B=B, N=N)
-        k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, a2.k_norm.weight, None, None, B=B, N=L)
-        o2, lse2 = ops.attn_fwd(q2, k2, v2, B, H, d, a2.scale, key_bias=sh.enc_bias)
+        k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, a2.k_norm.weight, None, None, B=sh.Bt, N=L)
+        o2, lse2 = ops.attn_fwd(q2, k2, v2, B, H, d, a2.scale, key_bias=sh.enc_bias,
+                                kv_shared=sh.text_shared)
         if has_lora:
             u_o, su = ops.lora_down(o2, Ao, split=True)
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1,
@@ -452,10 +457,13 @@ class _BlockFn(torch.autograd.Function):
         else:
             do2 = ops.gemm(dh2, W["o2_wT"])
         dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
-                                     key_bias=sh.enc_bias)
+                                     key_bias=sh.enc_bias, kv_shared=sh.text_shared)
         del do2
+        if sh.text_shared:  # gradient of the shared text rows = sum over the query batches
+            dk2 = ops.batch_sum(dk2, B)
+            dv2 = ops.batch_sum(dv2, B)
         dq2raw, _ = ops.qk_norm_rope_bwd(dq2, q2raw, a2.q_norm.weight, rq2, B=B, N=N)
-        dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=B, N=L)
+        dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=sh.Bt, N=L)
         del dq2, dk2
         if has_lora:
             ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
@@ -752,13 +760,22 @@ class Transformer3DModel(nn.Module):
         dt = torch.bfloat16
         if self.dtype != dt:
             raise TypeError("the MI355X path computes in bf16: call model.to(torch.bfloat16)")
+        # one prompt expanded over the batch (stride-0 views, as train_step passes it): run the
+        # text side once; the cross-attention reads the shared K/V for every sample
+        m = encoder_attention_mask
+        text_shared = (B > 1 and encoder_hidden_states.stride(0) == 0
+                       and (m is None or m.shape[0] == 1 or m.stride(0) == 0))
+        if text_shared:
+            encoder_hidden_states = encoder_hidden_states[:1]
+            m = None if m is None else m[:1]
+        Bt = 1 if text_shared else B
         # encoder mask -> additive bias (transformer3d.py:441-445): (1 - m) * -10000 in bf16
         enc_bias = None
-        if encoder_attention_mask is not None:
-            if encoder_attention_mask.ndim == 2:
-                enc_bias = ((1 - encoder_attention_mask.to(dt)) * -10000.0).float().contiguous()
+        if m is not None:
+            if m.ndim == 2:
+                enc_bias = ((1 - m.to(dt)) * -10000.0).float().contiguous()
             else:
-                enc_bias = encoder_attention_mask.reshape(B, -1).float().contiguous()
+                enc_bias = m.reshape(Bt, -1).float().contiguous()
         with torch.no_grad():
             h = ops.gemm(x_in.reshape(B * N, C), self.patchify_proj.weight,
                          bias=self.patchify_proj.bias)
@@ -767,12 +784,12 @@ class Transformer3DModel(nn.Module):
                             self.positional_embedding_max_pos)
         enc = encoder_hidden_states.to(dt)
         L = enc.shape[1]
-        enc2d = enc.reshape(B * L, enc.shape[2]).contiguous()
+        enc2d = enc.reshape(Bt * L, enc.shape[2]).contiguous()
         cp = self.caption_projection
         enc2 = _CaptionProjFn.apply(enc2d, cp.linear_1.weight, cp.linear_1.bias,
                                     cp.linear_2.weight, cp.linear_2.bias)
         eps = self.transformer_blocks[0].norm_eps if len(self.transformer_blocks) else 1e-6
-        sh = _Shared(B, N, L, H, self.attention_head_dim, rope, enc_bias, eps)
+        sh = _Shared(B, N, L, H, self.attention_head_dim, rope, enc_bias, eps, text_shared)
         keep = torch.is_grad_enabled()
         for blk in self.transformer_blocks:
             with torch.no_grad():
