@@ -179,6 +179,10 @@ int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, int64_t ldw,
 /* Tuning knob for A/B measurements of GEMM schedules (0: per-tile DMA split over two quarters,
  * the default; 1: one burst). Process-global. */
 int ltx_gemm_set_variant(int variant);
+/* Caller-owned f32 workspace for split-K on small grids (e.g. the M = 256 text-side GEMMs): the
+ * library keeps the pointer until the next call (stream-ordered reuse by consecutive GEMMs on
+ * one stream); bytes = 0 disables split-K. */
+int ltx_gemm_set_workspace(void* ptr, int64_t bytes);
 
 /* ---- LoRA skinny contractions in f32 (peft lora_A / lora_B, training.py:50-68) --------------- */
 /* out[m,j] = alpha * sum_k x[m,k] * Wr[j,k], Wr element (j,k) at Wr[j*wj + k*wk]; x bf16 [M,K]

@@ -44,6 +44,7 @@ def g(*shape, dtype=torch.bfloat16, scale=1.0, seed=0):
 
 # ------------------------------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(256, 128, 64), (300, 136, 128), (1024, 2048, 2048), (8, 768, 256),
+                                   (256, 2048, 2048), (200, 1000, 4096),  # split-K grids
                                    (14336 // 7, 6144, 2048), (4000, 4104, 192), (14336, 2048, 8192)])
 def test_gemm_store(M, N, K):
     from ltx_amd import ops
@@ -68,9 +69,10 @@ def test_gemm_strided_views_and_no_bias():
     assert float(outbuf[:, :N].abs().max()) == 0.0
 
 
-def test_gemm_epilogues():
+@pytest.mark.parametrize("M,N,K", [(512, 256, 256), (256, 512, 2048)])  # one pass / split-K
+def test_gemm_epilogues(M, N, K):
     from ltx_amd import ops
-    M, N, K, r, B = 512, 256, 256, 16, 4
+    r, B = 16, 4
     a, w, b = g(M, K, seed=6), g(N, K, seed=7, scale=K ** -0.5), g(N, seed=8)
     y = (a.float() @ w.float().t() + b.float()).to(torch.bfloat16)
     # GELU + pre-activation store
@@ -364,7 +366,7 @@ def test_gemm_k_extension_lora_fusion():
     """LoRA fused into the K loop: [x | split(u)] . [W | split(s*B)]^T == x.W^T + b + s*u.B^T
     with u = x.A^T in f32 (peft), for both tile kernels and for the dgrad orientation."""
     from ltx_amd import ops
-    for M, N, K in ((512, 256, 256), (14336 // 2, 2048, 2048)):
+    for M, N, K in ((512, 256, 256), (14336 // 2, 2048, 2048), (256, 2048, 2048)):  # + split-K
         r, s = 16, 0.5
         x, w, b = g(M, K, seed=21), g(N, K, seed=22, scale=K ** -0.5), g(N, seed=23)
         A = torch.randn(r, K, device=DEV) / K ** 0.5

@@ -49,6 +49,10 @@ struct GemmParams {
   const bf16_t* W2;
   int64_t lda2, ldw2;
   int K2;
+  // split-K (small grids): S partial f32 tiles [S][M][N] in a caller-provided workspace, summed by
+  // splitk_epilogue_kernel which then applies bias + the epilogue
+  float* ws;
+  int splitk;
 };
 
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
@@ -171,8 +175,9 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int split = blockIdx.x / (ntm * ntn);  // split-K slice (0 unless p.splitk > 1)
   int tm, tn;
-  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
+  block_to_tile(blockIdx.x % (ntm * ntn), ntm, ntn, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- staging addresses: wave w loads 4 x 1 KiB (8 rows each) of the X tile and of the W tile
@@ -221,14 +226,16 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int nk = nk_main + p.K2 / BK;
-  stage(0, 0);
+  const int nk_all = nk_main + p.K2 / BK;
+  const int S = p.splitk > 1 ? p.splitk : 1;
+  const int kt0 = (int)((int64_t)split * nk_all / S), nk = (int)((int64_t)(split + 1) * nk_all / S);
+  stage(0, kt0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int frow = lane & 15;   // fragment row within a 16-row subtile
   const int fchunk = lane >> 4;  // fragment k-chunk (8 elements) within a 32-deep k-step
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+  for (int kt = kt0; kt < nk; ++kt) {
+    const int cur = (kt - kt0) & 1;
     if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
     const char* xs = smem + cur * STAGE_BYTES;
     const char* ws = xs + TILE_BYTES;
@@ -255,6 +262,19 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
     __syncthreads();
   }
 
+  if (S > 1) {  // split-K: raw f32 partial, 4 consecutive n per lane (16-B stores)
+    float* part = p.ws + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wn * 64 + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + (lane & 15);
+        if (m < p.M && n < p.N) *(f32x4*)(part + (int64_t)m * p.N + n) = acc[i][j];
+      }
+    }
+    return;
+  }
   // ---- epilogue stage 1: bf16(acc + bias) -> LDS image [128 m][128 n] (row stride C_STRIDE)
   // lane holds C^T[n = i*16 + (lane>>4)*4 + r][m = j*16 + (lane&15)], r = 0..3
   char* cimg = smem;
@@ -300,6 +320,38 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
     pk[3] = pack2(o[6], o[7]);
     *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
   }
+}
+
+// split-K tail: sum the S partials, + bias, bf16 round (what the one-pass kernels stage in LDS),
+// then the epilogue; 8 columns per thread
+template <int EPI, int R>
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c8 = p.N / 8;
+  if (idx >= (int64_t)p.M * c8) return;
+  const int m = (int)(idx / c8);
+  const int n = (int)(idx % c8) * 8;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < p.splitk; ++k) {
+    const float* src = p.ws + ((int64_t)k * p.M + m) * p.N + n;
+    const f32x4 a = *(const f32x4*)src, b = *(const f32x4*)(src + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s[i] += a[i];
+      s[4 + i] += b[i];
+    }
+  }
+  bf16_t cv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cv[j] = f2bf(s[j] + (p.bias ? bf2f(p.bias[n + j]) : 0.f));
+  float o[8];
+  epilogue_row8<EPI, R>(p, m, n, cv, o);
+  u32x4 pk;
+  pk[0] = pack2(o[0], o[1]);
+  pk[1] = pack2(o[2], o[3]);
+  pk[2] = pack2(o[4], o[5]);
+  pk[3] = pack2(o[6], o[7]);
+  *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1076,6 +1128,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_p(const GemmParams p) {
 }
 
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
+static float* g_ws = nullptr;   // split-K workspace (caller-owned, ltx_gemm_set_workspace)
+static size_t g_ws_bytes = 0;
 static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (t-kernel, auto tile height),
                                 // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split,
                                 // 11 ping-pong, 12 interleaved DMA, 13/14/15 t-kernel 256/224/auto,
@@ -1160,7 +1214,25 @@ static int launch(const GemmParams& p, hipStream_t s) {
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 0>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
   } else {
     const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
-    hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(ntm * ntn), dim3(GEMM_THREADS), LDS_BYTES, s, p);
+    const int tiles = ntm * ntn;
+    const int nk = p.K / BK + p.K2 / BK;
+    // split-K when the grid leaves most CUs idle and each slice keeps >= 4 K-tiles
+    int S = 1;
+    if (tiles < 128 && nk >= 8) {
+      S = min(min(8, nk / 4), (256 + tiles - 1) / tiles);
+      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > g_ws_bytes) --S;
+    }
+    if (S > 1) {
+      GemmParams q = p;
+      q.ws = g_ws;
+      q.splitk = S;
+      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles * S), dim3(GEMM_THREADS), LDS_BYTES, s, q);
+      LTX_LAUNCH_CHECK();
+      const int64_t n8 = (int64_t)p.M * (p.N / 8);
+      hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, R>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, q);
+    } else {
+      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles), dim3(GEMM_THREADS), LDS_BYTES, s, p);
+    }
   }
   LTX_LAUNCH_CHECK();
   return LTX_OK;
@@ -1182,6 +1254,14 @@ using namespace ltx;
 
 extern "C" int ltx_gemm_set_variant(int variant) {
   g_variant = variant;
+  return LTX_OK;
+}
+
+extern "C" int ltx_gemm_set_workspace(void* ptr, int64_t bytes) {
+  LTX_CHECK_ARG(bytes >= 0 && (ptr != nullptr || bytes == 0) && ((uintptr_t)ptr % 16) == 0,
+                "gemm_set_workspace: bad buffer");
+  g_ws = (float*)ptr;
+  g_ws_bytes = (size_t)bytes;
   return LTX_OK;
 }
 
@@ -1228,6 +1308,7 @@ extern "C" int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, i
   p.aux0 = aux0; p.ld0 = ld0; p.aux1 = aux1; p.ld1 = ld1; p.aux2 = aux2; p.ld2 = ld2;
   p.alpha = alpha; p.rank = (int)rank; p.rows_per_batch = (int)(rows_per_batch > 0 ? rows_per_batch : M);
   p.A2 = (const bf16_t*)A2; p.W2 = (const bf16_t*)W2; p.lda2 = lda2; p.ldw2 = ldw2; p.K2 = (int)K2;
+  p.ws = nullptr; p.splitk = 1;
   hipStream_t s = (hipStream_t)stream;
   switch (epilogue) {
     case LTX_EPI_STORE: return launch<LTX_EPI_STORE>(p, s);

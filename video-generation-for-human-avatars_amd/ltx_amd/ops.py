@@ -316,12 +316,28 @@ def set_launch_timer(timer):
     _timer = timer
 
 
+_GEMM_WS = {}
+GEMM_WS_BYTES = 32 << 20
+
+
+def _gemm_workspace(device):
+    """The split-K workspace handed to the library once per process (caller-owned memory)."""
+    key = str(device)
+    if key not in _GEMM_WS:
+        ws = torch.empty(GEMM_WS_BYTES // 4, dtype=F32, device=device)
+        call("ltx_gemm_set_workspace", _p(ws), GEMM_WS_BYTES)
+        _GEMM_WS.clear()
+        _GEMM_WS[key] = ws
+    return _GEMM_WS[key]
+
+
 def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2=None,
          alpha=1.0, rank=0, rows_per_batch=0, ext=None):
     """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias) [+ a2 . w2^T]); see LTX_EPI_* in ltx_hip.h.
     ext = (a2 [M,K2], w2 [N,K2]) appends K-extension tiles (the fused LoRA branch)."""
     _need(a, BF16, "gemm a")
     _need(w, BF16, "gemm w")
+    _gemm_workspace(a.device)
     M, K = a.shape
     N, K2 = w.shape
     if K != K2:
