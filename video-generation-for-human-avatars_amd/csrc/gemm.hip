@@ -680,7 +680,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
 // (k-half, n-half) with the next quarter's fragments prefetched, one barrier per K-tile.
 // X pieces (8 rows x 128 B) go to waves 4w..4w+3 (for BMT = 224 wave 7 moves only W pieces).
 // ---------------------------------------------------------------------------------------------
-template <int EPI, int R, int BMT>
+template <int EPI, int R, int BMT, int DMAW>
 __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   static_assert(BMT == 256 || BMT == 224, "tile height");
   constexpr int WMW = (BMT == 256) ? 4 : 2;  // waves along m
@@ -706,16 +706,21 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   const int nk = nk_main + p.K2 / BK;
 
   // ---- DMA bookkeeping (see gemm_nt_kernel_l: per-lane 32-bit offsets, scalar bases)
+  // DMAW = waves that issue the LDS-DMA (8: all, 4 pieces of each operand each; 4: waves 0-3,
+  // 8 pieces each, so waves 4-7 only compute)
+  constexpr int PPW = 32 / DMAW;
   const int lrow = lane >> 3, pchunk = lane & 7;
-  const int xp = min(4, max(0, XPIECES - 4 * wv));  // X pieces of this wave (uniform)
-  uint32_t xo[4], wo[4];
+  const bool dma_wave = wv < DMAW;
+  const int xp = dma_wave ? min(PPW, max(0, XPIECES - PPW * wv)) : 0;  // X pieces of this wave
+  const int wp = dma_wave ? PPW : 0;                                     // W pieces of this wave
+  uint32_t xo[PPW], wo[PPW];
   const char* xb = nullptr;
   const char* wb = nullptr;
   auto set_x = [&](bool ext) {
     const int64_t ld = ext ? p.lda2 : p.lda;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = min((wave * 4 + i) * 8 + lrow, BMT - 1);
+    for (int i = 0; i < PPW; ++i) {
+      const int row = min(((wave % DMAW) * PPW + i) * 8 + lrow, BMT - 1);
       xo[i] = (uint32_t)(((int64_t)(min(m0 + row, p.M - 1) - m0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
     }
     xb = (const char*)(ext ? p.A2 : p.A) + (int64_t)m0 * ld * 2;
@@ -723,8 +728,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   auto set_w = [&](bool ext) {
     const int64_t ld = ext ? p.ldw2 : p.ldw;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (wave * 4 + i) * 8 + lrow;
+    for (int i = 0; i < PPW; ++i) {
+      const int row = ((wave % DMAW) * PPW + i) * 8 + lrow;
       wo[i] = (uint32_t)(((int64_t)(min(n0 + row, p.N - 1) - n0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
     }
     wb = (const char*)(ext ? p.W2 : p.W) + (int64_t)n0 * ld * 2;
@@ -740,17 +745,18 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   auto stage_x = [&](int st, int kt) {
     if (kt == nk_main && nk_main > 0) set_x(true);  // ext tiles come last, in issue order
     const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-    const uint32_t l = lds0 + st * ST + wv * 4096;
+    const uint32_t l = lds0 + st * ST + wv * (PPW * 1024);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < PPW; ++i)
       if (i < xp) glds_s(xo[i], sb, l + i * 1024);
   };
   auto stage_w = [&](int st, int kt) {
     if (kt == nk_main && nk_main > 0) set_w(true);
     const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-    const uint32_t l = lds0 + st * ST + XT + wv * 4096;
+    const uint32_t l = lds0 + st * ST + XT + wv * (PPW * 1024);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds_s(wo[i], sb, l + i * 1024);
+    for (int i = 0; i < PPW; ++i)
+      if (i < wp) glds_s(wo[i], sb, l + i * 1024);
   };
 
   const int wm = (WMW == 4) ? (wave >> 1) : (wave >> 2);
@@ -780,12 +786,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   if (nk > 1) {
     stage_x(1, 1);
     stage_w(1, 1);
-    if (xp == 4)
-      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-    else if (xp == 0)
-      asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    switch (xp + wp) {  // stage 0 landed: only this wave's stage-1 pieces may remain in flight
+      case 16: asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory"); break;
+      case 12: asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); break;
+    }
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
@@ -1156,24 +1163,33 @@ static int launch(const GemmParams& p, hipStream_t s) {
     }
     if (g_variant == 16)  // previous default: l-kernel, asm DMA, split issue, static priority
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant == 0 || (g_variant >= 13 && g_variant <= 15)) {
+    else if (g_variant == 0 || (g_variant >= 13 && g_variant <= 15) || g_variant == 17) {
       // default (0 = 15): gemm_nt_kernel_t with the tile height that fills the last round best;
       // 13 forces BMT 256, 14 forces BMT 224
       static bool t_set = false;
       if (!t_set) {
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
         t_set = true;
       }
       const int64_t ntn = (p.N + BN2 - 1) / BN2;
       const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
       // fraction of the last round of 256 CUs that has work, per tile height
       auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
-      const bool use224 = g_variant == 14 || ((g_variant == 15 || g_variant == 0) && fill(t224) > fill(t256) + 0.02);
-      if (use224)
-        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
-      else
-        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
+      const bool use224 = g_variant == 14 || ((g_variant == 15 || g_variant == 0 || g_variant == 17) &&
+                                              fill(t224) > fill(t256) + 0.02);
+      if (g_variant == 17) {  // DMA issued by waves 0-3 only
+        if (use224)
+          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
+        else
+          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 4>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
+      } else if (use224) {  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
+        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
+      } else {
+        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
+      }
     }
     else if (g_variant == 11) {  // ping-pong 8-phase kernel
       static bool pp_set = false;
