@@ -9,7 +9,10 @@ from ltx_amd import ops, _lib
 M = 14336
 SHAPES = {"ff_up_gelu": (M, 8192, 2048, "gelu"), "n8192_k8192": (M, 8192, 8192, "store"),
           "qkv": (M, 6144, 2048, "store"), "n2048_k2048": (M, 2048, 2048, "store"),
-          "n2048_k8192": (M, 2048, 8192, "store")}
+          "n2048_k8192": (M, 2048, 8192, "store"),
+          "out1_gres": (M, 2048, 2048, "gated_residual"), "ffdown_gres": (M, 2048, 8192, "gated_residual"),
+          "o2_accum": (M, 2048, 2048, "accum"), "ffdgrad_gelubwd": (M, 8192, 2048, "gelu_bwd")}
+ROWS = 1792  # rows per batch (gated residual gates)
 
 
 def timeit(fn, iters=20):
@@ -42,14 +45,22 @@ for name in names:
     w = (torch.randn(n, k, device="cuda") / k ** 0.5).bfloat16()
     bias = torch.randn(n, device="cuda").bfloat16()
     pre = torch.empty(m, n, device="cuda", dtype=torch.bfloat16) if epi == "gelu" else None
+    aux1 = None
+    if epi in ("gated_residual", "accum", "gelu_bwd"):
+        pre = torch.randn(m, n, device="cuda").bfloat16()
+    if epi == "gated_residual":
+        aux1 = torch.randn(m // ROWS, n, device="cuda").bfloat16()
+    if epi in ("accum", "gelu_bwd"):
+        bias = None
     c = torch.empty(m, n, device="cuda", dtype=torch.bfloat16)
+    kw = dict(bias=bias, epilogue=epi, aux0=pre, aux1=aux1, rows_per_batch=ROWS if aux1 is not None else 0)
     fl = 2.0 * m * n * k
     if args.only is not None:
         if args.torch:
             ms = timeit(lambda: torch.matmul(x, w.t()), args.iters)
         else:
             lib.ltx_gemm_set_variant(args.only)
-            ms = timeit(lambda: ops.gemm(x, w, bias=bias, epilogue=epi, aux0=pre, out=c), args.iters)
+            ms = timeit(lambda: ops.gemm(x, w, out=c, **kw), args.iters)
         print(f"{name} {'torch' if args.torch else 'v%d' % args.only} {fl / ms / 1e9:.1f} TF")
         continue
     if args.check:
@@ -57,13 +68,21 @@ for name in names:
         for v in [int(s2) for s2 in args.variants.split(",")]:
             lib.ltx_gemm_set_variant(v)
             c.fill_(0)
-            ops.gemm(x, w, bias=bias, epilogue=epi, aux0=pre, out=c)
+            ops.gemm(x, w, out=c, **kw)
             torch.cuda.synchronize()
             outs[v] = c.clone()
         lib.ltx_gemm_set_variant(0)
-        ref = (x.float() @ w.float().t() + bias.float())
+        ref = x.float() @ w.float().t() + (bias.float() if bias is not None else 0)
         if epi == "gelu":
             ref = torch.nn.functional.gelu(ref.bfloat16().float(), approximate="tanh")
+        elif epi == "gated_residual":
+            ref = pre.float() + aux1.float().repeat_interleave(ROWS, 0) * ref
+        elif epi == "accum":
+            ref = pre.float() + ref
+        elif epi == "gelu_bwd":
+            pf = pre.float().requires_grad_()
+            torch.nn.functional.gelu(pf, approximate="tanh").backward(ref)
+            ref = pf.grad
         v0 = list(outs)[0]
         for v, o in outs.items():
             rel = float((o.float() - ref).norm() / ref.norm())
@@ -72,7 +91,7 @@ for name in names:
     for rnd in range(3):
         for v in [int(s) for s in args.variants.split(",")]:
             lib.ltx_gemm_set_variant(v)
-            ms = timeit(lambda: ops.gemm(x, w, bias=bias, epilogue=epi, aux0=pre, out=c))
+            ms = timeit(lambda: ops.gemm(x, w, out=c, **kw))
             row.setdefault(f"v{v}", []).append(fl / ms / 1e9)
         ms = timeit(lambda: torch.matmul(x, w.t()))
         row.setdefault("torch", []).append(fl / ms / 1e9)

@@ -61,6 +61,37 @@ __device__ __forceinline__ float gelu_tanh_fast(float x) {
   float inner = kBeta * (x + kKappa * x_cube);
   return 0.5f * x * (1.0f + fast_tanh(inner));
 }
+// GEMM-epilogue forms on float pairs (v_pk_mul/fma/add_f32: two values per VALU instruction).
+// 0.5 x (1 + tanh(u)) == x * sigmoid(2u) == x / (1 + 2^w), w = -2 log2(e) u = x (A + B x^2):
+// 3 packed ops + v_exp_f32 + 1 packed add + v_rcp_f32 + 1 packed mul per pair instead of ~14 ops
+// per value. Differs from the tanh form by f32 rounding only (v_exp/v_rcp ~1 ulp).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+namespace gelu_k {
+constexpr float A = -2.0f * 0.7978845608028654f * 1.4426950408889634f;  // -2 sqrt(2/pi) log2(e)
+constexpr float B = A * 0.044715f;
+constexpr float C0 = 2.0f * 0.7978845608028654f;                        // 2u' = C0 + C1 x^2
+constexpr float C1 = 6.0f * 0.7978845608028654f * 0.044715f;
+}  // namespace gelu_k
+__device__ __forceinline__ f32x2 sigmoid2u_pk(f32x2 x, f32x2 x2) {
+  const f32x2 w = x * __builtin_elementwise_fma(x2, (f32x2)gelu_k::B, (f32x2)gelu_k::A);
+  f32x2 d;
+  d[0] = __builtin_amdgcn_exp2f(w[0]);
+  d[1] = __builtin_amdgcn_exp2f(w[1]);
+  d = d + 1.0f;
+  f32x2 s;
+  s[0] = __builtin_amdgcn_rcpf(d[0]);
+  s[1] = __builtin_amdgcn_rcpf(d[1]);
+  return s;
+}
+__device__ __forceinline__ f32x2 gelu_tanh_pk(f32x2 x) { return x * sigmoid2u_pk(x, x * x); }
+// d gelu / dx = s + x s (1 - s) 2u'  (s = sigmoid(2u); 0.5(1 + tanh) = s, 1 - tanh^2 = 4 s (1 - s))
+__device__ __forceinline__ f32x2 gelu_tanh_grad_pk(f32x2 x) {
+  const f32x2 x2 = x * x;
+  const f32x2 s = sigmoid2u_pk(x, x2);
+  const f32x2 du = __builtin_elementwise_fma(x2, (f32x2)gelu_k::C1, (f32x2)gelu_k::C0);
+  return __builtin_elementwise_fma(s * (x * (1.0f - s)), du, s);
+}
+
 // d gelu_tanh / dx, same association as ATen's GeluBackward (approximate="tanh"); the caller
 // multiplies by dy
 __device__ __forceinline__ float gelu_tanh_grad(float x) {

@@ -97,7 +97,11 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       *(u32x4*)((bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0) = pk;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) out8[j] = gelu_tanh_fast(v[j]);
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 g = gelu_tanh_pk((f32x2){v[j], v[j + 1]});
+      out8[j] = g[0];
+      out8[j + 1] = g[1];
+    }
   } else if constexpr (EPI == LTX_EPI_GATED_RESIDUAL) {
     // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1)
     const int b = m / p.rows_per_batch;
@@ -133,9 +137,11 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
     // dF = bf16(bf16(acc) * gelu'(F)), F = aux0 pre-activation bf16 (ld0)
     const u32x4 f4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float f = bf2f((bf16_t)(f4[j >> 1] >> ((j & 1) * 16)));
-      out8[j] = v[j] * gelu_tanh_grad(f);
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 f = {bf2f((bf16_t)f4[j >> 1]), bf2f((bf16_t)(f4[j >> 1] >> 16))};
+      const f32x2 g = (f32x2){v[j], v[j + 1]} * gelu_tanh_grad_pk(f);
+      out8[j] = g[0];
+      out8[j + 1] = g[1];
     }
   } else if constexpr (EPI == LTX_EPI_ACCUM) {
     // out = R + bf16(acc): R = aux0 (ld0); C may alias R
