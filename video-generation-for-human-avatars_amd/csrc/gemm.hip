@@ -686,9 +686,17 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
 // (k-half, n-half) with the next quarter's fragments prefetched, one barrier per K-tile.
 // X pieces (8 rows x 128 B) go to waves 4w..4w+3 (for BMT = 224 wave 7 moves only W pieces).
 // ---------------------------------------------------------------------------------------------
-template <int EPI, int R, int BMT, int DMAW>
+// STAMP (diagnostic build only, ltx_gemm_set_variant 19 + ltx_gemm_set_stamps): thread 0 of every
+// workgroup writes s_memrealtime (100 MHz) at start / after the prologue wait / after the main
+// loop / after the epilogue image barrier / at the end, plus HW_ID and XCC_ID, into a buffer of
+// its own (8 u64 per workgroup); no output value depends on them.
+static __device__ __forceinline__ uint64_t rt_stamp() { return __builtin_amdgcn_s_memrealtime(); }
+
+template <int EPI, int R, int BMT, int DMAW, int STAMP = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   static_assert(BMT == 256 || BMT == 224, "tile height");
+  uint64_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
+  if constexpr (STAMP) st0 = rt_stamp();
   constexpr int WMW = (BMT == 256) ? 4 : 2;  // waves along m
   constexpr int WNW = 8 / WMW;                // waves along n
   constexpr int WTM = BMT / WMW;              // 64 | 112
@@ -802,6 +810,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
+  if constexpr (STAMP) st1 = rt_stamp();
   s16x8 aE[NFH], aO[NFH], b0[MF], b1[MF];  // A even/odd quarter sets, B per k-half
 #pragma unroll
   for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(smem + aoff[0][i]);
@@ -856,6 +865,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   }
 #undef LTX_MFMA_T
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if constexpr (STAMP) st2 = rt_stamp();
 
   // epilogue stage 1: bf16(acc + bias) -> LDS image [BMT m][256 n]
   char* cimg = smem;
@@ -881,6 +891,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
     }
   }
   __syncthreads();
+  if constexpr (STAMP) st3 = rt_stamp();
   const int cgrp = tid & 31;
   for (int rr = tid >> 5; rr < BMT; rr += 512 / 32) {
     const int m = m0 + rr;
@@ -898,6 +909,15 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
     pk[2] = pack2(o[4], o[5]);
     pk[3] = pack2(o[6], o[7]);
     *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
+  }
+  if constexpr (STAMP) {
+    if (tid == 0) {
+      uint64_t* o = (uint64_t*)p.ws + (int64_t)blockIdx.x * 8;
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = rt_stamp();
+      o[5] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+      o[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      o[7] = (uint64_t)(tm * 65536 + tn);
+    }
   }
 }
 
@@ -1143,6 +1163,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_p(const GemmParams p) {
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
 static float* g_ws = nullptr;   // split-K workspace (caller-owned, ltx_gemm_set_workspace)
 static size_t g_ws_bytes = 0;
+static void* g_stamps = nullptr;  // diagnostic stamp buffer (variants 19/20)
 static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (t-kernel, auto tile height),
                                 // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split,
                                 // 11 ping-pong, 12 interleaved DMA, 13/14/15 t-kernel 256/224/auto,
@@ -1166,6 +1187,23 @@ static int launch(const GemmParams& p, hipStream_t s) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 35>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 99>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       attr_set = true;
+    }
+    if constexpr (EPI == LTX_EPI_STORE && R == 0) {
+      if (g_variant == 19 || g_variant == 20) {  // stamp diagnostics (19: 224-row, 20: 256-row tiles)
+        if (!g_stamps) return fail(LTX_ERR_BAD_ARG, "gemm variant 19/20: ltx_gemm_set_stamps first");
+        GemmParams q = p;
+        q.ws = (float*)g_stamps;
+        const int64_t ntn = (p.N + BN2 - 1) / BN2;
+        if (g_variant == 19) {
+          (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4, 1>), dim3((unsigned)(((p.M + 223) / 224) * ntn)), dim3(512), LDS2, s, q);
+        } else {
+          (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 1>), dim3((unsigned)(((p.M + 255) / 256) * ntn)), dim3(512), LDS2, s, q);
+        }
+        LTX_LAUNCH_CHECK();
+        return LTX_OK;
+      }
     }
     if (g_variant == 16)  // previous default: l-kernel, asm DMA, split issue, static priority
       hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
@@ -1276,6 +1314,12 @@ using namespace ltx;
 
 extern "C" int ltx_gemm_set_variant(int variant) {
   g_variant = variant;
+  return LTX_OK;
+}
+
+// diagnostic: stamp buffer of 8 u64 per workgroup for variants 19/20 (not in ltx_hip.h: tooling only)
+extern "C" int ltx_gemm_set_stamps(void* ptr) {
+  g_stamps = ptr;
   return LTX_OK;
 }
 
