@@ -232,6 +232,36 @@ int ltx_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_s
                    int is_bf16, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int64_t step, void* stream);
 
+/* ---- inference denoising step (csrc/denoise.hip) ------------------------------ */
+/* RoPE indices_grid of an inference call: latent coords * (sf_t, sf_h, sf_w) with the causal
+ * first-frame fix (vae_encode.py:215-226), as float32 with the time axis / frame_rate
+ * (pipeline_ltx_video.py:1121-1122). out [B,3,F*H*W] f32; pixel_out [B,3,N] int64 or null. */
+int ltx_pixel_coords_f32(float* out, int64_t* pixel_out, int64_t B, int64_t F, int64_t H,
+                         int64_t W, int64_t sf_t, int64_t sf_h, int64_t sf_w, int causal_fix,
+                         float frame_rate, void* stream);
+/* Skip-layer (STG) blend, eager bf16: out = bf16(bf16(a*m) + bf16(c*bf16(1-m))), m =
+ * mask[row / rows_per_batch] (bf16 [B]): AttentionSkip / AttentionValues before to_out
+ * (attention.py:1071-1085), TransformerBlock on the block output (attention.py:312-319). */
+int ltx_skip_blend_bf16(const void* a, int64_t lda, const void* c, int64_t ldc, const void* mask,
+                        void* out, int64_t ldo, int64_t M, int64_t D, int64_t rows_per_batch,
+                        void* stream);
+/* RectifiedFlowScheduler.step, deterministic (rf.py:305-374) + denoising_step's keep
+ * (pipeline_ltx_video.py:1346-1379): dt = t - max{sched[k] < t - 1e-6} (0 if none),
+ * out = sample - dt * v over [BN, C]; timestep f32 [1] (global) or [BN] (per_token);
+ * round_v = eager semantics of a 0-dim dt times a bf16 prediction (dt and the product rounded
+ * to bf16); cond_mask f32 [BN] or null: out = sample where !(t_cond - 1e-6 < 1 - cond_mask).
+ * sample / v / out each f32 or bf16 (flags). */
+int ltx_rf_euler_step(const void* sample, int sample_f32, const void* v, int v_f32,
+                      const float* timestep, int per_token, const float* sched, int64_t nsched,
+                      const float* cond_mask, float t_cond, int round_v, void* out, int out_f32,
+                      int64_t BN, int64_t C, void* stream);
+/* CFG / CFG* / STG / STG rescaling of the batched prediction pred [nc*B, L] bf16 (chunks
+ * uncond | text | perturbed, only the active ones) -> out [B, L] bf16, per-op bf16 rounding as
+ * pipeline_ltx_video.py:1229-1268 evaluates it eagerly. workspace >= B * 258 floats. */
+int ltx_guidance_bf16(const void* pred, int64_t B, int64_t L, int do_cfg, int do_stg,
+                      float guidance_scale, float stg_scale, float rescaling_scale, int cfg_star,
+                      float* workspace, int64_t ws_floats, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

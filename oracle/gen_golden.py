@@ -25,6 +25,9 @@ Fixtures (safetensors + a JSON sidecar each):
   rf_sched          RectifiedFlowScheduler add_noise / build_velocity_target / shift_timesteps
                     (rf.py:216-225, 376-426) and the train_step t-sampling (training.py:124-132).
   train_config      load_train_config_from_yaml(configs/train-avatars.yaml) (config.py:62-154).
+  infer_step        inference call of the tiny model (CFG+STG batch of 3, float pixel coords,
+                    per-token timesteps, every SkipLayerStrategy) and RectifiedFlowScheduler
+                    set_timesteps / step, global and per-token (rf.py:179-374).
 """
 import dataclasses
 import json
@@ -276,6 +279,88 @@ def gen_rf():
                             "tsample_seed": 31337})
 
 
+def gen_infer():
+    """Inference path: one denoising step's transformer call as
+    pipeline_ltx_video.py:1089-1228 makes it -- CFG + STG batch of 3 (uncond, cond, perturbed),
+    float pixel coordinates / frame_rate, per-token timesteps min(t, 1 - conditioning_mask), a
+    skip-layer mask for block 1 of the perturbed batch -- through the reference
+    Transformer3DModel.forward for every SkipLayerStrategy; plus RectifiedFlowScheduler
+    set_timesteps / step (rf.py:179-374), global and per-token."""
+    from ltx_video.utils.skip_layer_strategy import SkipLayerStrategy
+
+    def latent_to_pixel_coords_from_factors(latent_coords, scale_factors, causal_fix=False):
+        # vae_encode.py:215-226 (its module imports the VAE, which the shim does not provide)
+        pixel_coords = latent_coords * torch.tensor(scale_factors)[None, :, None]
+        if causal_fix:
+            pixel_coords[:, 0] = (pixel_coords[:, 0] + 1 - scale_factors[0]).clamp(min=0)
+        return pixel_coords
+
+    seed, rank, frame_rate = 1234, 16, 25.0
+    model, pf = _build(TINY_CONFIG, seed, torch.bfloat16, rank)
+    core = model.base_model.model
+    core.eval()
+    g = torch.Generator().manual_seed(2024)
+    F_, H_, W_ = 2, 8, 8
+    latents = torch.randn(1, 128, F_, H_, W_, generator=g)
+    tokens, lat_coords = pf.patchify(latents)
+    ref = torch.randn(1, 128, 1, H_, W_, generator=g)
+    pose = torch.randn(1, 128, F_, H_, W_, generator=g)
+    neg = torch.randn(1, 4, 64, generator=g)
+    pos = torch.randn(1, 4, 64, generator=g)
+    nc = 3
+    enc = torch.cat([neg, pos, pos]).to(torch.bfloat16)
+    enc_mask = torch.tensor([[1, 1, 0, 0], [1, 1, 1, 0], [1, 1, 1, 0]], dtype=torch.long)
+    pixel = latent_to_pixel_coords_from_factors(lat_coords, (8, 32, 32), causal_fix=True)
+    frac = torch.cat([pixel] * nc).to(torch.float32)
+    frac[:, 0] = frac[:, 0] * (1.0 / frame_rate)
+    cond_mask = torch.zeros(1, tokens.shape[1])
+    cond_mask[:, : H_ * W_] = 1.0  # first latent frame hard-conditioned
+    t = torch.tensor(0.7)
+    ts_global = t[None].expand(nc).unsqueeze(-1)
+    ts_tok = torch.min(ts_global, 1.0 - torch.cat([cond_mask] * nc))
+    skip = core.create_skip_layer_mask(1, nc, nc - 1, [1])
+    x = torch.cat([tokens] * nc).to(torch.bfloat16)
+    kw = dict(indices_grid=frac, ref_image_hidden_states=torch.cat([ref] * nc).to(torch.bfloat16),
+              pose_hidden_states=torch.cat([pose] * nc).to(torch.bfloat16),
+              encoder_hidden_states=enc, encoder_attention_mask=enc_mask, return_dict=False)
+    out = {"in.tokens": x, "in.indices_grid": frac, "in.ref": kw["ref_image_hidden_states"],
+           "in.pose": kw["pose_hidden_states"], "in.enc": enc, "in.enc_mask": enc_mask,
+           "in.ts_global": ts_global, "in.ts_tok": ts_tok, "in.skip_layer_mask": skip,
+           "in.pixel_coords": pixel, "in.cond_mask": cond_mask}
+    with torch.no_grad():
+        out["out.global"] = core(hidden_states=x.clone(), timestep=ts_global, **kw)[0]
+        out["out.tok"] = core(hidden_states=x.clone(), timestep=ts_tok, **kw)[0]
+        for s in SkipLayerStrategy:
+            out[f"out.tok_{s.name}"] = core(hidden_states=x.clone(), timestep=ts_tok,
+                                            skip_layer_mask=skip, skip_layer_strategy=s, **kw)[0]
+    # scheduler (rf.py:179-374)
+    g2 = torch.Generator().manual_seed(77)
+    sample = torch.randn(2, 64, 16, generator=g2)
+    v = torch.randn(2, 64, 16, generator=g2)
+    for name, sch in (("Uniform", RectifiedFlowScheduler(sampler="Uniform")),
+                      ("LinearQuadratic", RectifiedFlowScheduler(sampler="LinearQuadratic")),
+                      ("SD3", RectifiedFlowScheduler(sampler="Uniform", shifting="SD3",
+                                                     target_shift_terminal=0.1))):
+        sch.set_timesteps(num_inference_steps=20, samples_shape=torch.Size([2, 128, 7, 16, 16]))
+        out[f"sched.{name}.timesteps"] = sch.timesteps
+        tg = sch.timesteps[3]
+        out[f"sched.{name}.prev_global"] = sch.step(v, tg, sample, return_dict=False)[0]
+        out[f"sched.{name}.prev_global_bf16v"] = sch.step(v.to(torch.bfloat16), tg, sample,
+                                                          return_dict=False)[0]
+        tt = torch.full((2, 64), float(tg))
+        tt[:, 0] = 0.0
+        tt[1, 5] = float((sch.timesteps[5] + sch.timesteps[6]) / 2)
+        out[f"sched.{name}.t_tok"] = tt
+        out[f"sched.{name}.prev_tok"] = sch.step(v, tt, sample, return_dict=False)[0]
+    out["sched.sample"] = sample
+    out["sched.v"] = v
+    meta = {"config": TINY_CONFIG, "param_seed": seed, "lora_rank": rank, "lora_alpha": rank,
+            "frame_rate": frame_rate, "t": 0.7, "strategies": [s.name for s in SkipLayerStrategy],
+            "source": "reference Transformer3DModel.forward (inference call, "
+                      "pipeline_ltx_video.py:1089-1228) + rf.py:179-374 via oracle/shim"}
+    _save("infer_step", out, meta)
+
+
 def gen_config():
     cfg = load_train_config_from_yaml(os.path.join(REF, "configs", "train-avatars.yaml"))
     d = dataclasses.asdict(cfg)
@@ -293,3 +378,4 @@ if __name__ == "__main__":
     gen_rope()
     gen_tiny()
     gen_block2b()
+    gen_infer()

@@ -165,8 +165,15 @@ def caption_projection(p, enc):
 # ----------------------------------------------------------------------------------------------
 # attention + block
 # ----------------------------------------------------------------------------------------------
-def attention(p, name, x, heads, freqs=None, enc=None, mask_bias=None, lora_scaling=1.0):
-    """Attention + AttnProcessor2_0.__call__ (attention.py:935-1114), training branch."""
+SKIP_STRATEGIES = ("AttentionSkip", "AttentionValues", "Residual", "TransformerBlock")
+
+
+def attention(p, name, x, heads, freqs=None, enc=None, mask_bias=None, lora_scaling=1.0,
+              skip_mask=None, skip_strategy=None):
+    """Attention + AttnProcessor2_0.__call__ (attention.py:935-1114). skip_mask [B] (this block's
+    row of the skip-layer mask) blends the SDPA output before to_out (attention.py:1071-1085):
+    AttentionSkip with the processor input, AttentionValues with to_v's output. Residual only
+    acts when attn.residual_connection (False in LTX: a no-op, attention.py:1103-1110)."""
     B = x.shape[0]
     q = lora_linear(x, p, name + ".to_q", lora_scaling)
     q = rmsnorm(q, 1e-5, p[name + ".q_norm.weight"])
@@ -177,6 +184,7 @@ def attention(p, name, x, heads, freqs=None, enc=None, mask_bias=None, lora_scal
         k = apply_rotary_emb(k, *freqs)
         q = apply_rotary_emb(q, *freqs)
     v = lora_linear(src, p, name + ".to_v", lora_scaling)
+    value_for_stg = v
     hd = k.shape[-1] // heads
     q = q.view(B, -1, heads, hd).transpose(1, 2)
     k = k.view(B, -1, heads, hd).transpose(1, 2)
@@ -186,20 +194,31 @@ def attention(p, name, x, heads, freqs=None, enc=None, mask_bias=None, lora_scal
         mask = mask_bias.repeat_interleave(heads, dim=0).view(B, heads, -1, mask_bias.shape[-1])
     o = F.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=0.0, is_causal=False)
     o = o.transpose(1, 2).reshape(B, -1, heads * hd).to(q.dtype)
+    if skip_mask is not None:
+        m = skip_mask.reshape(B, 1, 1)
+        if skip_strategy == "AttentionSkip":
+            o = o * m + x * (1.0 - m)
+        elif skip_strategy == "AttentionValues":
+            o = o * m + value_for_stg * (1.0 - m)
     return lora_linear(o, p, name + ".to_out.0", lora_scaling)
 
 
-def block(p, i, h, freqs, enc, enc_bias, tmod, heads, lora_scaling=1.0, eps=1e-6):
-    """BasicTransformerBlock.forward (attention.py:198-321), single_scale_shift, rms_norm."""
+def block(p, i, h, freqs, enc, enc_bias, tmod, heads, lora_scaling=1.0, eps=1e-6,
+          skip_mask=None, skip_strategy=None):
+    """BasicTransformerBlock.forward (attention.py:198-321), single_scale_shift, rms_norm;
+    skip_mask [B] is passed to attn1 only, TransformerBlock blends the block output with its
+    input (attention.py:312-319)."""
     pre = f"transformer_blocks.{i}"
     B = h.shape[0]
+    original = h
     n = rmsnorm(h, eps)
     sst = p[pre + ".scale_shift_table"]
     ada = sst[None, None] + tmod.reshape(B, tmod.shape[1], 6, -1)
     sh_msa, sc_msa, g_msa, sh_mlp, sc_mlp, g_mlp = ada.unbind(dim=2)
     n = n * (1 + sc_msa) + sh_msa
     n = n.squeeze(1)
-    a = attention(p, pre + ".attn1", n, heads, freqs=freqs, lora_scaling=lora_scaling)
+    a = attention(p, pre + ".attn1", n, heads, freqs=freqs, lora_scaling=lora_scaling,
+                  skip_mask=skip_mask, skip_strategy=skip_strategy)
     h = g_msa * a + h
     a = attention(p, pre + ".attn2", h, heads, enc=enc, mask_bias=enc_bias,
                   lora_scaling=lora_scaling)
@@ -209,12 +228,18 @@ def block(p, i, h, freqs, enc, enc_bias, tmod, heads, lora_scaling=1.0, eps=1e-6
     f = linear(n, p, pre + ".ff.net.0.proj")
     f = F.gelu(f, approximate="tanh")
     f = linear(f, p, pre + ".ff.net.2")
-    return g_mlp * f + h
+    h = g_mlp * f + h
+    if skip_mask is not None and skip_strategy == "TransformerBlock":
+        m = skip_mask.view(-1, 1, 1)
+        h = h * m + original * (1.0 - m)
+    return h
 
 
 def forward(p, cfg, hidden_states, indices_grid, ref_image_hidden_states, pose_hidden_states,
-            encoder_hidden_states, timestep, encoder_attention_mask=None, lora_scaling=1.0):
-    """Transformer3DModel.forward (transformer3d.py:361-565), training call (no skip layers).
+            encoder_hidden_states, timestep, encoder_attention_mask=None, lora_scaling=1.0,
+            skip_layer_mask=None, skip_layer_strategy=None):
+    """Transformer3DModel.forward (transformer3d.py:361-565): timestep [B], [B,1] or per token
+    [B,N]; skip_layer_mask [num_layers, B] with a SkipLayerStrategy name (inference / STG).
     Does NOT mutate ``hidden_states`` (the reference does, in place, transformer3d.py:447-466)."""
     dtype = p["patchify_proj.weight"].dtype
     heads = cfg["num_attention_heads"]
@@ -240,7 +265,9 @@ def forward(p, cfg, hidden_states, indices_grid, ref_image_hidden_states, pose_h
     enc = caption_projection(p, encoder_hidden_states).view(B, -1, D)
     for i in range(cfg["num_layers"]):
         h = block(p, i, h, freqs, enc, enc_bias, tmod, heads, lora_scaling,
-                  eps=cfg.get("norm_eps", 1e-6))
+                  eps=cfg.get("norm_eps", 1e-6),
+                  skip_mask=None if skip_layer_mask is None else skip_layer_mask[i],
+                  skip_strategy=skip_layer_strategy)
     ssv = p["scale_shift_table"][None, None] + emb[:, :, None]
     shift, scale = ssv[:, :, 0], ssv[:, :, 1]
     h = F.layer_norm(h, (D,), eps=1e-6)
@@ -278,6 +305,99 @@ def train_step(p, cfg, latents, ref_image_latents, pose_latents, prompt_embeds,
     nrmse = torch.sqrt(loss) / (std + 1e-12)
     return {"loss": loss, "rel_mse": rel, "nrmse": nrmse, "sample": out, "t": t, "noise": noise,
             "x_t": x_t, "v_target": v, "coords": coords}
+
+
+# ----------------------------------------------------------------------------------------------
+# inference denoising step
+# ----------------------------------------------------------------------------------------------
+def pixel_coords(latent_coords, scale_factors=(8, 32, 32), causal_fix=True):
+    """latent_to_pixel_coords_from_factors (ltx_video/models/autoencoders/vae_encode.py:215-226)."""
+    pc = latent_coords * torch.tensor(scale_factors, device=latent_coords.device)[None, :, None]
+    if causal_fix:
+        pc[:, 0] = (pc[:, 0] + 1 - scale_factors[0]).clamp(min=0)
+    return pc
+
+
+def fractional_coords(pixel, frame_rate):
+    """pipeline_ltx_video.py:1121-1122: float pixel coordinates, time axis / frame_rate."""
+    f = pixel.to(torch.float32)
+    f[:, 0] = f[:, 0] * (1.0 / frame_rate)
+    return f
+
+
+def linear_quadratic_schedule(num_steps, threshold_noise=0.025, linear_steps=None):
+    """rf.py:25-46."""
+    if num_steps == 1:
+        return torch.tensor([1.0])
+    if linear_steps is None:
+        linear_steps = num_steps // 2
+    lin = [i * threshold_noise / linear_steps for i in range(linear_steps)]
+    diff = linear_steps - threshold_noise * num_steps
+    qsteps = num_steps - linear_steps
+    qcoef = diff / (linear_steps * qsteps ** 2)
+    lcoef = threshold_noise / linear_steps - 2 * diff / (qsteps ** 2)
+    const = qcoef * (linear_steps ** 2)
+    quad = [qcoef * (i ** 2) + lcoef * i + const for i in range(linear_steps, num_steps)]
+    sched = [1.0 - x for x in lin + quad + [1.0]]
+    return torch.tensor(sched[:-1])
+
+
+def rf_step(model_output, timestep, sample, timesteps, t_eps=1e-6):
+    """RectifiedFlowScheduler.step, deterministic branch (rf.py:305-374): Euler to the next lower
+    scheduled timestep, global (0-dim t) or per token ([B,N] t)."""
+    padded = torch.cat([timesteps, torch.zeros(1, device=timesteps.device)])
+    if timestep.ndim == 0:
+        lower = padded[padded < timestep - t_eps][0]
+        dt = timestep - lower
+    else:
+        lower_mask = padded[:, None, None] < timestep[None] - t_eps
+        lower, _ = (lower_mask * padded[:, None, None]).max(dim=0)
+        dt = (timestep - lower)[..., None]
+    return sample - dt * model_output
+
+
+def denoising_step(latents, noise_pred, current_timestep, conditioning_mask, t, timesteps,
+                   t_eps=1e-6):
+    """LTXVideoPipeline.denoising_step (pipeline_ltx_video.py:1346-1379)."""
+    den = rf_step(noise_pred, t if current_timestep is None else current_timestep, latents,
+                  timesteps)
+    if conditioning_mask is None:
+        return den
+    keep = (t - t_eps < (1.0 - conditioning_mask)).unsqueeze(-1)
+    return torch.where(keep, den, latents)
+
+
+def guidance(noise_pred, batch_size, do_cfg, do_stg, guidance_scale=1.0, stg_scale=0.0,
+             rescaling_scale=1.0, cfg_star_rescale=False):
+    """CFG / CFG* / STG / rescaling of the batched prediction (pipeline_ltx_video.py:1229-1268),
+    in the prediction's dtype (eager bf16 ops)."""
+    num_conds = 1 + int(do_cfg) + int(do_stg)
+    chunks = noise_pred.chunk(num_conds)
+    if do_stg:
+        text, perturb = chunks[-2:]
+    if do_cfg:
+        uncond, text = chunks[:2]
+        if cfg_star_rescale:
+            pf = text.view(batch_size, -1)
+            nf = uncond.view(batch_size, -1)
+            dot = torch.sum(pf * nf, dim=1, keepdim=True)
+            sq = torch.sum(nf ** 2, dim=1, keepdim=True) + 1e-8
+            alpha = dot / sq
+            uncond = alpha * uncond
+        out = uncond + guidance_scale * (text - uncond)
+    elif do_stg:
+        out = text
+    else:
+        out = noise_pred
+    if do_stg:
+        out = out + stg_scale * (text - perturb)
+        if rescaling_scale != 1.0 and stg_scale > 0.0:
+            text_std = text.view(batch_size, -1).std(dim=1, keepdim=True)
+            out_std = out.view(batch_size, -1).std(dim=1, keepdim=True)
+            factor = text_std / out_std
+            factor = rescaling_scale * factor + (1 - rescaling_scale)
+            out = out * factor.view(batch_size, 1, 1)
+    return out
 
 
 def trainable_names(names):

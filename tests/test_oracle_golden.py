@@ -126,3 +126,74 @@ def test_param_init_is_pinned():
         h.update(canonical_name(name).encode())
         h.update(p[name].detach().to(torch.float32).contiguous().numpy().tobytes())
     assert h.hexdigest() == meta["weights_sha256"]
+
+
+# ---- inference denoising step ---------------------------------------------
+def _infer_inputs(d):
+    return dict(indices_grid=d["in.indices_grid"], ref_image_hidden_states=d["in.ref"],
+                pose_hidden_states=d["in.pose"], encoder_hidden_states=d["in.enc"],
+                encoder_attention_mask=d["in.enc_mask"])
+
+
+def test_infer_pixel_coords_match_reference():
+    d, meta = _load("infer_step")
+    _, lat = O.patchify(torch.zeros(1, 1, 2, 8, 8))
+    pc = O.pixel_coords(lat, (8, 32, 32), causal_fix=True)
+    assert torch.equal(pc, d["in.pixel_coords"])
+    frac = O.fractional_coords(torch.cat([pc] * 3), meta["frame_rate"])
+    assert torch.equal(frac, d["in.indices_grid"])
+
+
+@pytest.mark.parametrize("case", ["global", "tok", "tok_AttentionSkip", "tok_AttentionValues",
+                                  "tok_Residual", "tok_TransformerBlock"])
+def test_infer_forward_matches_reference(case):
+    d, meta = _load("infer_step")
+    tiny, _ = _load("tiny_train_step")  # same config and parameter seed -> same weights
+    p = {k[2:]: v for k, v in tiny.items() if k.startswith("w.")}
+    ts = d["in.ts_global"] if case == "global" else d["in.ts_tok"]
+    strat = case[4:] if case.startswith("tok_") else None
+    with torch.no_grad():
+        out = O.forward(p, meta["config"], d["in.tokens"], timestep=ts,
+                        skip_layer_mask=d["in.skip_layer_mask"] if strat else None,
+                        skip_layer_strategy=strat, **_infer_inputs(d))
+    assert _rel(out, d["out." + case]) < 2e-3, case
+
+
+@pytest.mark.parametrize("name", ["Uniform", "LinearQuadratic", "SD3"])
+def test_infer_scheduler_matches_reference(name):
+    d, _ = _load("infer_step")
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    kw = {"Uniform": {}, "LinearQuadratic": {"sampler": "LinearQuadratic"},
+          "SD3": {"shifting": "SD3", "target_shift_terminal": 0.1}}[name]
+    sch = RectifiedFlowScheduler(**kw)
+    sch.set_timesteps(num_inference_steps=20, samples_shape=torch.Size([2, 128, 7, 16, 16]))
+    ts = d[f"sched.{name}.timesteps"]
+    assert torch.allclose(sch.timesteps, ts, rtol=0, atol=1e-7)
+    s, v = d["sched.sample"], d["sched.v"]
+    assert torch.equal(O.rf_step(v, ts[3], s, ts), d[f"sched.{name}.prev_global"])
+    assert torch.equal(O.rf_step(v.to(torch.bfloat16), ts[3], s, ts),
+                       d[f"sched.{name}.prev_global_bf16v"])
+    assert torch.equal(O.rf_step(v, d[f"sched.{name}.t_tok"], s, ts), d[f"sched.{name}.prev_tok"])
+
+
+@pytest.mark.parametrize("sampler", ["LinearQuadratic", "Uniform"])
+def test_reference_scheduler_cases(sampler):
+    """The reference's own tests/test_scheduler.py cases, restated against the oracle step."""
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    sch = RectifiedFlowScheduler(sampler=sampler)
+    g = torch.Generator().manual_seed(0)
+    lat = torch.randn(2, 4096, 128, generator=g)
+    sch.set_timesteps(num_inference_steps=20, samples_shape=lat.shape)
+    ts = sch.timesteps
+    for i, t in enumerate(ts):
+        v = torch.randn(lat.shape, generator=g)
+        nt = ts[i + 1] if i < len(ts) - 1 else 0.0
+        assert torch.allclose(O.rf_step(v, t, lat, ts), lat - (t - nt) * v, atol=1e-6)
+        tt = torch.full(lat.shape[:2], float(t))
+        tt[:, 0] = 0.0
+        out = O.rf_step(v, tt, lat, ts)
+        assert torch.allclose(out[:, 1:], (lat - (t - nt) * v)[:, 1:], atol=1e-6)
+        assert torch.allclose(out[:, 0], lat[:, 0], atol=1e-6)
+        tm = (ts[i] + ts[i + 1]) / 2 if i < len(ts) - 1 else ts[i] / 2
+        out = O.rf_step(v, torch.full(lat.shape[:2], float(tm)), lat, ts)
+        assert torch.allclose(out, lat - (tm - nt) * v, atol=1e-6)

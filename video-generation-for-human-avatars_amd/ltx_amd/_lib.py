@@ -60,6 +60,11 @@ _SIGNATURES = {
     "ltx_batch_sum_bf16": [_p, _i64, _i64, _i64, _i64, _p, _i64, _p],
     "ltx_mse_fwd_bwd": [_p, _p, _p, _p, _i64, _f32, _p],
     "ltx_adamw_step": [_p, _p, _p, _p, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i64, _p],
+    "ltx_pixel_coords_f32": [_p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p],
+    "ltx_skip_blend_bf16": [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p],
+    "ltx_rf_euler_step": [_p, _i32, _p, _i32, _p, _i32, _p, _i64, _p, _f32, _i32, _p, _i32, _i64,
+                          _i64, _p],
+    "ltx_guidance_bf16": [_p, _i64, _i64, _i32, _i32, _f32, _f32, _f32, _i32, _p, _i64, _p, _p],
 }
 
 EPI = {"store": 0, "gelu": 1, "gated_residual": 2, "lora": 3, "lora_residual": 4,

@@ -482,3 +482,79 @@ def adamw_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_d
     call("ltx_adamw_step", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), param.numel(),
          is_bf16, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay),
          int(step), _s())
+
+
+# ---------------------------------------------------------------------------------------------
+# inference denoising step (csrc/denoise.hip)
+# ---------------------------------------------------------------------------------------------
+def pixel_coords(B, F, H, W, device, scale_factors=(8, 32, 32), causal_fix=True, frame_rate=25.0):
+    """(float indices_grid [B,3,N] with the time axis / frame_rate, int64 pixel coords [B,3,N])
+    (vae_encode.py:215-226, pipeline_ltx_video.py:1121-1122)."""
+    out = torch.empty(B, 3, F * H * W, dtype=F32, device=device)
+    pix = torch.empty(B, 3, F * H * W, dtype=torch.int64, device=device)
+    call("ltx_pixel_coords_f32", _p(out), _p(pix), B, F, H, W, int(scale_factors[0]),
+         int(scale_factors[1]), int(scale_factors[2]), 1 if causal_fix else 0, float(frame_rate),
+         _s())
+    return out, pix
+
+
+def skip_blend(a, c, mask, rows_per_batch, out=None):
+    """bf16(bf16(a * m) + bf16(c * bf16(1 - m))), m = mask[row // rows_per_batch] (bf16 [B])."""
+    _need(a, BF16, "a")
+    _need(c, BF16, "c")
+    M, D = a.shape
+    mask = mask.to(BF16).contiguous()
+    out = torch.empty(M, D, dtype=BF16, device=a.device) if out is None else out
+    call("ltx_skip_blend_bf16", _p(a), _rows(a, "a"), _p(c), _rows(c, "c"), _p(mask), _p(out),
+         _rows(out, "out"), M, D, rows_per_batch, _s())
+    return out
+
+
+def rf_euler_step(model_output, timestep, sample, timesteps, cond_mask=None, t_cond=0.0):
+    """RectifiedFlowScheduler.step (rf.py:305-374, deterministic) with eager dtype semantics:
+    0-dim timestep -> global dt (a bf16 prediction rounds dt and dt*v to bf16), [B,N] timestep ->
+    per-token dt in f32. Output dtype = torch's promotion of (sample, dt * v). cond_mask [B,N]:
+    denoising_step's keep (pipeline_ltx_video.py:1378-1379) at scalar t_cond."""
+    if model_output.shape != sample.shape:
+        raise ValueError("rf_euler_step: model_output and sample shapes differ")
+    for t, n in ((model_output, "model_output"), (sample, "sample")):
+        if t.dtype not in (F32, BF16):
+            raise TypeError(f"{n}: f32 or bf16 expected")
+        if not t.is_cuda:
+            raise _lib.LtxHipError(f"{n}: tensor is not on a ROCm device (no CPU fallback)")
+    dev = sample.device
+    per_token = timestep.ndim != 0
+    if per_token and timestep.ndim != 2:
+        raise ValueError("per-token timesteps must be [B, N]")
+    ts = timestep.to(device=dev, dtype=F32).contiguous().reshape(-1)
+    sched = timesteps.to(device=dev, dtype=F32).contiguous()
+    v_f32 = model_output.dtype == F32
+    prod_dtype = F32 if (per_token or v_f32) else BF16
+    out_dtype = torch.promote_types(sample.dtype, prod_dtype)
+    C = sample.shape[-1]
+    BN = sample.numel() // C
+    out = torch.empty(sample.shape, dtype=out_dtype, device=dev)
+    cm = None if cond_mask is None else cond_mask.to(device=dev, dtype=F32).contiguous()
+    call("ltx_rf_euler_step", _p(sample.contiguous()), 1 if sample.dtype == F32 else 0,
+         _p(model_output.contiguous()), 1 if v_f32 else 0, _p(ts), 1 if per_token else 0,
+         _p(sched), sched.numel(), _p(cm), float(t_cond), 0 if (per_token or v_f32) else 1,
+         _p(out), 1 if out_dtype == F32 else 0, BN, C, _s())
+    return out
+
+
+def guidance(noise_pred, batch_size, do_cfg, do_stg, guidance_scale=1.0, stg_scale=0.0,
+             rescaling_scale=1.0, cfg_star_rescale=False):
+    """CFG / CFG* / STG / rescaling (pipeline_ltx_video.py:1229-1268) of the batched bf16
+    prediction [nc*B, ...] -> [B, ...] bf16."""
+    _need(noise_pred, BF16, "noise_pred")
+    nc = 1 + int(bool(do_cfg)) + int(bool(do_stg))
+    if noise_pred.shape[0] != nc * batch_size:
+        raise ValueError(f"noise_pred batch {noise_pred.shape[0]} != {nc} x {batch_size}")
+    pred = noise_pred.contiguous()
+    L = pred[0].numel()
+    out = torch.empty((batch_size,) + tuple(pred.shape[1:]), dtype=BF16, device=pred.device)
+    ws = torch.empty(batch_size * 258, dtype=F32, device=pred.device)
+    call("ltx_guidance_bf16", _p(pred), batch_size, L, int(bool(do_cfg)), int(bool(do_stg)),
+         float(guidance_scale), float(stg_scale), float(rescaling_scale),
+         int(bool(cfg_star_rescale)), _p(ws), ws.numel(), _p(out), _s())
+    return out

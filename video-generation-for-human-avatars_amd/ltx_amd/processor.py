@@ -2,8 +2,8 @@
 935-1114). Computes one Attention call (q/k/v projections with optional LoRA, q/k RMSNorm, RoPE
 for self-attention, SDPA, to_out) with the same kernels the fused block uses.
 
-Round-1 scope: forward only (inference / pipeline use, e.g. LTXVideoPipeline's
-`transformer(...)` calls). Training runs the fused per-block autograd Function instead; calling
+Forward only (inference / pipeline use, e.g. LTXVideoPipeline's `transformer(...)` calls),
+including the skip-layer (STG) blends of attention.py:1071-1085. Training runs the fused per-block autograd Function instead; calling
 this processor on tensors that require grad raises.
 """
 import torch
@@ -18,8 +18,6 @@ class HipAttnProcessor:
         from .transformer3d import _lin
         if torch.is_grad_enabled() and hidden_states.requires_grad:
             raise NotImplementedError("HipAttnProcessor is forward-only; training uses the fused block")
-        if skip_layer_mask is not None:
-            raise NotImplementedError("skip-layer (STG) blending is an inference row not yet built")
         B, N, Dq = hidden_states.shape
         src = hidden_states if encoder_hidden_states is None else encoder_hidden_states
         L = src.shape[1]
@@ -50,5 +48,13 @@ class HipAttnProcessor:
         if attention_mask is not None:
             bias = attention_mask.reshape(B, -1).float().contiguous()
         o, _ = ops.attn_fwd(q, k, v, B, H, d, attn.scale, key_bias=bias)
+        if skip_layer_mask is not None and skip_layer_strategy is not None:
+            # attention.py:1071-1085 (Residual needs attn.residual_connection: False in LTX)
+            name = getattr(skip_layer_strategy, "name", str(skip_layer_strategy))
+            m = skip_layer_mask.reshape(B).to(torch.bfloat16)
+            if name == "AttentionSkip":
+                o = ops.skip_blend(o, x, m, N)
+            elif name == "AttentionValues":
+                o = ops.skip_blend(o, v, m, N)
         out = proj(attn.to_out[0], o)
         return out.view(B, N, -1)

@@ -1,18 +1,44 @@
-"""RectifiedFlowScheduler, training side (ltx_video/schedulers/rf.py:179-426).
+"""RectifiedFlowScheduler (ltx_video/schedulers/rf.py:179-426): training side and the
+inference step.
 
 add_noise / build_velocity_target keep the reference signatures; on ROCm tensors both run in the
 fused kernel ltx_rf_noise_velocity (f32 arithmetic, bf16 result -- the reference computes the
 same f32 values and train_step casts them to the model dtype at training.py:143,146).
 shift_timesteps implements the SD3 and SimpleDiffusion resolution shifts (rf.py:49-149);
 anything else is the reference's silent no-op. The timestep shift math acts on [B] scalars and
-stays in torch (host-side plumbing).
+stays in torch (host-side plumbing), as does the 20-entry schedule of set_timesteps.
+step() is the Euler update over the latent tokens: the fused kernel ltx_rf_euler_step
+(next-lower-timestep search + update, global or per-token timesteps).
 """
+import json
 import math
-from typing import Optional
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Optional, Union
 
 import torch
 
 from . import ops
+
+
+def linear_quadratic_schedule(num_steps, threshold_noise=0.025, linear_steps=None):
+    """rf.py:25-46."""
+    if num_steps == 1:
+        return torch.tensor([1.0])
+    if linear_steps is None:
+        linear_steps = num_steps // 2
+    linear_sigma_schedule = [i * threshold_noise / linear_steps for i in range(linear_steps)]
+    threshold_noise_step_diff = linear_steps - threshold_noise * num_steps
+    quadratic_steps = num_steps - linear_steps
+    quadratic_coef = threshold_noise_step_diff / (linear_steps * quadratic_steps ** 2)
+    linear_coef = threshold_noise / linear_steps - 2 * threshold_noise_step_diff / (
+        quadratic_steps ** 2)
+    const = quadratic_coef * (linear_steps ** 2)
+    quadratic_sigma_schedule = [quadratic_coef * (i ** 2) + linear_coef * i + const
+                                for i in range(linear_steps, num_steps)]
+    sigma_schedule = linear_sigma_schedule + quadratic_sigma_schedule + [1.0]
+    sigma_schedule = [1.0 - x for x in sigma_schedule]
+    return torch.tensor(sigma_schedule[:-1])
 
 
 def simple_diffusion_resolution_dependent_timestep_shift(samples_shape, timesteps, n=32 * 32):
@@ -61,6 +87,16 @@ def sd3_resolution_dependent_timestep_shift(samples_shape, timesteps, target_shi
     return out
 
 
+@dataclass
+class RectifiedFlowSchedulerOutput:
+    """rf.py:157-170."""
+    prev_sample: torch.Tensor
+    pred_original_sample: Optional[torch.Tensor] = None
+
+    def __getitem__(self, i):
+        return (self.prev_sample,)[i]
+
+
 class RectifiedFlowScheduler:
     order = 1
 
@@ -74,6 +110,104 @@ class RectifiedFlowScheduler:
         self.sampler = sampler
         self.shift = shift
         self.init_noise_sigma = 1.0
+        self.num_inference_steps = None
+        self.config = {"num_train_timesteps": num_train_timesteps, "shifting": shifting,
+                       "base_resolution": base_resolution,
+                       "target_shift_terminal": target_shift_terminal, "sampler": sampler,
+                       "shift": shift}
+        self.timesteps = self.sigmas = self.get_initial_timesteps(num_train_timesteps, shift=shift)
+
+    @classmethod
+    def from_config(cls, config):
+        keys = ("num_train_timesteps", "shifting", "base_resolution", "target_shift_terminal",
+                "sampler", "shift")
+        return cls(**{k: v for k, v in dict(config).items() if k in keys})
+
+    @staticmethod
+    def from_pretrained(pretrained_model_path: Union[str, Path]):
+        """Single-file safetensors (metadata['config']['scheduler']) or a diffusers directory
+        (scheduler/scheduler_config.json), rf.py:250-274."""
+        path = Path(pretrained_model_path)
+        if path.is_file():
+            from safetensors import safe_open
+            with safe_open(str(path), framework="pt", device="cpu") as f:
+                config = json.loads(f.metadata()["config"])["scheduler"]
+        else:
+            with open(path / "scheduler" / "scheduler_config.json") as f:
+                config = json.load(f)
+        return RectifiedFlowScheduler.from_config(config)
+
+    def get_initial_timesteps(self, num_timesteps: int, shift: Optional[float] = None):
+        """rf.py:198-214."""
+        if self.sampler == "Uniform":
+            return torch.linspace(1, 1 / num_timesteps, num_timesteps)
+        if self.sampler == "LinearQuadratic":
+            return linear_quadratic_schedule(num_timesteps)
+        if self.sampler == "Constant":
+            assert shift is not None, "Shift must be provided for constant time shift sampler."
+            return time_shift(shift, 1, torch.linspace(1, 1 / num_timesteps, num_timesteps))
+        return None
+
+    def set_timesteps(self, num_inference_steps=None, samples_shape=None, timesteps=None,
+                      device=None):
+        """rf.py:227-248."""
+        if timesteps is not None and num_inference_steps is not None:
+            raise ValueError("You cannot provide both `timesteps` and `num_inference_steps`.")
+        if timesteps is None:
+            num_inference_steps = min(self.num_train_timesteps, num_inference_steps)
+            timesteps = self.get_initial_timesteps(num_inference_steps, shift=self.shift).to(device)
+            timesteps = self.shift_timesteps(samples_shape, timesteps)
+        else:
+            timesteps = torch.Tensor(timesteps).to(device)
+            num_inference_steps = len(timesteps)
+        self.timesteps = timesteps
+        self.num_inference_steps = num_inference_steps
+        self.sigmas = self.timesteps
+
+    def scale_model_input(self, sample, timestep=None):
+        return sample
+
+    def step(self, model_output, timestep, sample, return_dict=True, stochastic_sampling=False,
+             generator=None, **kwargs):
+        """rf.py:305-374 on the device: Euler from `timestep` (0-dim global or [B,N] per token)
+        to the next lower scheduled timestep, in ltx_rf_euler_step. stochastic_sampling
+        re-noises the x0 estimate to the next timestep (rf.py:359-365)."""
+        if self.num_inference_steps is None:
+            raise ValueError("Number of inference steps is 'None', you need to run "
+                             "'set_timesteps' after creating the scheduler")
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor(float(timestep))
+        if stochastic_sampling:
+            return self._stochastic_step(model_output, timestep, sample, return_dict, generator)
+        prev = ops.rf_euler_step(model_output, timestep, sample, self.timesteps)
+        if not return_dict:
+            return (prev,)
+        return RectifiedFlowSchedulerOutput(prev_sample=prev)
+
+    def _stochastic_step(self, model_output, timestep, sample, return_dict, generator):
+        """x0 = sample - t * v; prev = add_noise(x0, randn, t - dt) (rf.py:359-365). The
+        Euler kernel gives sample - dt * v with the same dt; x0 and the re-noising are
+        rf_noise_velocity's f32 arithmetic."""
+        dev = sample.device
+        t = timestep.to(device=dev, dtype=torch.float32)
+        zero = torch.zeros((), device=dev)
+        # dt from the kernel on a unit prediction: sample' = 0 - dt * 1
+        unit = torch.ones(sample.shape[:-1] + (1,), dtype=torch.float32, device=dev)
+        dt = -ops.rf_euler_step(unit, t, torch.zeros_like(unit), self.timesteps)
+        tt = t.reshape(t.shape + (1,)) if t.ndim else t
+        x0 = sample - tt * model_output
+        next_t = tt - dt if t.ndim else (t - dt.reshape(-1)[0] + zero)
+        noise = torch.randn(sample.shape, generator=generator, device=dev, dtype=sample.dtype)
+        prev = self.add_noise_f32(x0, noise, next_t)
+        if not return_dict:
+            return (prev,)
+        return RectifiedFlowSchedulerOutput(prev_sample=prev)
+
+    @staticmethod
+    def add_noise_f32(x0, noise, t):
+        """rf.py:376-386 in f32 (append_dims broadcasting)."""
+        s = t.reshape(t.shape + (1,) * (x0.ndim - t.ndim)) if t.ndim else t
+        return (1 - s) * x0 + s * noise
 
     def shift_timesteps(self, samples_shape, timesteps):
         if self.shifting == "SD3":

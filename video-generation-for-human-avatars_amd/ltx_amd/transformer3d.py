@@ -18,6 +18,7 @@ import json
 import math
 import os
 from dataclasses import dataclass
+from enum import Enum, auto
 from pathlib import Path
 from typing import Any, Dict, List, Optional
 
@@ -62,6 +63,14 @@ OURS_TRANSFORMER_CONFIG = {
 # diffusers checkpoint key renames (diffusers_config_mapping.py:140-145)
 TRANSFORMER_KEYS_RENAME_DICT = {"proj_in": "patchify_proj", "time_embed": "adaln_single",
                                 "norm_q": "q_norm", "norm_k": "k_norm"}
+
+
+class SkipLayerStrategy(Enum):
+    """ltx_video/utils/skip_layer_strategy.py:4-8 (same members, same order)."""
+    AttentionSkip = auto()
+    AttentionValues = auto()
+    Residual = auto()
+    TransformerBlock = auto()
 
 
 @dataclass
@@ -311,8 +320,12 @@ class PixArtAlphaTextProjection(nn.Module):
 class _Shared:
     """Per-forward constants shared by all blocks."""
 
-    def __init__(self, B, N, L, heads, head_dim, rope, enc_bias, eps, text_shared=False):
+    def __init__(self, B, N, L, heads, head_dim, rope, enc_bias, eps, text_shared=False,
+                 per_token=False):
         self.B, self.N, self.L = B, N, L
+        # AdaLN rows: one modulation row per batch (training) or per token (inference with a
+        # [B, N] timestep, transformer3d.py:488-491): kernels index mod rows by m // rpm
+        self.rpm = 1 if per_token else N
         # text_shared: every sample attends to the same prompt (train_step expands one prompt
         # over the batch, training.py:415), so the text side holds one batch (Bt = 1)
         self.text_shared = text_shared
@@ -351,9 +364,14 @@ class _BlockFn(torch.autograd.Function):
     """One BasicTransformerBlock.forward (attention.py:198-321) + its backward."""
 
     @staticmethod
-    def forward(ctx, blk, sh, keep, h, enc2, mods, onep, *lora_ab):
+    def forward(ctx, blk, sh, keep, skip, h, enc2, mods, onep, *lora_ab):
+        """skip = (mask row [B] bf16, SkipLayerStrategy) for STG inference (attention.py:312-319,
+        1071-1085), or None."""
         B, N, L, H, d, D = sh.B, sh.N, sh.L, sh.H, sh.d, sh.D
         M = B * N
+        rpm = sh.rpm
+        if skip is not None and keep:
+            raise NotImplementedError("skip-layer masks are an inference (forward-only) feature")
         W = blk.packed()
         a1, a2, ff = blk.attn1, blk.attn2, blk.ff
         ldm = mods.stride(0)
@@ -362,16 +380,23 @@ class _BlockFn(torch.autograd.Function):
         r = lora[0].r if has_lora else 0
         s = lora[0].scaling if has_lora else 1.0
         # ---- 1. norm1 + AdaLN(msa) -> fused QKV -> q/k RMSNorm + RoPE -> SDPA -> gated residual
-        x1, rstd1 = ops.rmsnorm_modulate_fwd(h, mods[:, 0], onep[:, 1], ldm, N, blk.norm_eps)
+        x1, rstd1 = ops.rmsnorm_modulate_fwd(h, mods[:, 0], onep[:, 1], ldm, rpm, blk.norm_eps)
         qkv = ops.gemm(x1, W["qkv_w"], bias=W["qkv_b"])
-        del x1
+        strat = skip[1] if skip is not None else None
+        if strat is not SkipLayerStrategy.AttentionSkip:
+            del x1
         qk = torch.empty(M, 2 * D, dtype=torch.bfloat16, device=h.device)
         _, _, rq1, rk1 = ops.qk_norm_rope_fwd(qkv[:, :D], qkv[:, D:2 * D], a1.q_norm.weight,
                                               a1.k_norm.weight, sh.rope, q_out=qk[:, :D],
                                               k_out=qk[:, D:])
         o1, lse1 = ops.attn_fwd(qk[:, :D], qk[:, D:], qkv[:, 2 * D:], B, H, d, a1.scale)
+        if strat is SkipLayerStrategy.AttentionSkip:  # blend with the processor input
+            o1 = ops.skip_blend(o1, x1, skip[0], N)
+            del x1
+        elif strat is SkipLayerStrategy.AttentionValues:  # blend with to_v's output
+            o1 = ops.skip_blend(o1, qkv[:, 2 * D:], skip[0], N)
         h1 = ops.gemm(o1, a1.to_out[0].weight, bias=a1.to_out[0].bias, epilogue="gated_residual",
-                      aux0=h, aux1=mods[:, 2], rows_per_batch=N)
+                      aux0=h, aux1=mods[:, 2], rows_per_batch=rpm)
         # ---- 2. attn2 on the un-normalised h1 (attention.py:273-285), LoRA fused into the GEMMs
         wq, bq, _ = _lin(a2.to_q)
         wk, bk, _ = _lin(a2.to_k)
@@ -405,14 +430,16 @@ class _BlockFn(torch.autograd.Function):
             u_o = None
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1)
         # ---- 3. norm2 + AdaLN(mlp) -> FF (tanh-GELU fused) -> gated residual
-        x2, rstd2 = ops.rmsnorm_modulate_fwd(h2, mods[:, 3], onep[:, 4], ldm, N, blk.norm_eps)
+        x2, rstd2 = ops.rmsnorm_modulate_fwd(h2, mods[:, 3], onep[:, 4], ldm, rpm, blk.norm_eps)
         fpre = torch.empty(M, ff.net[0].proj.out_features, dtype=torch.bfloat16, device=h.device)
         act = ops.gemm(x2, ff.net[0].proj.weight, bias=ff.net[0].proj.bias, epilogue="gelu",
                        aux0=fpre)
         del x2
         h3 = ops.gemm(act, ff.net[2].weight, bias=ff.net[2].bias, epilogue="gated_residual",
-                      aux0=h2, aux1=mods[:, 5], rows_per_batch=N)
+                      aux0=h2, aux1=mods[:, 5], rows_per_batch=rpm)
         del act
+        if strat is SkipLayerStrategy.TransformerBlock:
+            h3 = ops.skip_blend(h3, h, skip[0], N)
         if keep:
             lora_saved = (u_q, u_k, u_v, u_o) if has_lora else ()
             ctx.save_for_backward(h, enc2, mods, onep, rstd1, qkv, qk, rq1, rk1, o1, lse1, h1,
@@ -440,12 +467,13 @@ class _BlockFn(torch.autograd.Function):
             lora = _lora_params(blk)
             r, s = lora[0].r, lora[0].scaling
         # ---- FF: h3 = h2 + g_mlp * ff(x2)
-        d_ffo = ops.gate_mul(dh3, mods[:, 5], N)
+        rpm = sh.rpm
+        d_ffo = ops.gate_mul(dh3, mods[:, 5], rpm)
         d_f = ops.gemm(d_ffo, W["ff2_wT"], epilogue="gelu_bwd", aux0=fpre)
         del d_ffo
         dx2 = ops.gemm(d_f, W["ff1_wT"])
         del d_f
-        dh2 = ops.rmsnorm_modulate_bwd(dx2, h2, rstd2, onep[:, 4], ldm, N, dres=dh3)
+        dh2 = ops.rmsnorm_modulate_bwd(dx2, h2, rstd2, onep[:, 4], ldm, rpm, dres=dh3)
         del dx2
         # ---- attn2: h2 = h1 + to_out(o2)   (LoRA grads: peft f32 adapters)
         if has_lora:
@@ -490,7 +518,7 @@ class _BlockFn(torch.autograd.Function):
             ops.gemm(dv2, W["v2_wT"], epilogue="accum", aux0=denc, out=denc)
         del dq2raw, dk2raw, dv2, dh2
         # ---- attn1: h1 = h + g_msa * to_out(sdpa(rope(qn(q)), rope(kn(k)), v))
-        d_y1 = ops.gate_mul(dh1, mods[:, 2], N)
+        d_y1 = ops.gate_mul(dh1, mods[:, 2], rpm)
         do1 = ops.gemm(d_y1, W["out1_wT"])
         del d_y1
         M = B * N
@@ -503,10 +531,10 @@ class _BlockFn(torch.autograd.Function):
                              dk_out=dqkv[:, D:2 * D])
         del dq1, dk1
         dh = None
-        if ctx.needs_input_grad[3]:  # (blk, sh, keep, h, ...)
+        if ctx.needs_input_grad[4]:  # (blk, sh, keep, skip, h, ...)
             dx1 = ops.gemm(dqkv, W["qkv_wT"])
-            dh = ops.rmsnorm_modulate_bwd(dx1, h, rstd1, onep[:, 1], ldm, N, dres=dh1)
-        return (None, None, None, dh, denc, None, None, *grads_lora)
+            dh = ops.rmsnorm_modulate_bwd(dx1, h, rstd1, onep[:, 1], ldm, rpm, dres=dh1)
+        return (None, None, None, None, dh, denc, None, None, *grads_lora)
 
 
 class _CaptionProjFn(torch.autograd.Function):
@@ -732,12 +760,13 @@ class Transformer3DModel(nn.Module):
                 class_labels=None, cross_attention_kwargs=None, attention_mask=None,
                 encoder_attention_mask=None, skip_layer_mask=None, skip_layer_strategy=None,
                 return_dict=True):
-        """transformer3d.py:361-565 (training call). Does not mutate `hidden_states`."""
+        """transformer3d.py:361-565: the training call and the inference call (timestep [B],
+        [B,1] or per token [B,N]; float pixel-coordinate indices_grid; skip_layer_mask
+        [num_layers, B] with a SkipLayerStrategy -- forward only). Does not mutate
+        `hidden_states` (the reference lerps into it in place, transformer3d.py:447-466)."""
         _lib.ensure_device(hidden_states.device)
-        if skip_layer_mask is not None or skip_layer_strategy is not None:
-            raise NotImplementedError("skip-layer (STG) guidance is an inference feature (next row)")
         if attention_mask is not None:
-            raise NotImplementedError("self-attention masks are not used on the LTX training path")
+            raise NotImplementedError("self-attention masks are not used on the LTX paths")
         dt = torch.bfloat16
         if ref_image_hidden_states is None or pose_hidden_states is None:
             raise ValueError("the avatar model conditions on ref_image_hidden_states and pose_hidden_states")
@@ -745,13 +774,14 @@ class Transformer3DModel(nn.Module):
         x_in = ops.condition_lerp(hidden_states.to(dt), ref_image_hidden_states.to(dt),
                                   pose_hidden_states.to(dt))
         out = self._forward_tokens(x_in, indices_grid, encoder_hidden_states, timestep,
-                                   encoder_attention_mask)
+                                   encoder_attention_mask, skip_layer_mask, skip_layer_strategy)
         if not return_dict:
             return (out,)
         return Transformer3DModelOutput(sample=out)
 
     def _forward_tokens(self, x_in, indices_grid, encoder_hidden_states, timestep,
-                        encoder_attention_mask=None):
+                        encoder_attention_mask=None, skip_layer_mask=None,
+                        skip_layer_strategy=None):
         """Everything after the conditioning lerp: patchify_proj, AdaLN-single, RoPE, caption
         projection, the block stack and the output head. x_in [B, N, C] bf16 -> [B, N, C_out]."""
         B, N, C = x_in.shape
@@ -776,10 +806,14 @@ class Transformer3DModel(nn.Module):
                 enc_bias = ((1 - m.to(dt)) * -10000.0).float().contiguous()
             else:
                 enc_bias = m.reshape(Bt, -1).float().contiguous()
+        # per-token timesteps (inference with conditioning latents, pipeline_ltx_video.py:1190-1195)
+        per_token = timestep.numel() != B
+        if per_token and timestep.numel() != B * N:
+            raise ValueError(f"timestep has {timestep.numel()} values for batch {B} x {N} tokens")
         with torch.no_grad():
             h = ops.gemm(x_in.reshape(B * N, C), self.patchify_proj.weight,
                          bias=self.patchify_proj.bias)
-            tmod, emb = self._adaln(timestep, B)
+            tmod, emb = self._adaln(timestep)
         rope = ops.RopeSpec(indices_grid, D, self.positional_embedding_theta,
                             self.positional_embedding_max_pos)
         enc = encoder_hidden_states.to(dt)
@@ -789,9 +823,17 @@ class Transformer3DModel(nn.Module):
         enc2 = _CaptionProjFn.apply(enc2d, cp.linear_1.weight, cp.linear_1.bias,
                                     cp.linear_2.weight, cp.linear_2.bias)
         eps = self.transformer_blocks[0].norm_eps if len(self.transformer_blocks) else 1e-6
-        sh = _Shared(B, N, L, H, self.attention_head_dim, rope, enc_bias, eps, text_shared)
+        sh = _Shared(B, N, L, H, self.attention_head_dim, rope, enc_bias, eps, text_shared,
+                     per_token)
         keep = torch.is_grad_enabled()
-        for blk in self.transformer_blocks:
+        strat = None
+        if skip_layer_mask is not None and skip_layer_strategy is not None:
+            strat = SkipLayerStrategy[skip_layer_strategy.name] if isinstance(
+                skip_layer_strategy, Enum) else SkipLayerStrategy[str(skip_layer_strategy)]
+            if strat is SkipLayerStrategy.Residual:  # acts only with residual_connection (False)
+                strat = None
+        for i, blk in enumerate(self.transformer_blocks):
+            skip = None if strat is None else (skip_layer_mask[i].to(dt).contiguous(), strat)
             with torch.no_grad():
                 mods, onep = ops.ada_modulation(blk.scale_shift_table, tmod, (1 << 1) | (1 << 4))
             lora = _lora_params(blk)
@@ -801,22 +843,21 @@ class Transformer3DModel(nn.Module):
                     ab += [m.lora_A["default"].weight, m.lora_B["default"].weight]
             if self.training and self.gradient_checkpointing and keep:
                 h = torch.utils.checkpoint.checkpoint(
-                    lambda *a, _b=blk: _BlockFn.apply(_b, sh, True, *a),
+                    lambda *a, _b=blk, _s=skip: _BlockFn.apply(_b, sh, True, _s, *a),
                     h, enc2, mods, onep, *ab, use_reentrant=False)
             else:
-                h = _BlockFn.apply(blk, sh, keep, h, enc2, mods, onep, *ab)
+                h = _BlockFn.apply(blk, sh, keep, skip, h, enc2, mods, onep, *ab)
         with torch.no_grad():
             hmod, honep = ops.ada_modulation(self.scale_shift_table, emb, 1 << 1, broadcast=True)
-        out = _HeadFn.apply(h, hmod, honep, self.proj_out.weight, self.proj_out.bias, N, 1e-6)
+        out = _HeadFn.apply(h, hmod, honep, self.proj_out.weight, self.proj_out.bias, sh.rpm, 1e-6)
         return out.view(B, N, self.out_channels)
 
-    def _adaln(self, timestep, B):
-        """AdaLayerNormSingle (transformer3d.py:473-491): returns (tmod [B,6D], emb [B,D])."""
-        if timestep.numel() != B:
-            raise NotImplementedError("per-token timesteps are an inference feature (next row)")
+    def _adaln(self, timestep):
+        """AdaLayerNormSingle (transformer3d.py:473-491) of timestep.flatten(): returns
+        (tmod [T,6D], emb [T,D]), T = B (one timestep per sample) or B*N (per token)."""
         mult = float(self.timestep_scale_multiplier or 1.0)
         ad = self.adaln_single
-        te = ops.timestep_embedding(timestep.reshape(B).float().contiguous(), mult)
+        te = ops.timestep_embedding(timestep.reshape(-1).float().contiguous(), mult)
         e1 = ops.gemm(te, ad.emb.timestep_embedder.linear_1.weight,
                       bias=ad.emb.timestep_embedder.linear_1.bias)
         emb = ops.gemm(ops.silu(e1), ad.emb.timestep_embedder.linear_2.weight,
