@@ -146,13 +146,79 @@ def load_traffic():
         return None
 
 
+def infer_main(args):
+    """--infer: one LTXVideoPipeline denoising step per "step": CFG 3.0 +
+    STG 1.0 (AttentionValues on block 19) + rescaling 0.7, first latent frame hard-conditioned
+    (per-token timesteps), `--infer-batch` videos of 49f 512x512 -> transformer batch 3 x B of
+    N = 1792 tokens, guidance + Euler update included. Prints its own JSON line (not the
+    training metric)."""
+    torch.cuda.set_device(0)
+    device = torch.device("cuda", 0)
+    from ltx_amd import _lib
+    from ltx_amd.denoise import denoise_step
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    from ltx_amd.transformer3d import SkipLayerStrategy
+    _lib.ensure_device(device)
+    model = build_model(device)
+    model.eval()
+    for p in model.parameters():
+        p.requires_grad_(False)
+    B = args.infer_batch
+    N = F_LAT * H_LAT * W_LAT
+    g = torch.Generator().manual_seed(20251015)
+    lat = torch.randn(B, N, 128, generator=g).to(device)
+    ref = torch.randn(B, 128, 1, H_LAT, W_LAT, generator=g).to(device, torch.bfloat16)
+    pose = torch.randn(B, 128, F_LAT, H_LAT, W_LAT, generator=g).to(device, torch.bfloat16)
+    neg = torch.randn(B, L_TXT, 4096, generator=g)
+    pos = torch.randn(B, L_TXT, 4096, generator=g)
+    enc = torch.cat([neg, pos, pos]).to(device, torch.bfloat16)
+    m = (torch.arange(L_TXT) < 16).long().view(1, L_TXT)
+    mask = torch.cat([torch.ones(B, L_TXT, dtype=torch.long), m.expand(2 * B, -1)]).to(device)
+    cond = torch.zeros(B, N, device=device)
+    cond[:, : H_LAT * W_LAT] = 1.0
+    sch = RectifiedFlowScheduler(sampler="LinearQuadratic")
+    sch.set_timesteps(num_inference_steps=max(args.steps + args.warmup, 2), device=device)
+    kw = dict(prompt_embeds_batch=enc, prompt_attention_mask_batch=mask,
+              ref_image_hidden_states=ref, pose_hidden_states=pose, frame_rate=25.0,
+              batch_size=B, guidance_scale=3.0, stg_scale=1.0, rescaling_scale=0.7,
+              skip_block_list=[19], skip_layer_strategy=SkipLayerStrategy.AttentionValues,
+              conditioning_mask=cond)
+    with torch.no_grad():
+        for i in range(args.warmup):
+            lat = denoise_step(model, sch, lat, sch.timesteps[i], **kw)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.warmup, args.warmup + args.steps):
+            lat = denoise_step(model, sch, lat, sch.timesteps[i], **kw)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    fwd, _ = step_flops_per_sample(N)
+    tflops = fwd * 3 * B * args.steps / (elapsed * 1e12)
+    print(json.dumps({
+        "metric": "LTX-2B inference denoising steps/sec (CFG+STG: transformer batch 3 x videos)",
+        "value": round(args.steps / elapsed, 4), "unit": "steps/s",
+        "tokens_per_s": round(3 * B * N * args.steps / elapsed, 1),
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "higher_is_better": True, "dtype": "bf16",
+        "data": "synthetic latents/pose/ref/prompts; random-init LTX-2B weights",
+        "config": {"workload": "denoise_step: CFG 3.0 + STG 1.0 (AttentionValues, block 19) + "
+                               "rescale 0.7, per-token timesteps (first frame conditioned), "
+                               "49f 512x512 -> N=1792", "videos": B, "transformer_batch": 3 * B},
+        "fwd_tflops": round(tflops, 1), "mfma_frac": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+    }), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--infer", action="store_true", help="inference denoising-step benchmark")
+    ap.add_argument("--infer-batch", type=int, default=1)
     args = ap.parse_args()
+    if args.infer:
+        return infer_main(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
