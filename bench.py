@@ -216,7 +216,17 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--infer", action="store_true", help="inference denoising-step benchmark")
     ap.add_argument("--infer-batch", type=int, default=1)
+    ap.add_argument("--config", choices=["a", "x"], default="a",
+                    help="a: 49f 512x512 (N=1792, the metric); x: 97f 768x768 (N=7488, "
+                         "BASELINE configs[3], long-sequence stress)")
+    ap.add_argument("--batch", type=int, default=None, help="micro-batch per GPU (default 8)")
+    ap.add_argument("--grad-ckpt", action="store_true", help="per-block gradient checkpointing")
     args = ap.parse_args()
+    global F_LAT, H_LAT, W_LAT, B_PER_GPU
+    if args.config == "x":
+        F_LAT, H_LAT, W_LAT = 13, 24, 24
+    if args.batch:
+        B_PER_GPU = args.batch
     if args.infer:
         return infer_main(args)
 
@@ -238,6 +248,7 @@ def main():
     _lib.ensure_device(device)
 
     model = build_model(device)
+    model.gradient_checkpointing = bool(args.grad_ckpt)
     batch, prompt, mask = synthetic_batch(device, rank)
     cfg = TrainConfig(checkpoint_path="-", batch_size=B_PER_GPU, learning_rate=1e-4,
                       lora_rank=LORA_RANK, lora_alpha=LORA_RANK, gradient_accumulation_steps=ACCUM,
@@ -289,7 +300,7 @@ def main():
     dom_flops = 2.0 * dom_key[0] * dom_key[1] * dom_key[2]
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     line = {
-        "metric": "LTX-2B LoRA train-step samples/sec (latent-tokens/sec = samples/sec x 1792)",
+        "metric": f"LTX-2B LoRA train-step samples/sec (latent-tokens/sec = samples/sec x {N})",
         "value": round(value, 4),
         "unit": "samples/s",
         "tokens_per_s": round(value * N, 1),
@@ -303,18 +314,21 @@ def main():
         "dtype": "bf16",
         "data": "synthetic latents/pose/ref/prompt of the configured shapes; random-init LTX-2B weights",
         "config": {"workload": "LTX-Video 2B LoRA(r=16, attn2 q/k/v/out) + caption_projection "
-                               "train step, 49f 512x512 -> latent 7x16x16 (N=1792), 1xMI355X per rank",
+                               + ("train step, 49f 512x512 -> latent 7x16x16 (N=1792), 1xMI355X per rank"
+                                  if args.config == "a" else
+                                  "train step, 97f 768x768 -> latent 13x24x24 (N=7488), 1xMI355X per rank")
+                               + (", per-block gradient checkpointing" if args.grad_ckpt else ""),
                    "model": "LTX-Video-2B (28 layers, D 2048, 32x64 heads)", "global_batch": B_PER_GPU * world,
                    "micro_batch_per_gpu": B_PER_GPU, "seq_len": N, "text_len": L_TXT,
                    "grad_accum": ACCUM, "parallelism": f"dp{world}"},
         "step_tflops_per_gpu": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-        "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel_t<GELU, 256> FF-up [14336x2048].[8192x2048]^T",
+        "roofline": {"bound": "mfma", "kernel": f"gemm_nt_kernel_t<GELU> FF-up [{M}x2048].[8192x2048]^T",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": load_traffic(),
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": load_traffic() if args.config == "a" else None,
                      "launch_ms": round(dom_ms, 4), "launches": len(timer.pairs)},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "a":
         try:
             line["cpu_baseline"] = cpu_baseline()
         except Exception as exc:  # the baseline must never hide the GPU measurement
