@@ -28,6 +28,8 @@ Fixtures (safetensors + a JSON sidecar each):
   infer_step        inference call of the tiny model (CFG+STG batch of 3, float pixel coords,
                     per-token timesteps, every SkipLayerStrategy) and RectifiedFlowScheduler
                     set_timesteps / step, global and per-token (rf.py:179-374).
+  ckpt_export       save_training_checkpoint of the tiny model: lora_audio (peft merge) and full
+                    (state dict) safetensors, tensors + metadata (torch_utils.py:39-133).
 """
 import dataclasses
 import json
@@ -361,6 +363,33 @@ def gen_infer():
     _save("infer_step", out, meta)
 
 
+def gen_ckpt():
+    """Checkpoint formats: the reference's save_training_checkpoint
+    (torch_utils.py:105-133) of the tiny model in both train modes -- lora_audio exports the peft
+    merge (export_merged_safetensors, :66-102), full saves the state dict
+    (save_module_safetensors, :39-63) -- read back: tensors + safetensors metadata."""
+    import copy
+    import tempfile
+    from safetensors import safe_open
+    from ltx_video.utils.torch_utils import save_training_checkpoint
+    seed, rank = 1234, 16
+    model, _ = _build(TINY_CONFIG, seed, torch.bfloat16, rank)
+    out, meta = {}, {"config": TINY_CONFIG, "param_seed": seed, "lora_rank": rank}
+    with tempfile.TemporaryDirectory() as tmp:
+        for mode, m in (("lora_audio", model), ("full", copy.deepcopy(model).merge_and_unload())):
+            path = os.path.join(tmp, f"model_epoch_3.safetensors")
+            save_training_checkpoint(m, path, mode, metadata={"epoch": "3", "source": "gen"},
+                                     is_best=(mode == "full"))
+            if mode == "full":
+                path = os.path.join(tmp, "best_model_epoch_3.safetensors")
+            with safe_open(path, framework="pt", device="cpu") as f:
+                meta[f"{mode}.metadata"] = f.metadata()
+                for k in f.keys():
+                    out[f"{mode}.{k}"] = f.get_tensor(k)
+    meta["source"] = "reference ltx_video/utils/torch_utils.py:39-133 via oracle/shim"
+    _save("ckpt_export", out, meta)
+
+
 def gen_config():
     cfg = load_train_config_from_yaml(os.path.join(REF, "configs", "train-avatars.yaml"))
     d = dataclasses.asdict(cfg)
@@ -379,3 +408,4 @@ if __name__ == "__main__":
     gen_tiny()
     gen_block2b()
     gen_infer()
+    gen_ckpt()

@@ -83,6 +83,27 @@ class PeftModel(nn.Module):
         except AttributeError:
             return getattr(self.base_model.model, name)
 
+    @torch.no_grad()
+    def merge_and_unload(self):
+        """peft 0.17.1 LoraModel.merge_and_unload (safe_merge=False): per LoRA Linear,
+        delta = (B @ A) * scaling in the adapter dtype (get_delta_weight), then
+        base_layer.weight.data += delta (in-place, promoted add rounded to the base dtype);
+        the wrapper is replaced by its base layer."""
+        model = self.base_model.model
+        for name, mod in list(model.named_modules()):
+            if isinstance(mod, LoraLinear):
+                wa = mod.lora_A["default"].weight
+                wb = mod.lora_B["default"].weight
+                delta = (wb @ wa) * mod.scaling
+                mod.base_layer.weight.data += delta
+                parent_name, _, child = name.rpartition(".")
+                parent = model.get_submodule(parent_name)
+                if child.isdigit():
+                    parent[int(child)] = mod.base_layer
+                else:
+                    setattr(parent, child, mod.base_layer)
+        return model
+
 
 def get_peft_model(model, peft_config, **kwargs):
     for name in peft_config.target_modules:

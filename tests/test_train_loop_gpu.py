@@ -1,0 +1,103 @@
+"""Training around the step (SURVEY 8c-5 loss curve, 8f row 3 formats), on the MI355X:
+  * loss curve: 10 optimizer steps of the tiny model -- train_step + FusedAdamW through the HIP
+    library vs the pinned oracle's train_step + torch.optim.AdamW on the same device, same
+    per-step t / noise streams; per-step loss within bf16 drift;
+  * train_loop over precomputed .pt latents on disk (LatentPairDataset + LatentLoader) writes the
+    reference's per-epoch checkpoints (best_model_epoch_N.safetensors, metadata) that load back
+    through Transformer3DModel.from_pretrained.
+"""
+import os
+
+import pytest
+import torch
+from safetensors.torch import load_file
+
+import ltx_oracle as O
+from model_utils import build_model
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DEV = "cuda"
+
+
+def _tiny():
+    import json
+    with open(os.path.join(GOLD, "tiny_train_step.json")) as f:
+        meta = json.load(f)
+    d = load_file(os.path.join(GOLD, "tiny_train_step.safetensors"))
+    return d, {k[2:]: v for k, v in d.items() if k.startswith("w.")}, meta
+
+
+def test_loss_curve_matches_oracle():
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    from ltx_amd.training import FusedAdamW, train_step
+    d, params, meta = _tiny()
+    cfg = meta["config"]
+    model = build_model(cfg, params, meta["lora_rank"], device=DEV)
+    model.train()
+    trainable = [p for p in model.parameters() if p.requires_grad]
+    opt = FusedAdamW(trainable, lr=1e-3)
+    q = {k: v.to(DEV).requires_grad_(("lora_" in k) or ("caption_projection" in k))
+         for k, v in params.items()}
+    ref_opt = torch.optim.AdamW([v for v in q.values() if v.requires_grad], lr=1e-3,
+                                foreach=False)
+    tc = TrainConfig(checkpoint_path="-", gradient_accumulation_steps=1)
+    batch = {k[3:]: d[k].to(DEV) for k in ("in.latents", "in.ref_image_latents", "in.pose_latents")}
+    prompt, mask = d["in.prompt_embeds"].to(DEV), d["in.prompt_attention_mask"].to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(123)
+    B, C = batch["latents"].shape[:2]
+    N = batch["latents"][0, 0].numel()
+    ours, refs = [], []
+    for step in range(10):
+        t = torch.rand(B, generator=g, device=DEV) * 0.9 + 0.05
+        noise = torch.randn(B, N, C, generator=g, device=DEV).bfloat16()
+        loss, _, _, _ = train_step(model, batch, RectifiedFlowScheduler(), model.patchifier, tc,
+                                   prompt, mask, t=t, noise=noise)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        r = O.train_step(q, cfg, batch["latents"], batch["ref_image_latents"],
+                         batch["pose_latents"], prompt, mask, t=t, noise=noise)
+        r["loss"].backward()
+        ref_opt.step()
+        ref_opt.zero_grad(set_to_none=True)
+        ours.append(float(loss))
+        refs.append(float(r["loss"]))
+    for i, (a, b) in enumerate(zip(ours, refs)):
+        assert abs(a - b) <= 2e-2 * abs(b), (i, ours, refs)
+    assert ours[-1] < ours[0] * 1.5  # training moves; no blow-up
+
+
+def test_train_loop_writes_reference_checkpoints(tmp_path):
+    from ltx_amd import io
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.training import train_loop
+    from ltx_amd.transformer3d import Transformer3DModel
+    d, params, meta = _tiny()
+    cfg = meta["config"]
+    enc, cond = tmp_path / "enc", tmp_path / "cond"
+    enc.mkdir()
+    cond.mkdir()
+    g = torch.Generator().manual_seed(0)
+    for i in range(4):
+        io.save_latents_pt(torch.randn(1, 128, 2, 8, 8, generator=g), enc / f"clip{i}.pt")
+        io.save_latents_pt(torch.randn(1, 128, 2, 8, 8, generator=g), cond / f"clip{i}.pt")
+        io.save_latents_pt(torch.randn(1, 128, 1, 8, 8, generator=g), cond / f"clip{i}_ref.pt")
+    ds = io.LatentPairDataset(str(cond), str(enc))
+    loader = io.LatentLoader(ds, 2, DEV, shuffle=True, seed=1)
+    model = build_model(cfg, params, meta["lora_rank"], device=DEV)
+    a0 = model.transformer_blocks[0].attn2.to_q.lora_A["default"].weight.detach().clone()
+    tc = TrainConfig(checkpoint_path="-", learning_rate=1e-3, num_epochs=2,
+                     gradient_accumulation_steps=2, output_dir=str(tmp_path / "out"),
+                     save_every_n_epochs=1)
+    tc.train_mode = "lora_audio"  # set by the CLI in the reference (training.py:497-505)
+    logs = []
+    train_loop(model, tc, loader, d["in.prompt_embeds"].to(DEV),
+               d["in.prompt_attention_mask"].to(DEV), log_fn=lambda p, s: logs.append((s, p)))
+    assert [s for s, p in logs if "train/loss" in p] == [1, 2]
+    assert not torch.equal(model.transformer_blocks[0].attn2.to_q.lora_A["default"].weight, a0)
+    for ep in (1, 2):
+        path = tmp_path / "out" / f"best_model_epoch_{ep}.safetensors"
+        assert path.exists()
+        m2 = Transformer3DModel.from_pretrained(str(path))
+        assert m2.config["num_layers"] == cfg["num_layers"]

@@ -68,3 +68,21 @@ def merged_state_dict(model):
             continue
         out[k] = v
     return out
+
+
+@torch.no_grad()
+def unload_lora(model):
+    """peft merge_and_unload in place: base_layer.weight += (B @ A) * scaling (promoted add
+    rounded to the base dtype), each LoraLinear replaced by its base nn.Linear."""
+    for name, mod in list(model.named_modules()):
+        if isinstance(mod, LoraLinear):
+            a = mod.lora_A["default"].weight
+            b = mod.lora_B["default"].weight
+            mod.base_layer.weight.data += (b @ a) * mod.scaling
+            parent_name, _, child = name.rpartition(".")
+            parent = model.get_submodule(parent_name)
+            if child.isdigit():
+                parent[int(child)] = mod.base_layer
+            else:
+                setattr(parent, child, mod.base_layer)
+    return model

@@ -142,3 +142,87 @@ class GradAllReduce:
                 else:
                     p.grad.copy_(g)
                 off += n
+
+
+def train_one_epoch(model, dataloader, optimizer, scheduler, patchifier, device, config,
+                    prompt_embeds, prompt_attention_mask, epoch, global_step, reducer=None,
+                    log_fn=None):
+    """training.py:169-231: micro-steps with gradient accumulation, the optimizer step every
+    `gradient_accumulation_steps` batches (after the DP gradient all-reduce when `reducer` is
+    given), per-step logging of loss / rel_mse / nrmse / lr through `log_fn` (wandb.log in the
+    reference). Returns (global_step, mean epoch loss). The loss values stay on the device until
+    an optimizer step logs them (one host sync per optimizer step, as the reference's .item())."""
+    model.train()
+    accum = max(1, int(config.gradient_accumulation_steps))
+    optimizer.zero_grad(set_to_none=True)
+    losses = []
+    for batch_idx, batch in enumerate(dataloader):
+        loss, rel_mse, nrmse, loss_dict = train_step(model, batch, scheduler, patchifier, config,
+                                                     prompt_embeds, prompt_attention_mask, device)
+        losses.append(loss.detach().float())
+        if (batch_idx + 1) % accum == 0:
+            if reducer is not None:
+                reducer()
+            optimizer.step()
+            optimizer.zero_grad(set_to_none=True)
+            global_step += 1
+            if log_fn is not None:
+                payload = {"train/loss": float(loss), "train/rel_mse": float(rel_mse),
+                           "train/nrmse": float(nrmse), "train/epoch": epoch,
+                           "train/lr": optimizer.param_groups[0]["lr"]}
+                for k, v in (loss_dict or {}).items():
+                    payload[f"train/{k}"] = float(v)
+                log_fn(payload, global_step)
+    epoch_loss = float(torch.stack(losses).mean()) if losses else 0.0
+    return global_step, epoch_loss
+
+
+def train_loop(model, config, dataloader, prompt_embeds, prompt_attention_mask, device=None,
+               log_fn=None, rank=0):
+    """training.py:234-401 for precomputed prompt embeddings (the T5 encode of main() is out of
+    scope): trainable set per config.train_mode, FusedAdamW(lr), per-epoch checkpoints every
+    `save_every_n_epochs` (best_ prefix on a new best epoch loss) through
+    io.save_training_checkpoint, DP gradient averaging when torch.distributed is initialised."""
+    import os
+
+    from . import io
+    from .scheduler import RectifiedFlowScheduler
+    device = device or model.device
+    patchifier = model.patchifier or SymmetricPatchifier(1)
+    if getattr(config, "gradient_checkpointing", False):
+        model.gradient_checkpointing = True
+    rf = RectifiedFlowScheduler(num_train_timesteps=config.rf_num_train_timesteps,
+                                shifting=config.rf_shifting,
+                                base_resolution=config.rf_base_resolution,
+                                target_shift_terminal=config.rf_target_shift_terminal,
+                                sampler=config.rf_sampler, shift=config.rf_shift)
+    params = [p for p in model.parameters() if p.requires_grad]
+    optimizer = FusedAdamW(params, lr=config.learning_rate)
+    reducer = GradAllReduce(params) if (dist.is_available() and dist.is_initialized()) else None
+    best = float("inf")
+    global_step = 0
+    for epoch in range(config.num_epochs or 0):
+        if hasattr(dataloader, "set_epoch"):
+            dataloader.set_epoch(epoch)
+        global_step, epoch_loss = train_one_epoch(model, dataloader, optimizer, rf, patchifier,
+                                                  device, config, prompt_embeds,
+                                                  prompt_attention_mask, epoch, global_step,
+                                                  reducer, log_fn)
+        if log_fn is not None:
+            log_fn({"train/epoch_loss": epoch_loss}, global_step)
+        if config.output_dir and rank == 0 and (epoch + 1) % config.save_every_n_epochs == 0:
+            os.makedirs(config.output_dir, exist_ok=True)
+            path = os.path.join(config.output_dir, f"model_epoch_{epoch + 1}.safetensors")
+            meta = {"epoch": str(epoch + 1), "global_step": str(global_step),
+                    "source": "single_gpu_epoch",
+                    "scheduler": {"num_train_timesteps": config.rf_num_train_timesteps,
+                                  "shifting": config.rf_shifting,
+                                  "base_resolution": config.rf_base_resolution,
+                                  "target_shift_terminal": config.rf_target_shift_terminal,
+                                  "sampler": config.rf_sampler, "shift": config.rf_shift},
+                    "vae": {"timestep_conditioning": True}}
+            # the reference never updates best_loss (training.py:315, 395): every finite epoch
+            # loss is "best" and the file gets the best_ prefix -- kept for drop-in paths
+            io.save_training_checkpoint(model, path, getattr(config, "train_mode", "full"),
+                                        metadata=meta, is_best=epoch_loss < best)
+    return model
