@@ -37,7 +37,8 @@ enum {
   LTX_EPI_GELU = 1,             /* aux0 <- y (pre-act, optional); C = bf16(gelu_tanh(y))
                                    attention.py:1237-1238 (diffusers GELU tanh), PixArt proj */
   LTX_EPI_GATED_RESIDUAL = 2,   /* C = bf16(R + bf16(gate[b] * y)); R = aux0, gate = aux1 row b =
-                                   m / rows_per_batch (row stride ld1)    attention.py:265-268,305-308 */
+                                   m / rows_per_batch (row stride ld1); aux2 <- y (optional, ld2:
+                                   the gate's gradient, train_mode='full') attention.py:265-268,305-308 */
   LTX_EPI_LORA = 3,             /* C = bf16(y + alpha * U[m,:].Lb[n,:]); U = aux1 f32 [M,rank],
                                    Lb = aux2 f32 [N,rank]      peft lora.Linear, training.py:50-68 */
   LTX_EPI_LORA_RESIDUAL = 4,    /* C = bf16(R + bf16(LORA)); R = aux0        attention.py:285 */
@@ -231,6 +232,42 @@ int ltx_mse_fwd_bwd(const void* out, const void* v, void* dout, float* stats, in
 int ltx_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n,
                    int is_bf16, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int64_t step, void* stream);
+
+/* ---- train_mode='full' parameter gradients (csrc/paramgrad.hip) --------- */
+/* Weight gradient of the q/k RMSNorm weights: partials[(which * splits + s) * D + d] (f32) =
+ * sum over row split s of bf16(dn * bf16(x_raw * rstd)), dn = RoPE^T of the incoming gradient (the
+ * roundings of ltx_qk_norm_rope_bwd); which = 0 (q) / 1 (k, when dk_in != null). Reduce with
+ * ltx_colsum_finish (G = 1 or 2 per call site, S = splits). */
+int ltx_qk_norm_wgrad(const void* dq_in, int64_t ldq_in, int dq_is_f32, const void* dk_in,
+                      int64_t ldk_in, int dk_is_f32, const void* q_raw, int64_t ldq_raw,
+                      const void* k_raw, int64_t ldk_raw, const float* rstd_q, const float* rstd_k,
+                      const uint32_t* rope_cs, int64_t cs_batch_rows, int64_t B, int64_t N, int64_t D,
+                      int rope, int64_t splits, float* partials, void* stream);
+/* Column sums over row groups (M = G * rows_per_group), f32 partials [G, splits, D]:
+ * mode 0: a; 1: bf16(a*b); 2: bf16(a * bf16(b * r[m])) (RMSNorm scale grad);
+ * 3: bf16(a * bf16((b - mean[m]) * r[m])) (LayerNorm scale grad). */
+int ltx_group_colsum(const void* a, int64_t lda, const void* b, int64_t ldb, const float* r,
+                     const float* mean, int mode, int64_t M, int64_t D, int64_t rows_per_group,
+                     int64_t splits, float* partials, void* stream);
+/* bf16 result of the partials: per group out[g*ldo + d] = bf16(sum_s), or with sum_groups
+ * out[d] = bf16(sum_g bf16(sum_s)); accumulate adds into out (bf16 .grad accumulation). */
+int ltx_colsum_finish(const float* partials, int64_t G, int64_t S, int64_t D, int sum_groups,
+                      int accumulate, void* out, int64_t ldo, void* stream);
+/* torch silu_backward in bf16: dx = bf16(dy * s * (1 + x * (1 - s))), s = sigmoid(x); with dres
+ * (nullable) dx = bf16(dres + that) */
+int ltx_silu_bwd_bf16(const void* x, const void* dy, const void* dres, void* dx, int64_t n,
+                      void* stream);
+
+/* ---- ZeRO-2 optimizer buffers (BASELINE config Z; csrc/zero.hip) ------------------------------ */
+int ltx_cast_bf16_f32(const void* src, float* dst, int64_t n, void* stream);
+int ltx_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
+/* out (one f64 on the device) [+]= sum x^2 */
+int ltx_sumsq_f32(const float* x, int64_t n, double* out, int accumulate, void* stream);
+/* coef = inv_world * min(1, max_norm / (sqrt(sumsq) * inv_world + 1e-6)) (max_norm <= 0: 1),
+ * written to *coef; x *= coef (the averaged, global-norm-clipped gradient shard; DeepSpeed
+ * gradient_clipping) -- read from device memory, no host sync. */
+int ltx_clip_scale_f32(float* x, int64_t n, const double* sumsq, float max_norm, float inv_world,
+                       float* coef, void* stream);
 
 /* ---- inference denoising step (csrc/denoise.hip) ------------------------------ */
 /* RoPE indices_grid of an inference call: latent coords * (sf_t, sf_h, sf_w) with the causal

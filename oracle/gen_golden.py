@@ -28,6 +28,8 @@ Fixtures (safetensors + a JSON sidecar each):
   infer_step        inference call of the tiny model (CFG+STG batch of 3, float pixel coords,
                     per-token timesteps, every SkipLayerStrategy) and RectifiedFlowScheduler
                     set_timesteps / step, global and per-token (rf.py:179-374).
+  tiny_full_step    train_mode='full' step of the tiny model (no LoRA; attention, AdaLN, norms,
+                    scale-shift tables, caption projection, proj_out trainable): all grads.
   ckpt_export       save_training_checkpoint of the tiny model: lora_audio (peft merge) and full
                     (state dict) safetensors, tensors + metadata (torch_utils.py:39-133).
 """
@@ -114,7 +116,7 @@ def _capture_train_step(model, pf, batch, prompt, mask, seed, rank):
         return add_noise(original_samples=original_samples, noise=noise, timesteps=timesteps)
 
     sch.add_noise = add_noise_hook
-    core = model.base_model.model
+    core = model.base_model.model if hasattr(model, "base_model") else model
 
     def pre_hook(mod, args, kwargs):
         # forward mutates hidden_states in place (transformer3d.py:447-466): clone first
@@ -390,6 +392,39 @@ def gen_ckpt():
     _save("ckpt_export", out, meta)
 
 
+def gen_full():
+    """train_mode='full' (training.py:75-91; BASELINE config Z's trainable set):
+    the tiny model without LoRA, attn1/attn2 (incl. q/k norms), every scale_shift_table,
+    adaln_single, caption_projection and proj_out trainable; train_step + backward."""
+    seed, B = 1234, 2
+    g = torch.Generator().manual_seed(99)
+    batch = {
+        "latents": torch.randn(B, 128, 2, 8, 8, generator=g),
+        "ref_image_latents": torch.randn(B, 128, 1, 8, 8, generator=g),
+        "pose_latents": torch.randn(B, 128, 2, 8, 8, generator=g),
+    }
+    prompt = torch.randn(1, 4, 64, generator=g)
+    mask = torch.tensor([[1, 1, 1, 0]], dtype=torch.long)
+    pf = SymmetricPatchifier(patch_size=1)
+    model = Transformer3DModel.from_config(TINY_CONFIG)
+    model.patchifier = pf
+    P.init_module_(model, seed, dtype=torch.bfloat16)
+    model = T.apply_training_strategy(model, _train_cfg(16), "full")
+    cap = _capture_train_step(model, pf, batch, prompt, mask, seed=4321, rank=16)
+    grads = _grads(model)
+    tensors = {f"in.{k}": v for k, v in batch.items()}
+    tensors["in.prompt_embeds"] = prompt
+    tensors["in.prompt_attention_mask"] = mask
+    for k in ("tokens", "noise", "t", "hidden_states", "indices_grid", "sample", "loss"):
+        tensors[f"out.{k}"] = cap[k]
+    for k, v in grads.items():
+        tensors[f"grad.{k}"] = v
+    meta = {"config": TINY_CONFIG, "param_seed": seed, "train_seed": 4321, "train_mode": "full",
+            "trainable": sorted(grads), "weights_sha256": P.weights_sha256(model),
+            "source": "reference ltx_video/training.py:75-91 + 94-166 via oracle/shim"}
+    _save("tiny_full_step", tensors, meta)
+
+
 def gen_config():
     cfg = load_train_config_from_yaml(os.path.join(REF, "configs", "train-avatars.yaml"))
     d = dataclasses.asdict(cfg)
@@ -409,3 +444,4 @@ if __name__ == "__main__":
     gen_block2b()
     gen_infer()
     gen_ckpt()
+    gen_full()

@@ -277,3 +277,95 @@ def test_grad_allreduce_gloo_world2():
             assert got.dtype == e.dtype
             assert torch.equal(got, e), (r, i)
     assert math.isfinite(float(expect[0].sum()))
+
+
+# ------------------------------------------------------------------ ZeRO-2 (gloo, world size 2)
+ZSHAPES = [(16, 64), (64,), (300,), (7, 5), (1001,)]
+Z_LR, Z_CLIP, Z_STEPS = 1e-2, 0.5, 3
+
+
+def _ref_adamw(master, g, m, v, step, lr, b1=0.9, b2=0.999, eps=1e-8, wd=1e-2):
+    """torch.optim.AdamW's single-tensor update (the math ltx_adamw_step implements)."""
+    master.mul_(1 - lr * wd)
+    m.lerp_(g, 1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    master.addcdiv_(m, denom, value=-lr / bc1)
+
+
+def _zero_cpu_cls():
+    """Zero2AdamW with its HIP kernels swapped for torch math: the CPU gloo test checks the
+    partition, bucketing, collectives and clip bookkeeping (the kernels are covered on the GPU)."""
+    from ltx_amd.zero import Zero2AdamW
+
+    class CpuZero2(Zero2AdamW):
+        def _cast_to_f32(self, src, dst):
+            dst.copy_(src.float())
+
+        def _cast_to_bf16(self, src, dst):
+            dst.copy_(src.to(torch.bfloat16))
+
+        def _sumsq(self, x, out):
+            out.fill_(float((x.double() ** 2).sum()))
+
+        def _clip_scale(self, x, sumsq, coef):
+            norm = math.sqrt(float(sumsq)) / self.world
+            c = min(1.0, self.clip / (norm + 1e-6)) if self.clip > 0 else 1.0
+            coef.fill_(c / self.world)
+            x.mul_(float(coef))
+
+        def _adamw(self, master, g, m, v, step):
+            _ref_adamw(master, g, m, v, step, self.lr)
+    return CpuZero2
+
+
+def _zero_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g0 = torch.Generator().manual_seed(7)
+        params = [torch.nn.Parameter(torch.randn(s, generator=g0).to(torch.bfloat16))
+                  for s in ZSHAPES]
+        opt = _zero_cpu_cls()(params, lr=Z_LR, gradient_clipping=Z_CLIP, bucket_elems=512)
+        g = torch.Generator().manual_seed(100 + rank)
+        for _ in range(Z_STEPS):
+            for p in params:  # accumulate into the flat-buffer views, as the kernels do
+                p.grad.add_(torch.randn(p.shape, generator=g).to(torch.bfloat16))
+            opt.step()
+            opt.zero_grad()
+        torch.save([p.detach().clone() for p in params], os.path.join(out_dir, f"z{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zero2_gloo_world2_matches_single_process_math():
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        mp.start_processes(_zero_worker, args=(world, _free_port(), td), nprocs=world,
+                           start_method="spawn", join=True)
+        res = [torch.load(os.path.join(td, f"z{r}.pt"), weights_only=True) for r in range(world)]
+    # reference: one process, f32 master of all params, averaged + globally clipped grads
+    g0 = torch.Generator().manual_seed(7)
+    params = [torch.randn(s, generator=g0).to(torch.bfloat16) for s in ZSHAPES]
+    master = [p.float() for p in params]
+    m = [torch.zeros_like(x) for x in master]
+    v = [torch.zeros_like(x) for x in master]
+    gens = [torch.Generator().manual_seed(100 + r) for r in range(world)]
+    for step in range(1, Z_STEPS + 1):
+        grads = [torch.zeros_like(x) for x in master]
+        for r in range(world):
+            for i, s in enumerate(ZSHAPES):
+                grads[i] += torch.randn(s, generator=gens[r]).to(torch.bfloat16).float()
+        grads = [x / world for x in grads]
+        norm = math.sqrt(sum(float((x.double() ** 2).sum()) for x in grads))
+        c = min(1.0, Z_CLIP / (norm + 1e-6))
+        for i in range(len(master)):
+            _ref_adamw(master[i], grads[i] * c, m[i], v[i], step, Z_LR)
+    expect = [x.to(torch.bfloat16) for x in master]
+    for r in range(world):
+        for i, e in enumerate(expect):
+            assert torch.allclose(res[r][i].float(), e.float(), rtol=0, atol=1e-2), (r, i)
+            assert (res[r][i] != e).float().mean() < 0.02, (r, i)  # bf16 ulp flips only
+    for i in range(len(expect)):
+        assert torch.equal(res[0][i], res[1][i])  # every rank holds the same weights

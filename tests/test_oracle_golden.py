@@ -197,3 +197,25 @@ def test_reference_scheduler_cases(sampler):
         tm = (ts[i] + ts[i + 1]) / 2 if i < len(ts) - 1 else ts[i] / 2
         out = O.rf_step(v, torch.full(lat.shape[:2], float(tm)), lat, ts)
         assert torch.allclose(out, lat - (tm - nt) * v, atol=1e-6)
+
+
+# ---- train_mode='full'  ------------------------------------------------
+FULL_KEYS = ("proj_out", "scale_shift_table", "adaln_single", "caption_projection", "attn")
+
+
+def test_full_mode_step_matches_reference():
+    d, meta = _load("tiny_full_step")
+    cfg = meta["config"]
+    p = O.make_params(cfg, meta["param_seed"], lora_rank=0, requires_grad=False)
+    for k, v in p.items():
+        v.requires_grad_(any(s in k for s in FULL_KEYS))
+    assert sorted(k for k, v in p.items() if v.requires_grad) == meta["trainable"]
+    torch.manual_seed(meta["train_seed"])
+    r = O.train_step(p, cfg, d["in.latents"], d["in.ref_image_latents"], d["in.pose_latents"],
+                     d["in.prompt_embeds"], d["in.prompt_attention_mask"])
+    assert torch.equal(r["x_t"], d["out.hidden_states"])
+    assert _rel(r["sample"], d["out.sample"]) < 2e-3
+    r["loss"].backward()
+    for k, v in d.items():
+        if k.startswith("grad."):
+            assert _rel(p[k[5:]].grad, v) < 5e-3, k

@@ -103,7 +103,16 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       out8[j + 1] = g[1];
     }
   } else if constexpr (EPI == LTX_EPI_GATED_RESIDUAL) {
-    // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1)
+    // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1);
+    // aux2 (optional, ld2): store of the pre-gate y (the gate's gradient in train_mode='full')
+    if (p.aux2) {
+      u32x4 pk;
+      pk[0] = (unsigned)cvals[0] | ((unsigned)cvals[1] << 16);
+      pk[1] = (unsigned)cvals[2] | ((unsigned)cvals[3] << 16);
+      pk[2] = (unsigned)cvals[4] | ((unsigned)cvals[5] << 16);
+      pk[3] = (unsigned)cvals[6] | ((unsigned)cvals[7] << 16);
+      *(u32x4*)((bf16_t*)p.aux2 + (int64_t)m * p.ld2 + n0) = pk;
+    }
     const int b = m / p.rows_per_batch;
     const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
     const u32x4 g4 = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)b * p.ld1 + n0);

@@ -423,6 +423,63 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
   }
 }
 
+// Weight gradient of the q/k RMSNorm (train_mode='full'): y = bf16(n) * w with n = x * rstd, so
+// dw = sum_rows bf16(dn * bf16(n)) where dn is the gradient at the norm output (the RoPE^T of the
+// incoming gradient, same roundings as qk_norm_rope_bwd_kernel). Block (which, split) sums its
+// rows for all D columns (8 per thread) into part[(which * S + split) * D + col] (f32).
+__global__ __launch_bounds__(256) void qk_norm_wgrad_kernel(
+    const void* __restrict__ dq_in, int64_t ldq_in, int dq_f32, const void* __restrict__ dk_in, int64_t ldk_in,
+    int dk_f32, const bf16_t* __restrict__ q_raw, int64_t ldq_raw, const bf16_t* __restrict__ k_raw,
+    int64_t ldk_raw, const float* __restrict__ rstd_q, const float* __restrict__ rstd_k,
+    const uint32_t* __restrict__ cs, int64_t cs_batch_rows, int N, int M, int D, int rope, int S,
+    float* __restrict__ part) {
+  const int which = blockIdx.y;
+  const int split = blockIdx.x;
+  const int e = threadIdx.x * 8;
+  const int m0 = (int)((int64_t)split * M / S), m1 = (int)((int64_t)(split + 1) * M / S);
+  const void* gin = which ? dk_in : dq_in;
+  const int64_t ldg = which ? ldk_in : ldq_in;
+  const int gf32 = which ? dk_f32 : dq_f32;
+  const bf16_t* xr = which ? k_raw : q_raw;
+  const int64_t ldx = which ? ldk_raw : ldq_raw;
+  const float* rs = which ? rstd_k : rstd_q;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (e < D) {
+    for (int m = m0; m < m1; ++m) {
+      float g8[8], dn[8], x8[8];
+      if (gf32) {
+        load8f((const float*)gin + (int64_t)m * ldg + e, g8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g8[j] = rbf(g8[j]);
+      } else {
+        load8((const bf16_t*)gin + (int64_t)m * ldg + e, g8);
+      }
+      if (rope) {
+        float c4[4], s4[4];
+        cs4(cs, ((int64_t)(m / N) * cs_batch_rows + (m % N)) * (D / 2), e, c4, s4);
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const float c = c4[j >> 1], s = s4[j >> 1];
+          const float da0 = rbf(g8[j] * c), da1 = rbf(g8[j + 1] * c);
+          const float dr0 = rbf(g8[j] * s), dr1 = rbf(g8[j + 1] * s);
+          dn[j] = rbf(da0 + dr1);
+          dn[j + 1] = rbf(da1 + (-dr0));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dn[j] = g8[j];
+      }
+      load8(xr + (int64_t)m * ldx + e, x8);
+      const float r = rs[m];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += rbf(dn[j] * rbf(x8[j] * r));
+    }
+    float* o = part + ((int64_t)which * S + split) * D + e;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = acc[j];
+  }
+}
+
 static inline unsigned row_blocks(int64_t items) { return (unsigned)((items + 3) / 4); }
 
 }  // namespace ltx
@@ -528,6 +585,23 @@ int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const
                      ldq_raw, (const bf16_t*)k_raw, ldk_raw, (const bf16_t*)q_weight, (const bf16_t*)k_weight,
                      rstd_q, rstd_k, (bf16_t*)dq_out, ldq_out, (bf16_t*)dk_out, ldk_out, rope_cs, cs_batch_rows,
                      (int)N, (int)M, (int)D, rope, nsel);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_qk_norm_wgrad(const void* dq_in, int64_t ldq_in, int dq_is_f32, const void* dk_in, int64_t ldk_in,
+                      int dk_is_f32, const void* q_raw, int64_t ldq_raw, const void* k_raw, int64_t ldk_raw,
+                      const float* rstd_q, const float* rstd_k, const uint32_t* rope_cs, int64_t cs_batch_rows,
+                      int64_t B, int64_t N, int64_t D, int rope, int64_t splits, float* partials, void* stream) {
+  LTX_CHECK_ARG(dq_in && q_raw && rstd_q && partials && B > 0 && N > 0 && splits > 0, "qk_norm_wgrad: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "qk_norm_wgrad: D must be %8 and <= 2048");
+  LTX_CHECK_ARG(!rope || (rope_cs && ((uintptr_t)rope_cs % 16) == 0), "qk_norm_wgrad: rope needs a 16-B aligned table");
+  const bool has_k = dk_in != nullptr;
+  LTX_CHECK_ARG(!has_k || (k_raw && rstd_k), "qk_norm_wgrad: incomplete k operands");
+  hipLaunchKernelGGL(qk_norm_wgrad_kernel, dim3((unsigned)splits, has_k ? 2u : 1u), dim3(256), 0, (hipStream_t)stream,
+                     dq_in, ldq_in, dq_is_f32, dk_in, ldk_in, dk_is_f32, (const bf16_t*)q_raw, ldq_raw,
+                     (const bf16_t*)k_raw, ldk_raw, rstd_q, rstd_k, rope_cs, cs_batch_rows, (int)N, (int)(B * N),
+                     (int)D, rope, (int)splits, partials);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

@@ -60,6 +60,15 @@ _SIGNATURES = {
     "ltx_batch_sum_bf16": [_p, _i64, _i64, _i64, _i64, _p, _i64, _p],
     "ltx_mse_fwd_bwd": [_p, _p, _p, _p, _i64, _f32, _p],
     "ltx_adamw_step": [_p, _p, _p, _p, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i64, _p],
+    "ltx_qk_norm_wgrad": [_p, _i64, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _p, _p, _p, _i64,
+                          _i64, _i64, _i64, _i32, _i64, _p, _p],
+    "ltx_group_colsum": [_p, _i64, _p, _i64, _p, _p, _i32, _i64, _i64, _i64, _i64, _p, _p],
+    "ltx_colsum_finish": [_p, _i64, _i64, _i64, _i32, _i32, _p, _i64, _p],
+    "ltx_silu_bwd_bf16": [_p, _p, _p, _p, _i64, _p],
+    "ltx_cast_bf16_f32": [_p, _p, _i64, _p],
+    "ltx_cast_f32_bf16": [_p, _p, _i64, _p],
+    "ltx_sumsq_f32": [_p, _i64, _p, _i32, _p],
+    "ltx_clip_scale_f32": [_p, _i64, _p, _f32, _f32, _p, _p],
     "ltx_pixel_coords_f32": [_p, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _f32, _p],
     "ltx_skip_blend_bf16": [_p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _p],
     "ltx_rf_euler_step": [_p, _i32, _p, _i32, _p, _i32, _p, _i64, _p, _f32, _i32, _p, _i32, _i64,

@@ -558,3 +558,84 @@ def guidance(noise_pred, batch_size, do_cfg, do_stg, guidance_scale=1.0, stg_sca
          float(guidance_scale), float(stg_scale), float(rescaling_scale),
          int(bool(cfg_star_rescale)), _p(ws), ws.numel(), _p(out), _s())
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# train_mode='full' parameter gradients (csrc/paramgrad.hip, norms.hip:qk_norm_wgrad)
+# ---------------------------------------------------------------------------------------------
+def _splits(rows, D, groups):
+    """row splits per group so that groups x splits ~ 512 blocks, >= 8 rows each"""
+    s = max(1, min(rows // 8, 512 // max(1, groups)))
+    return max(1, min(s, rows))
+
+
+def colsum_into(out, a, b=None, r=None, mean=None, mode=0, rows_per_group=None, sum_groups=True,
+                accumulate=True):
+    """out (bf16) [+]= bf16 column sums of `mode`-products over row groups of a [M, D] (see
+    ltx_group_colsum): sum_groups -> out [D] (sum over all groups), else out [G, D]."""
+    M, D = a.shape
+    rpg = M if rows_per_group is None else rows_per_group
+    G = M // rpg
+    S = _splits(rpg, D, G)
+    part = torch.empty(G, S, D, dtype=F32, device=a.device)
+    call("ltx_group_colsum", _p(a), _rows(a, "a"), _p(b), _rows(b, "b") if b is not None else 0,
+         _p(r), _p(mean), int(mode), M, D, rpg, S, _p(part), _s())
+    ldo = out.stride(0) if out.dim() == 2 else D
+    call("ltx_colsum_finish", _p(part), G, S, D, 1 if sum_groups else 0, 1 if accumulate else 0,
+         _p(out), ldo, _s())
+    return out
+
+
+def group_colsum(a, b=None, r=None, mean=None, mode=0, rows_per_group=None):
+    """bf16 [G, D]: per-group column sums (no accumulation)."""
+    M, D = a.shape
+    rpg = M if rows_per_group is None else rows_per_group
+    out = torch.empty(M // rpg, D, dtype=BF16, device=a.device)
+    return colsum_into(out, a, b, r, mean, mode, rpg, sum_groups=False, accumulate=False)
+
+
+def qk_norm_wgrad_into(dq, q_raw, rstd_q, gq, dk=None, k_raw=None, rstd_k=None, gk=None,
+                       rope: "RopeSpec" = None, B=None, N=None):
+    """q/k RMSNorm weight grads accumulated into gq / gk (bf16 [D])."""
+    M, D = q_raw.shape
+    if rope is not None:
+        B, N = rope.B, rope.N
+    S = _splits(M, D, 2 if dk is not None else 1)
+    nsel = 2 if dk is not None else 1
+    part = torch.empty(nsel, S, D, dtype=F32, device=q_raw.device)
+    call("ltx_qk_norm_wgrad", _p(dq), _rows(dq, "dq"), 1 if dq.dtype == F32 else 0, _p(dk),
+         _rows(dk, "dk") if dk is not None else 0, 1 if (dk is not None and dk.dtype == F32) else 0,
+         _p(q_raw), _rows(q_raw, "q_raw"), _p(k_raw), _rows(k_raw, "k_raw") if k_raw is not None else 0,
+         _p(rstd_q), _p(rstd_k), _p(rope.cs) if rope is not None else None,
+         rope.cs_batch_rows if rope is not None else 0, B, N, D, 1 if rope is not None else 0, S,
+         _p(part), _s())
+    call("ltx_colsum_finish", _p(part[0]), 1, S, D, 1, 1, _p(gq), D, _s())
+    if dk is not None:
+        call("ltx_colsum_finish", _p(part[1]), 1, S, D, 1, 1, _p(gk), D, _s())
+
+
+def silu_bwd(x, dy, dres=None):
+    out = torch.empty_like(dy)
+    call("ltx_silu_bwd_bf16", _p(x.contiguous()), _p(dy.contiguous()),
+         _p(dres.contiguous()) if dres is not None else None, _p(out), dy.numel(), _s())
+    return out
+
+
+def _tpad(x, npad):
+    """[M, C] -> [C, npad] bf16 transpose, zero-padded on the token axis (GEMM K % 64 == 0)."""
+    M, C = x.shape
+    buf = torch.empty(C, npad, dtype=BF16, device=x.device) if npad == M else \
+        torch.zeros(C, npad, dtype=BF16, device=x.device)
+    transpose(x, out=buf[:, :M])
+    return buf
+
+
+def wgrad_into(grad, dy, x, dyT=None):
+    """grad [N, K] (bf16) += bf16(dy^T . x) over the M token rows (dy [M, N], x [M, K]): the
+    weight gradient of an nn.Linear, through the NT GEMM on transposed operands (the token axis
+    becomes the GEMM K, zero-padded to a multiple of 64). dyT: a precomputed _tpad(dy)."""
+    M = dy.shape[0]
+    npad = (M + 63) // 64 * 64
+    a = dyT if dyT is not None else _tpad(dy, npad)
+    w = _tpad(x, npad)
+    gemm(a, w, epilogue="accum", aux0=grad, out=grad)

@@ -263,15 +263,14 @@ class BasicTransformerBlock(nn.Module):
 
     @torch.no_grad()
     def packed(self):
-        key = tuple((t.data_ptr(), t._version) for t in self._frozen())
+        """Fused QKV weight/bias and W^T copies for the dgrad GEMMs, rebuilt whenever a weight
+        changes (new storage, an in-place torch update, or a FusedAdamW step in
+        train_mode='full' -- ops.weight_generation())."""
+        key = (tuple((t.data_ptr(), t._version) for t in self._frozen()), ops.weight_generation()
+               if any(t.requires_grad for t in self._frozen()) else 0)
         if self._pack is not None and self._pack_key == key:
             return self._pack
         a1, a2, ff = self.attn1, self.attn2, self.ff
-        for t in self._frozen():
-            if t.requires_grad:
-                raise NotImplementedError(
-                    "fused block backward supports the lora_audio strategy (frozen attention/FF "
-                    "weights); train_mode='full' needs the wgrad path (DESIGN.md, next rows)")
         p = {}
         p["qkv_w"] = torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight], 0).contiguous()
         p["qkv_b"] = torch.cat([a1.to_q.bias, a1.to_k.bias, a1.to_v.bias], 0).contiguous()
@@ -335,9 +334,18 @@ class _Shared:
         self.rope = rope
         self.enc_bias = enc_bias
         self.eps = eps
+        self.full = False  # train_mode='full': attention / AdaLN weights take gradients
 
 
 _LORA_KEYS = ("q", "k", "v", "o")
+
+
+def _pgrad(p):
+    """p.grad (bf16), created zeroed on first use: the full-mode kernels accumulate into it
+    (the reference's .grad += over micro-steps)."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+    return p.grad
 
 
 def _lora_params(blk):
@@ -383,7 +391,10 @@ class _BlockFn(torch.autograd.Function):
         x1, rstd1 = ops.rmsnorm_modulate_fwd(h, mods[:, 0], onep[:, 1], ldm, rpm, blk.norm_eps)
         qkv = ops.gemm(x1, W["qkv_w"], bias=W["qkv_b"])
         strat = skip[1] if skip is not None else None
-        if strat is not SkipLayerStrategy.AttentionSkip:
+        full = sh.full and keep
+        if has_lora and full:
+            raise NotImplementedError("train_mode='full' trains the base weights without LoRA")
+        if strat is not SkipLayerStrategy.AttentionSkip and not full:
             del x1
         qk = torch.empty(M, 2 * D, dtype=torch.bfloat16, device=h.device)
         _, _, rq1, rk1 = ops.qk_norm_rope_fwd(qkv[:, :D], qkv[:, D:2 * D], a1.q_norm.weight,
@@ -392,11 +403,13 @@ class _BlockFn(torch.autograd.Function):
         o1, lse1 = ops.attn_fwd(qk[:, :D], qk[:, D:], qkv[:, 2 * D:], B, H, d, a1.scale)
         if strat is SkipLayerStrategy.AttentionSkip:  # blend with the processor input
             o1 = ops.skip_blend(o1, x1, skip[0], N)
-            del x1
+            if not full:
+                del x1
         elif strat is SkipLayerStrategy.AttentionValues:  # blend with to_v's output
             o1 = ops.skip_blend(o1, qkv[:, 2 * D:], skip[0], N)
+        y1 = torch.empty(M, D, dtype=torch.bfloat16, device=h.device) if full else None
         h1 = ops.gemm(o1, a1.to_out[0].weight, bias=a1.to_out[0].bias, epilogue="gated_residual",
-                      aux0=h, aux1=mods[:, 2], rows_per_batch=rpm)
+                      aux0=h, aux1=mods[:, 2], aux2=y1, rows_per_batch=rpm)
         # ---- 2. attn2 on the un-normalised h1 (attention.py:273-285), LoRA fused into the GEMMs
         wq, bq, _ = _lin(a2.to_q)
         wk, bk, _ = _lin(a2.to_k)
@@ -435,17 +448,19 @@ class _BlockFn(torch.autograd.Function):
         act = ops.gemm(x2, ff.net[0].proj.weight, bias=ff.net[0].proj.bias, epilogue="gelu",
                        aux0=fpre)
         del x2
+        y3 = torch.empty(M, D, dtype=torch.bfloat16, device=h.device) if full else None
         h3 = ops.gemm(act, ff.net[2].weight, bias=ff.net[2].bias, epilogue="gated_residual",
-                      aux0=h2, aux1=mods[:, 5], rows_per_batch=rpm)
+                      aux0=h2, aux1=mods[:, 5], aux2=y3, rows_per_batch=rpm)
         del act
         if strat is SkipLayerStrategy.TransformerBlock:
             h3 = ops.skip_blend(h3, h, skip[0], N)
         if keep:
             lora_saved = (u_q, u_k, u_v, u_o) if has_lora else ()
+            full_saved = (x1, y1, y3) if full else ()
             ctx.save_for_backward(h, enc2, mods, onep, rstd1, qkv, qk, rq1, rk1, o1, lse1, h1,
                                   q2raw, rq2, q2, k2raw, rk2, k2, v2, o2, lse2, h2, rstd2, fpre,
-                                  *lora_ab, *lora_saved)
-            ctx.blk, ctx.sh, ctx.has_lora = blk, sh, has_lora
+                                  *lora_ab, *lora_saved, *full_saved)
+            ctx.blk, ctx.sh, ctx.has_lora, ctx.full = blk, sh, has_lora, full
         return h3
 
     @staticmethod
@@ -461,6 +476,10 @@ class _BlockFn(torch.autograd.Function):
         ldm = mods.stride(0)
         dh3 = dh3.contiguous()
         grads_lora = []
+        full = ctx.full
+        if full:
+            x1, y1, y3 = saved[24:27]
+            dmods = torch.empty(B, 6, D, dtype=torch.bfloat16, device=h.device)
         if has_lora:
             Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo = saved[24:32]
             u_q, u_k, u_v, u_o = saved[32:36]
@@ -469,11 +488,18 @@ class _BlockFn(torch.autograd.Function):
         # ---- FF: h3 = h2 + g_mlp * ff(x2)
         rpm = sh.rpm
         d_ffo = ops.gate_mul(dh3, mods[:, 5], rpm)
+        if full:  # gate_mlp: sum over the batch's rows of bf16(dh3 * y3) (attention.py:305-308)
+            ops.colsum_into(dmods[:, 5], dh3, y3, mode=1, rows_per_group=rpm, sum_groups=False,
+                            accumulate=False)
         d_f = ops.gemm(d_ffo, W["ff2_wT"], epilogue="gelu_bwd", aux0=fpre)
         del d_ffo
         dx2 = ops.gemm(d_f, W["ff1_wT"])
         del d_f
         dh2 = ops.rmsnorm_modulate_bwd(dx2, h2, rstd2, onep[:, 4], ldm, rpm, dres=dh3)
+        if full:  # shift_mlp / scale_mlp (attention.py:287-290)
+            ops.colsum_into(dmods[:, 3], dx2, rows_per_group=rpm, sum_groups=False, accumulate=False)
+            ops.colsum_into(dmods[:, 4], dx2, h2, rstd2, mode=2, rows_per_group=rpm,
+                            sum_groups=False, accumulate=False)
         del dx2
         # ---- attn2: h2 = h1 + to_out(o2)   (LoRA grads: peft f32 adapters)
         if has_lora:
@@ -484,6 +510,10 @@ class _BlockFn(torch.autograd.Function):
             do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")))
         else:
             do2 = ops.gemm(dh2, W["o2_wT"])
+        if full:  # attn2.to_out.0
+            lin = a2.to_out[0]
+            ops.wgrad_into(_pgrad(lin.weight), dh2, o2)
+            ops.colsum_into(_pgrad(lin.bias), dh2)
         dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
                                      key_bias=sh.enc_bias, kv_shared=sh.text_shared)
         del do2
@@ -492,6 +522,15 @@ class _BlockFn(torch.autograd.Function):
             dv2 = ops.batch_sum(dv2, B)
         dq2raw, _ = ops.qk_norm_rope_bwd(dq2, q2raw, a2.q_norm.weight, rq2, B=B, N=N)
         dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=sh.Bt, N=L)
+        if full:  # attn2 q/k norm weights, to_q / to_k / to_v
+            ops.qk_norm_wgrad_into(dq2, q2raw, rq2, _pgrad(a2.q_norm.weight), B=B, N=N)
+            ops.qk_norm_wgrad_into(dk2, k2raw, rk2, _pgrad(a2.k_norm.weight), B=sh.Bt, N=L)
+            ops.wgrad_into(_pgrad(a2.to_q.weight), dq2raw, h1)
+            ops.colsum_into(_pgrad(a2.to_q.bias), dq2raw)
+            ops.wgrad_into(_pgrad(a2.to_k.weight), dk2raw, enc2)
+            ops.colsum_into(_pgrad(a2.to_k.bias), dk2raw)
+            ops.wgrad_into(_pgrad(a2.to_v.weight), dv2, enc2)
+            ops.colsum_into(_pgrad(a2.to_v.bias), dv2)
         del dq2, dk2
         if has_lora:
             ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
@@ -520,6 +559,12 @@ class _BlockFn(torch.autograd.Function):
         # ---- attn1: h1 = h + g_msa * to_out(sdpa(rope(qn(q)), rope(kn(k)), v))
         d_y1 = ops.gate_mul(dh1, mods[:, 2], rpm)
         do1 = ops.gemm(d_y1, W["out1_wT"])
+        if full:  # gate_msa, attn1.to_out.0
+            ops.colsum_into(dmods[:, 2], dh1, y1, mode=1, rows_per_group=rpm, sum_groups=False,
+                            accumulate=False)
+            lin = a1.to_out[0]
+            ops.wgrad_into(_pgrad(lin.weight), d_y1, o1)
+            ops.colsum_into(_pgrad(lin.bias), d_y1)
         del d_y1
         M = B * N
         dqkv = torch.empty(M, 3 * D, dtype=torch.bfloat16, device=h.device)
@@ -529,12 +574,29 @@ class _BlockFn(torch.autograd.Function):
         ops.qk_norm_rope_bwd(dq1, qkv[:, :D], a1.q_norm.weight, rq1, dk1, qkv[:, D:2 * D],
                              a1.k_norm.weight, rk1, sh.rope, dq_out=dqkv[:, :D],
                              dk_out=dqkv[:, D:2 * D])
+        if full:  # attn1 q/k norm weights, to_q / to_k / to_v (fused dQKV^T . x1)
+            ops.qk_norm_wgrad_into(dq1, qkv[:, :D], rq1, _pgrad(a1.q_norm.weight), dk1,
+                                   qkv[:, D:2 * D], rk1, _pgrad(a1.k_norm.weight), rope=sh.rope)
+            npad = (M + 63) // 64 * 64
+            dqkvT = ops._tpad(dqkv, npad)
+            x1T = ops._tpad(x1, npad)
+            for i, lin in enumerate((a1.to_q, a1.to_k, a1.to_v)):
+                g = _pgrad(lin.weight)
+                ops.gemm(dqkvT[i * D:(i + 1) * D], x1T, epilogue="accum", aux0=g, out=g)
+                ops.colsum_into(_pgrad(lin.bias), dqkv[:, i * D:(i + 1) * D])
+            del dqkvT, x1T
         del dq1, dk1
         dh = None
-        if ctx.needs_input_grad[4]:  # (blk, sh, keep, skip, h, ...)
+        if ctx.needs_input_grad[4] or full:  # (blk, sh, keep, skip, h, ...)
             dx1 = ops.gemm(dqkv, W["qkv_wT"])
             dh = ops.rmsnorm_modulate_bwd(dx1, h, rstd1, onep[:, 1], ldm, rpm, dres=dh1)
-        return (None, None, None, None, dh, denc, None, None, *grads_lora)
+            if full:  # shift_msa / scale_msa (attention.py:229-236)
+                ops.colsum_into(dmods[:, 0], dx1, rows_per_group=rpm, sum_groups=False,
+                                accumulate=False)
+                ops.colsum_into(dmods[:, 1], dx1, h, rstd1, mode=2, rows_per_group=rpm,
+                                sum_groups=False, accumulate=False)
+        dm = dmods if full else None
+        return (None, None, None, None, dh, denc, dm, None, *grads_lora)
 
 
 class _CaptionProjFn(torch.autograd.Function):
@@ -571,26 +633,100 @@ class _CaptionProjFn(torch.autograd.Function):
         return None, dw1, db1, dw2, db2
 
 
+def _tpad_t(x):
+    """x [R, C] -> x^T zero-padded to [C, round_up(R, 64)] (GEMM K % 64 == 0)."""
+    return ops._tpad(x, (x.shape[0] + 63) // 64 * 64)
+
+
+def _lin_wgrad(dy, x):
+    """nn.Linear weight grad dy^T . x over the rows (bf16, f32 accumulation)."""
+    return ops.gemm(_tpad_t(dy), _tpad_t(x))
+
+
+class _AdaModFn(torch.autograd.Function):
+    """ada_values = scale_shift_table + tmod (attention.py:225-231; head: transformer3d.py:554-556,
+    tmod broadcast over the P rows) -> (mods, 1 + mods on the scale rows). Differentiable for
+    train_mode='full': d sst = sum over the batch, d tmod = d ada (or its sum over the P rows)."""
+
+    @staticmethod
+    def forward(ctx, sst, tmod, scale_mask, broadcast):
+        mods, onep = ops.ada_modulation(sst, tmod, scale_mask, broadcast=broadcast)
+        ctx.broadcast, ctx.P = broadcast, sst.shape[0]
+        ctx.mark_non_differentiable(onep)
+        return mods, onep
+
+    @staticmethod
+    def backward(ctx, dmods, donep):
+        B, P, D = dmods.shape
+        d = dmods.contiguous().view(B, P * D)
+        dsst = ops.group_colsum(d).view(P, D)
+        dtmod = ops.group_colsum(d.view(B * P, D), rows_per_group=P) if ctx.broadcast else d
+        return dsst, dtmod, None, None
+
+
+class _AdaLNFn(torch.autograd.Function):
+    """AdaLayerNormSingle (transformer3d.py:473-491) with trainable weights (train_mode='full'):
+    te -> linear_1 -> SiLU -> linear_2 = emb; SiLU(emb) -> linear = tmod. Backward: the small
+    [B, *] GEMMs, SiLU backward kernels, weight grads over the B rows (zero-padded K)."""
+
+    @staticmethod
+    def forward(ctx, te, w1, b1, w2, b2, w, b):
+        e1 = ops.gemm(te, w1, bias=b1)
+        s1 = ops.silu(e1)
+        emb = ops.gemm(s1, w2, bias=b2)
+        s2 = ops.silu(emb)
+        tmod = ops.gemm(s2, w, bias=b)
+        ctx.save_for_backward(te, e1, s1, emb, s2, w2, w)
+        return tmod, emb
+
+    @staticmethod
+    def backward(ctx, dtmod, demb):
+        te, e1, s1, emb, s2, w2, w = ctx.saved_tensors
+        dtmod = dtmod.contiguous()
+        ds2 = ops.gemm(dtmod, ops.transpose(w))
+        dw, db = _lin_wgrad(dtmod, s2), ops.colsum(dtmod)
+        demb_t = ops.silu_bwd(emb, ds2, dres=None if demb is None else demb.contiguous())
+        ds1 = ops.gemm(demb_t, ops.transpose(w2))
+        dw2, db2 = _lin_wgrad(demb_t, s1), ops.colsum(demb_t)
+        de1 = ops.silu_bwd(e1, ds1)
+        dw1, db1 = _lin_wgrad(de1, te), ops.colsum(de1)
+        return None, dw1, db1, dw2, db2, dw, db
+
+
 class _HeadFn(torch.autograd.Function):
     """Output modulation + projection (transformer3d.py:553-561): LayerNorm (no affine,
-    eps 1e-6) * (1 + scale) + shift, then proj_out."""
+    eps 1e-6) * (1 + scale) + shift, then proj_out. In train_mode='full' also the grads of the
+    head's shift/scale rows (per batch) and of proj_out."""
 
     @staticmethod
     def forward(ctx, h, mod, onep, w, b, N, eps):
         ldm = mod.stride(0)
         y, mean, rstd = ops.layernorm_modulate_fwd(h, mod[:, 0], onep[:, 1], ldm, N, eps)
         out = ops.gemm(y, w, bias=b)
-        ctx.save_for_backward(h, mean, rstd, onep, w)
-        ctx.N = N
+        ctx.save_for_backward(h, mean, rstd, mod, onep, w)
+        ctx.N, ctx.eps = N, eps
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        h, mean, rstd, onep, w = ctx.saved_tensors
+        h, mean, rstd, mod, onep, w = ctx.saved_tensors
+        dout = dout.contiguous()
         wT = ops.transpose(w)
-        dy = ops.gemm(dout.contiguous(), wT)
+        dy = ops.gemm(dout, wT)
         dh = ops.layernorm_modulate_bwd(dy, h, mean, rstd, onep[:, 1], onep.stride(0), ctx.N)
-        return dh, None, None, None, None, None, None
+        dmod = dw = db = None
+        if ctx.needs_input_grad[1]:
+            B = mod.shape[0]
+            dmod = torch.empty(B, 2, h.shape[1], dtype=torch.bfloat16, device=h.device)
+            ops.colsum_into(dmod[:, 0], dy, rows_per_group=ctx.N, sum_groups=False,
+                            accumulate=False)
+            ops.colsum_into(dmod[:, 1], dy, h, rstd, mean, mode=3, rows_per_group=ctx.N,
+                            sum_groups=False, accumulate=False)
+        if ctx.needs_input_grad[3]:
+            y, _, _ = ops.layernorm_modulate_fwd(h, mod[:, 0], onep[:, 1], mod.stride(0), ctx.N,
+                                                 ctx.eps)
+            dw, db = _lin_wgrad(dout, y), ops.colsum(dout)
+        return dh, dmod, None, dw, db, None, None
 
 
 # ===============================================================================================
@@ -810,10 +946,25 @@ class Transformer3DModel(nn.Module):
         per_token = timestep.numel() != B
         if per_token and timestep.numel() != B * N:
             raise ValueError(f"timestep has {timestep.numel()} values for batch {B} x {N} tokens")
+        keep = torch.is_grad_enabled()
+        # train_mode='full' (training.py:75-91): AdaLN-single, every scale_shift_table, the
+        # attention weights and proj_out train
+        full = keep and self.adaln_single.linear.weight.requires_grad
         with torch.no_grad():
             h = ops.gemm(x_in.reshape(B * N, C), self.patchify_proj.weight,
                          bias=self.patchify_proj.bias)
-            tmod, emb = self._adaln(timestep)
+        if full:
+            ad = self.adaln_single
+            mult = float(self.timestep_scale_multiplier or 1.0)
+            te = ops.timestep_embedding(timestep.reshape(-1).float().contiguous(), mult)
+            tmod, emb = _AdaLNFn.apply(te, ad.emb.timestep_embedder.linear_1.weight,
+                                       ad.emb.timestep_embedder.linear_1.bias,
+                                       ad.emb.timestep_embedder.linear_2.weight,
+                                       ad.emb.timestep_embedder.linear_2.bias, ad.linear.weight,
+                                       ad.linear.bias)
+        else:
+            with torch.no_grad():
+                tmod, emb = self._adaln(timestep)
         rope = ops.RopeSpec(indices_grid, D, self.positional_embedding_theta,
                             self.positional_embedding_max_pos)
         enc = encoder_hidden_states.to(dt)
@@ -825,7 +976,7 @@ class Transformer3DModel(nn.Module):
         eps = self.transformer_blocks[0].norm_eps if len(self.transformer_blocks) else 1e-6
         sh = _Shared(B, N, L, H, self.attention_head_dim, rope, enc_bias, eps, text_shared,
                      per_token)
-        keep = torch.is_grad_enabled()
+        sh.full = full
         strat = None
         if skip_layer_mask is not None and skip_layer_strategy is not None:
             strat = SkipLayerStrategy[skip_layer_strategy.name] if isinstance(
@@ -834,8 +985,13 @@ class Transformer3DModel(nn.Module):
                 strat = None
         for i, blk in enumerate(self.transformer_blocks):
             skip = None if strat is None else (skip_layer_mask[i].to(dt).contiguous(), strat)
-            with torch.no_grad():
-                mods, onep = ops.ada_modulation(blk.scale_shift_table, tmod, (1 << 1) | (1 << 4))
+            if full:
+                mods, onep = _AdaModFn.apply(blk.scale_shift_table, tmod, (1 << 1) | (1 << 4),
+                                             False)
+            else:
+                with torch.no_grad():
+                    mods, onep = ops.ada_modulation(blk.scale_shift_table, tmod,
+                                                    (1 << 1) | (1 << 4))
             lora = _lora_params(blk)
             ab = []
             if lora is not None:
@@ -847,8 +1003,12 @@ class Transformer3DModel(nn.Module):
                     h, enc2, mods, onep, *ab, use_reentrant=False)
             else:
                 h = _BlockFn.apply(blk, sh, keep, skip, h, enc2, mods, onep, *ab)
-        with torch.no_grad():
-            hmod, honep = ops.ada_modulation(self.scale_shift_table, emb, 1 << 1, broadcast=True)
+        if full:
+            hmod, honep = _AdaModFn.apply(self.scale_shift_table, emb, 1 << 1, True)
+        else:
+            with torch.no_grad():
+                hmod, honep = ops.ada_modulation(self.scale_shift_table, emb, 1 << 1,
+                                                 broadcast=True)
         out = _HeadFn.apply(h, hmod, honep, self.proj_out.weight, self.proj_out.bias, sh.rpm, 1e-6)
         return out.view(B, N, self.out_channels)
 
