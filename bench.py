@@ -47,15 +47,19 @@ def step_flops_per_sample(N, r=LORA_RANK, D=2048, FF=8192, Lyr=28, L=L_TXT, C=12
     return fwd, bwd
 
 
-def build_model(device, seed=1234):
+FULL_KEYS = ("proj_out", "scale_shift_table", "adaln_single", "caption_projection", "attn")
+
+
+def build_model(device, seed=1234, mode="lora_audio"):
     from ltx_amd.config import TrainConfig
     from ltx_amd.lora import apply_training_strategy
     from ltx_amd.patchifier import SymmetricPatchifier
     from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG, Transformer3DModel
     with torch.device("meta"):
         model = Transformer3DModel.from_config(OURS_TRANSFORMER_CONFIG)
-        apply_training_strategy(model, TrainConfig(checkpoint_path="-", lora_rank=LORA_RANK,
-                                                   lora_alpha=LORA_RANK), "lora_audio")
+        if mode != "full":
+            apply_training_strategy(model, TrainConfig(checkpoint_path="-", lora_rank=LORA_RANK,
+                                                       lora_alpha=LORA_RANK), "lora_audio")
     g = torch.Generator(device=device).manual_seed(seed)
     sd = {}
     for name, p in model.named_parameters():
@@ -74,7 +78,10 @@ def build_model(device, seed=1234):
         sd[name] = t.to(dt)
     model.load_state_dict(sd, assign=True, strict=True)
     for n, p in model.named_parameters():
-        p.requires_grad_(("lora_" in n) or ("caption_projection" in n))
+        if mode == "full":  # training.py:75-91 trainable set (config Z)
+            p.requires_grad_(any(k in n for k in FULL_KEYS))
+        else:
+            p.requires_grad_(("lora_" in n) or ("caption_projection" in n))
     model.patchifier = SymmetricPatchifier(1)
     model.train()
     return model
@@ -221,8 +228,11 @@ def main():
                          "BASELINE configs[3], long-sequence stress)")
     ap.add_argument("--batch", type=int, default=None, help="micro-batch per GPU (default 8)")
     ap.add_argument("--grad-ckpt", action="store_true", help="per-block gradient checkpointing")
+    ap.add_argument("--mode", choices=["lora", "full"], default="lora",
+                    help="full: train_mode='full' + ZeRO-2 AdamW (BASELINE configs[4], "
+                         "ds_config_zero2.json: grad accumulation 3, clip 1.0)")
     args = ap.parse_args()
-    global F_LAT, H_LAT, W_LAT, B_PER_GPU
+    global F_LAT, H_LAT, W_LAT, B_PER_GPU, ACCUM
     if args.config == "x":
         F_LAT, H_LAT, W_LAT = 13, 24, 24
     if args.batch:
@@ -247,7 +257,10 @@ def main():
     from ltx_amd.training import FusedAdamW, GradAllReduce, train_step
     _lib.ensure_device(device)
 
-    model = build_model(device)
+    full = args.mode == "full"
+    if full:
+        ACCUM = 3  # ds_config_zero2.json gradient_accumulation_steps
+    model = build_model(device, mode="full" if full else "lora_audio")
     model.gradient_checkpointing = bool(args.grad_ckpt)
     batch, prompt, mask = synthetic_batch(device, rank)
     cfg = TrainConfig(checkpoint_path="-", batch_size=B_PER_GPU, learning_rate=1e-4,
@@ -255,8 +268,13 @@ def main():
                       rf_log_normal_mu=-0.5, rf_log_normal_sigma=1.0)
     sched = RectifiedFlowScheduler(num_train_timesteps=1000, shifting=None)
     trainable = [p for p in model.parameters() if p.requires_grad]
-    opt = FusedAdamW(trainable, lr=cfg.learning_rate)
-    reducer = GradAllReduce(trainable)
+    if full:
+        from ltx_amd.zero import Zero2AdamW
+        opt = Zero2AdamW(trainable, lr=cfg.learning_rate, gradient_clipping=1.0)
+        reducer = lambda: None  # noqa: E731  (the reduce-scatter is inside Zero2AdamW.step)
+    else:
+        opt = FusedAdamW(trainable, lr=cfg.learning_rate)
+        reducer = GradAllReduce(trainable)
     torch.manual_seed(20251015 + rank)
 
     N = F_LAT * H_LAT * W_LAT
@@ -296,11 +314,13 @@ def main():
     samples = B_PER_GPU * args.steps * world
     value = samples / elapsed
     fwd, bwd = step_flops_per_sample(N)
+    if full:  # + wgrad of every attention projection, adaln_single, proj_out (2*M*K*N each)
+        bwd += 28 * (2 * N * 2048 * 2048 * 6 + 4 * L_TXT * 2048 * 2048) + 2 * N * 2048 * 128
     step_tflops = (fwd + bwd) * B_PER_GPU * args.steps / (elapsed * 1e12)  # per GPU
     dom_flops = 2.0 * dom_key[0] * dom_key[1] * dom_key[2]
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     line = {
-        "metric": f"LTX-2B LoRA train-step samples/sec (latent-tokens/sec = samples/sec x {N})",
+        "metric": f"LTX-2B {'full (ZeRO-2)' if full else 'LoRA'} train-step samples/sec (latent-tokens/sec = samples/sec x {N})",
         "value": round(value, 4),
         "unit": "samples/s",
         "tokens_per_s": round(value * N, 1),
@@ -313,22 +333,25 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic latents/pose/ref/prompt of the configured shapes; random-init LTX-2B weights",
-        "config": {"workload": "LTX-Video 2B LoRA(r=16, attn2 q/k/v/out) + caption_projection "
+        "config": {"workload": ("LTX-Video 2B train_mode='full' (attn*, scale_shift_table, adaln_single, "
+                                "caption_projection, proj_out; %.0fM params) + ZeRO-2 AdamW, "
+                                % (sum(p.numel() for p in trainable) / 1e6)
+                                if full else "LTX-Video 2B LoRA(r=16, attn2 q/k/v/out) + caption_projection ")
                                + ("train step, 49f 512x512 -> latent 7x16x16 (N=1792), 1xMI355X per rank"
                                   if args.config == "a" else
                                   "train step, 97f 768x768 -> latent 13x24x24 (N=7488), 1xMI355X per rank")
                                + (", per-block gradient checkpointing" if args.grad_ckpt else ""),
                    "model": "LTX-Video-2B (28 layers, D 2048, 32x64 heads)", "global_batch": B_PER_GPU * world,
                    "micro_batch_per_gpu": B_PER_GPU, "seq_len": N, "text_len": L_TXT,
-                   "grad_accum": ACCUM, "parallelism": f"dp{world}"},
+                   "grad_accum": ACCUM, "parallelism": f"zero2-dp{world}" if full else f"dp{world}"},
         "step_tflops_per_gpu": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
         "roofline": {"bound": "mfma", "kernel": f"gemm_nt_kernel_t<GELU> FF-up [{M}x2048].[8192x2048]^T",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": load_traffic() if args.config == "a" else None,
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": load_traffic() if args.config == "a" and not full else None,
                      "launch_ms": round(dom_ms, 4), "launches": len(timer.pairs)},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "a":
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "a" and not full:
         try:
             line["cpu_baseline"] = cpu_baseline()
         except Exception as exc:  # the baseline must never hide the GPU measurement

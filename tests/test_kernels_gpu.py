@@ -386,3 +386,18 @@ def test_gemm_k_extension_lora_fusion():
         # the 3-term split reproduces the f32 rank-r product to ~1e-5
         sa, sw = ops.lora_split(u, "act").float(), ops.lora_split(Bm, "weight", s).float()
         assert rel(sa @ sw.t(), s * (u @ Bm.t())) < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 2048, 14336), (256, 2048, 2048 * 8), (512, 768, 4096)])
+def test_gemm_large_tile_split_k(M, N, K):
+    """Grids under one round of 256x256 tiles with a long K (full-mode weight grads) take the
+    split-K large-tile kernel: store and accumulate epilogues vs fp32, rounded once."""
+    from ltx_amd import ops
+    a, w = g(M, K, seed=31), g(N, K, seed=32, scale=K ** -0.5)
+    ref = a.float() @ w.float().t()
+    out = ops.gemm(a, w)
+    assert ulps_bad(out, ref.to(torch.bfloat16), 2) < 1e-3
+    acc = g(M, N, seed=33)
+    exp = (acc.float() + ref.to(torch.bfloat16).float()).to(torch.bfloat16)
+    ops.gemm(a, w, epilogue="accum", aux0=acc, out=acc)
+    assert ulps_bad(acc, exp, 2) < 1e-3

@@ -701,7 +701,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
 // its own (8 u64 per workgroup); no output value depends on them.
 static __device__ __forceinline__ uint64_t rt_stamp() { return __builtin_amdgcn_s_memrealtime(); }
 
-template <int EPI, int R, int BMT, int DMAW, int STAMP = 0>
+template <int EPI, int R, int BMT, int DMAW, int STAMP = 0, int SPLIT = 0>
 __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   static_assert(BMT == 256 || BMT == 224, "tile height");
   uint64_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
@@ -723,10 +723,20 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   const int wv = __builtin_amdgcn_readfirstlane(wave);
   const int ntm = (p.M + BMT - 1) / BMT, ntn = (p.N + BN2 - 1) / BN2;
   int tm, tn;
-  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
+  // SPLIT (split-K for grids under one round, K2 == 0): block = split * tiles + tile; the slice's
+  // K-tiles [kt0, kt0 + nk) and a raw f32 partial tile into p.ws[split] (splitk_epilogue_kernel)
+  int split = 0, kt0 = 0;
+  if constexpr (SPLIT) {
+    const int tiles = ntm * ntn;
+    split = blockIdx.x / tiles;
+    block_to_tile(blockIdx.x - split * tiles, ntm, ntn, tm, tn);
+    kt0 = (int)((int64_t)split * (p.K / BK) / p.splitk);
+  } else {
+    block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
+  }
   const int m0 = tm * BMT, n0 = tn * BN2;
-  const int nk_main = p.K / BK;
-  const int nk = nk_main + p.K2 / BK;
+  const int nk_main = SPLIT ? (int)((int64_t)(split + 1) * (p.K / BK) / p.splitk) - kt0 : p.K / BK;
+  const int nk = nk_main + (SPLIT ? 0 : p.K2 / BK);
 
   // ---- DMA bookkeeping (see gemm_nt_kernel_l: per-lane 32-bit offsets, scalar bases)
   // DMAW = waves that issue the LDS-DMA (8: all, 4 pieces of each operand each; 4: waves 0-3,
@@ -759,6 +769,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   };
   set_x(nk_main == 0);
   set_w(nk_main == 0);
+  if constexpr (SPLIT) {
+    xb += (int64_t)kt0 * (BK * 2);
+    wb += (int64_t)kt0 * (BK * 2);
+  }
   const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
   auto glds_s = [&](uint32_t voff, const char* sbase, uint32_t lds) {
     unsigned keep;
@@ -875,6 +889,19 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
 #undef LTX_MFMA_T
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if constexpr (STAMP) st2 = rt_stamp();
+  if constexpr (SPLIT) {  // raw f32 partial: lane holds 4 consecutive n of one m (16-B stores)
+    float* part = p.ws + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
+#pragma unroll
+      for (int j = 0; j < MF; ++j) {
+        const int m = m0 + wm * WTM + j * 16 + (lane & 15);
+        if (m < p.M && n < p.N) *(f32x4*)(part + (int64_t)m * p.N + n) = acc[i][j];
+      }
+    }
+    return;
+  }
 
   // epilogue stage 1: bf16(acc + bias) -> LDS image [BMT m][256 n]
   char* cimg = smem;
@@ -1186,6 +1213,34 @@ static int launch(const GemmParams& p, hipStream_t s) {
   }
   // large tile once the grid still fills the chip with 256-row tiles
   const int64_t big_tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + BN2 - 1) / BN2);
+  if constexpr ((EPI == LTX_EPI_STORE || EPI == LTX_EPI_ACCUM) && R == 0) {
+    // under one round of 256x256 tiles with a long K (the full-mode weight gradients: [2048 x 2048]
+    // over K = the token axis): split K over S slices of >= 16 K-tiles so the grid fills the chip
+    if (!g_force_small && g_variant == 0 && p.K2 == 0 && p.M >= BM2 && p.N >= BN2 && big_tiles < 256) {
+      const int nk = p.K / BK;
+      int S = (int)std::min<int64_t>(8, 256 / big_tiles);
+      while (S > 1 && nk / S < 16) --S;
+      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > g_ws_bytes) --S;
+      if (S > 1) {
+        static bool sk_set = false;
+        if (!sk_set) {
+          (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+          sk_set = true;
+        }
+        GemmParams q = p;
+        q.ws = g_ws;
+        q.splitk = S;
+        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>), dim3((unsigned)(big_tiles * S)), dim3(512),
+                           LDS2, s, q);
+        LTX_LAUNCH_CHECK();
+        const int64_t n8 = (int64_t)p.M * (p.N / 8);
+        hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, R>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, q);
+        LTX_LAUNCH_CHECK();
+        return LTX_OK;
+      }
+    }
+  }
   if (!g_force_small && p.M >= BM2 && big_tiles >= 256) {
     static bool attr_set = false;
     if (!attr_set) {
@@ -1289,7 +1344,8 @@ static int launch(const GemmParams& p, hipStream_t s) {
     int S = 1;
     if (tiles < 128 && nk >= 8) {
       S = min(min(8, nk / 4), (256 + tiles - 1) / tiles);
-      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > g_ws_bytes) --S;
+      // (capped at the 32 MiB the small-tile split-K was tuned and validated with)
+      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > std::min<size_t>(g_ws_bytes, 32u << 20)) --S;
     }
     if (S > 1) {
       GemmParams q = p;

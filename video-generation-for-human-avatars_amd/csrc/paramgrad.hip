@@ -63,22 +63,33 @@ __global__ __launch_bounds__(256) void group_colsum_kernel(const bf16_t* __restr
 }
 
 // out_g[d] = bf16(sum_s part[g,s,d]); sum_groups: out[d] = bf16(sum_g out_g[d]) (f32 accumulation);
-// accumulate: out = bf16(out + that)
+// accumulate: out = bf16(out + that). A workgroup owns 32 columns: its 8 waves-rows of 32 lanes
+// (ls = tid / 32) each sum every 8th split, the 8 partial sums meet in LDS (fixed order).
+constexpr int CF_COLS = 32, CF_LANES = 8;
 __global__ __launch_bounds__(256) void colsum_finish_kernel(const float* __restrict__ part, int G, int S, int D,
                                                             int sum_groups, int accumulate, bf16_t* __restrict__ out,
                                                             int64_t ldo) {
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t total = sum_groups ? D : (int64_t)G * D;
-  if (idx >= total) return;
-  const int d = (int)(idx % D);
-  const int g0 = sum_groups ? 0 : (int)(idx / D);
+  __shared__ float red[CF_LANES][CF_COLS];
+  const int cl = threadIdx.x % CF_COLS, ls = threadIdx.x / CF_COLS;
+  const int d = blockIdx.x * CF_COLS + cl;
+  const int g0 = sum_groups ? 0 : (int)blockIdx.y;
   const int g1 = sum_groups ? G : g0 + 1;
   float tot = 0.f;
   for (int g = g0; g < g1; ++g) {
     float s = 0.f;
-    for (int k = 0; k < S; ++k) s += part[((int64_t)g * S + k) * D + d];
-    tot += rbf(s);
+    if (d < D)
+      for (int k = ls; k < S; k += CF_LANES) s += part[((int64_t)g * S + k) * D + d];
+    red[ls][cl] = s;
+    __syncthreads();
+    if (ls == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < CF_LANES; ++j) t += red[j][cl];
+      tot += rbf(t);
+    }
+    __syncthreads();
   }
+  if (ls != 0 || d >= D) return;
   bf16_t* o = out + (sum_groups ? 0 : (int64_t)g0 * ldo) + d;
   const float v = rbf(tot);
   *o = f2bf(accumulate ? bf2f(*o) + v : v);
@@ -128,8 +139,8 @@ int ltx_group_colsum(const void* a, int64_t lda, const void* b, int64_t ldb, con
 int ltx_colsum_finish(const float* partials, int64_t G, int64_t S, int64_t D, int sum_groups, int accumulate,
                       void* out, int64_t ldo, void* stream) {
   LTX_CHECK_ARG(partials && out && G > 0 && S > 0 && D > 0, "colsum_finish: bad args");
-  const int64_t total = sum_groups ? D : G * D;
-  hipLaunchKernelGGL(colsum_finish_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  const dim3 grid((unsigned)((D + CF_COLS - 1) / CF_COLS), (unsigned)(sum_groups ? 1 : G));
+  hipLaunchKernelGGL(colsum_finish_kernel, grid, dim3(256), 0, (hipStream_t)stream,
                      partials, (int)G, (int)S, (int)D, sum_groups, accumulate, (bf16_t*)out, ldo);
   LTX_LAUNCH_CHECK();
   return LTX_OK;

@@ -317,7 +317,7 @@ def set_launch_timer(timer):
 
 
 _GEMM_WS = {}
-GEMM_WS_BYTES = 32 << 20
+GEMM_WS_BYTES = 128 << 20  # split-K partials: S x M x N f32 (S=4 at 2048 x 2048 = 64 MiB)
 
 
 def _gemm_workspace(device):
@@ -460,8 +460,11 @@ def transpose(x, out=None):
 
 
 def colsum(x):
+    """bf16 [N]: column sums of x [M, N] (f32 accumulation, one rounding)."""
     M, N = x.shape
     out = torch.empty(N, dtype=BF16, device=x.device)
+    if N % 8 == 0 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and M >= 64:
+        return colsum_into(out, x, accumulate=False)  # split over rows: fills the chip
     call("ltx_colsum_bf16", _p(x), _rows(x, "x"), _p(out), M, N, _s())
     return out
 
