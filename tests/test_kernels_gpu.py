@@ -304,6 +304,12 @@ def test_timestep_silu_transpose_colsum():
     assert ulps_bad(ops.silu(x), F.silu(x), 1) < 1e-3
     x = g(300, 136, seed=4)
     assert torch.equal(ops.transpose(x), x.t().contiguous())
+    # 16-B vector path: ragged tiles, a strided source view and a padded destination (_tpad)
+    x = g(1000, 136, seed=5)
+    assert torch.equal(ops.transpose(x), x.t().contiguous())
+    big = g(1000, 3 * 136, seed=6)
+    xt = ops._tpad(big[:, 136:272], 1024)
+    assert torch.equal(xt[:, :1000], big[:, 136:272].t()) and float(xt[:, 1000:].abs().max()) == 0
     cs = ops.colsum(x)
     assert rel(cs, x.float().sum(0)) < 5e-3
 

@@ -44,9 +44,49 @@ __global__ __launch_bounds__(256) void transpose_kernel(const bf16_t* __restrict
   }
 }
 
+// 16-B vector form (R, C, strides % 8 == 0, 16-B aligned bases): a lane loads 8 consecutive
+// columns of one row, and stores 8 consecutive output elements (8 tile rows of one column), so
+// both HBM sides move 128-B row segments per 8 lanes. LDS rows padded to 66 elements (odd dwords).
+__global__ __launch_bounds__(256) void transpose_v8_kernel(const bf16_t* __restrict__ in, int64_t ld_in,
+                                                           int64_t bstride_in, bf16_t* __restrict__ out,
+                                                           int64_t ld_out, int64_t bstride_out, int R, int C) {
+  __shared__ bf16_t tile[TT][TT + 2];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * TT, c0 = blockIdx.x * TT;
+  const bf16_t* src = in + (int64_t)b * bstride_in;
+  bf16_t* dst = out + (int64_t)b * bstride_out;
+  const int ch = threadIdx.x & 7, rr = threadIdx.x >> 3;  // 8-element chunk, row (0..31)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = rr + 32 * h, gr = r0 + r, gc = c0 + ch * 8;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (gr < R && gc < C) v = *(const u32x4*)(src + (int64_t)gr * ld_in + gc);
+    uint32_t* t = (uint32_t*)&tile[r][ch * 8];  // 4-B aligned: row stride 132 B, chunk 16 B
+    t[0] = v[0]; t[1] = v[1]; t[2] = v[2]; t[3] = v[3];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = rr + 32 * h, gc = c0 + c, gr = r0 + ch * 8;  // output row gc, columns gr..gr+7
+    if (gc >= C || gr >= R) continue;
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = (uint32_t)tile[ch * 8 + 2 * k][c] | ((uint32_t)tile[ch * 8 + 2 * k + 1][c] << 16);
+    *(u32x4*)(dst + (int64_t)gc * ld_out + gr) = o;
+  }
+}
+
 static int launch_transpose(const void* in, int64_t ld_in, int64_t bs_in, void* out, int64_t ld_out,
                             int64_t bs_out, int64_t R, int64_t C, int64_t B, hipStream_t s) {
   dim3 grid((unsigned)((C + TT - 1) / TT), (unsigned)((R + TT - 1) / TT), (unsigned)B);
+  if (R % 8 == 0 && C % 8 == 0 && ld_in % 8 == 0 && ld_out % 8 == 0 && bs_in % 8 == 0 && bs_out % 8 == 0 &&
+      ((uintptr_t)in % 16) == 0 && ((uintptr_t)out % 16) == 0) {
+    hipLaunchKernelGGL(transpose_v8_kernel, grid, dim3(256), 0, s, (const bf16_t*)in, ld_in, bs_in, (bf16_t*)out,
+                       ld_out, bs_out, (int)R, (int)C);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
   hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, s, (const bf16_t*)in, ld_in, bs_in,
                      (bf16_t*)out, ld_out, bs_out, (int)R, (int)C);
   LTX_LAUNCH_CHECK();

@@ -1221,7 +1221,7 @@ static int launch(const GemmParams& p, hipStream_t s) {
       int S = (int)std::min<int64_t>(8, 256 / big_tiles);
       while (S > 1 && nk / S < 16) --S;
       while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > g_ws_bytes) --S;
-      if (S > 1) {
+      if (S > 1 && big_tiles * S >= 128) {  // else the 128x128 kernel's split fills the chip better
         static bool sk_set = false;
         if (!sk_set) {
           (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>,

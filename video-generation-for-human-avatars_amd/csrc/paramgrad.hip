@@ -63,9 +63,9 @@ __global__ __launch_bounds__(256) void group_colsum_kernel(const bf16_t* __restr
 }
 
 // out_g[d] = bf16(sum_s part[g,s,d]); sum_groups: out[d] = bf16(sum_g out_g[d]) (f32 accumulation);
-// accumulate: out = bf16(out + that). A workgroup owns 32 columns: its 8 waves-rows of 32 lanes
-// (ls = tid / 32) each sum every 8th split, the 8 partial sums meet in LDS (fixed order).
-constexpr int CF_COLS = 32, CF_LANES = 8;
+// accumulate: out = bf16(out + that). A workgroup owns 16 columns: its 16 rows of 16 lanes
+// (ls = tid / 16) each sum every 16th split, the 16 partial sums meet in LDS (fixed order).
+constexpr int CF_COLS = 16, CF_LANES = 16;
 __global__ __launch_bounds__(256) void colsum_finish_kernel(const float* __restrict__ part, int G, int S, int D,
                                                             int sum_groups, int accumulate, bf16_t* __restrict__ out,
                                                             int64_t ldo) {
