@@ -401,9 +401,38 @@ def test_gemm_large_tile_split_k(M, N, K):
     from ltx_amd import ops
     a, w = g(M, K, seed=31), g(N, K, seed=32, scale=K ** -0.5)
     ref = a.float() @ w.float().t()
-    out = ops.gemm(a, w)
+    ops._BLASLT[0] = False  # plain stores of this size would go to hipBLASLt
+    try:
+        out = ops.gemm(a, w)
+    finally:
+        ops._BLASLT[0] = True
     assert ulps_bad(out, ref.to(torch.bfloat16), 2) < 1e-3
     acc = g(M, N, seed=33)
     exp = (acc.float() + ref.to(torch.bfloat16).float()).to(torch.bfloat16)
     ops.gemm(a, w, epilogue="accum", aux0=acc, out=acc)
     assert ulps_bad(acc, exp, 2) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(14336, 2048, 2048), (1000, 136, 264)])
+def test_gemm_blaslt_store_bias_and_wgrad(M, N, K):
+    """hipBLASLt (ltx_gemm_blaslt_bf16): plain store + bias, and the weight gradient read from
+    token-major operands (no transposes), fresh and accumulated."""
+    from ltx_amd import ops
+    a, w, b = g(M, K, seed=41), g(N, K, seed=42, scale=K ** -0.5), g(N, seed=43)
+    ref = (a.float() @ w.float().t() + b.float()).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.call("ltx_gemm_blaslt_bf16", 0, 0, ops._p(a), K, ops._p(w), K, ops._p(out), N, M, N, K,
+             ops._p(b), 0, ops._s())
+    assert ulps_bad(out, ref, 2) < 1e-3
+    dy = g(M, N, seed=44, scale=M ** -0.5)
+    wg = ops.wgrad(dy, a)
+    refw = dy.float().t() @ a.float()
+    assert ulps_bad(wg, refw.to(torch.bfloat16), 2) < 1e-3
+    acc = g(N, K, seed=45)
+    exp = acc.float() + refw
+    ops.wgrad_into(acc, dy, a)
+    assert ulps_bad(acc, exp.to(torch.bfloat16), 2) < 1e-3
+    # strided column slices (the fused q/k/v gradient rows of dQKV)
+    big = g(M, 3 * N, seed=46, scale=M ** -0.5)
+    wg2 = ops.wgrad(big[:, N:2 * N], a)
+    assert ulps_bad(wg2, (big[:, N:2 * N].float().t() @ a.float()).to(torch.bfloat16), 2) < 1e-3

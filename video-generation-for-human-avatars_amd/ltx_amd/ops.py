@@ -6,6 +6,7 @@ stride, any row stride that is a multiple of 8 elements), so fused buffers such 
 [M, 6144] QKV projection are consumed in place without copies.
 """
 import ctypes
+import os
 
 import torch
 
@@ -331,6 +332,12 @@ def _gemm_workspace(device):
     return _GEMM_WS[key]
 
 
+# plain-store GEMMs of at least this many MACs go to hipBLASLt (LTX_GEMM_BLASLT=0: hand-written
+# kernel for everything, for A/B); the fused-epilogue products always run the HIP kernels
+BLASLT_MIN_MNK = 1 << 30
+_BLASLT = [os.environ.get("LTX_GEMM_BLASLT", "1") != "0"]
+
+
 def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2=None,
          alpha=1.0, rank=0, rows_per_batch=0, ext=None):
     """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias) [+ a2 . w2^T]); see LTX_EPI_* in ltx_hip.h.
@@ -352,10 +359,17 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
         ev0.record()
     a2, w2 = ext if ext is not None else (None, None)
     K2 = a2.shape[1] if a2 is not None else 0
-    call("ltx_gemm_bf16_nt_ext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
-         _rows(a2, "a2") if a2 is not None else 0, _p(w2), _rows(w2, "w2") if w2 is not None else 0,
-         K2, _p(out), _rows(out, "out"), M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1),
-         ld1, _p(aux2), ld2, float(alpha), rank, rows_per_batch, _s())
+    if (epilogue == "store" and a2 is None and aux0 is None and aux1 is None and aux2 is None
+            and _BLASLT[0] and M * N * K >= BLASLT_MIN_MNK):
+        # no fused epilogue: the library GEMM (hipBLASLt, ltx_gemm_blaslt_bf16)
+        call("ltx_gemm_blaslt_bf16", 0, 0, _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(out),
+             _rows(out, "out"), M, N, K, _p(bias), 0, _s())
+    else:
+        call("ltx_gemm_bf16_nt_ext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
+             _rows(a2, "a2") if a2 is not None else 0, _p(w2),
+             _rows(w2, "w2") if w2 is not None else 0, K2, _p(out), _rows(out, "out"), M, N, K,
+             EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1), ld1, _p(aux2), ld2, float(alpha),
+             rank, rows_per_batch, _s())
     if timed:
         ev1.record()
         _timer.pairs.append((ev0, ev1))
@@ -633,12 +647,24 @@ def _tpad(x, npad):
     return buf
 
 
-def wgrad_into(grad, dy, x, dyT=None):
-    """grad [N, K] (bf16) += bf16(dy^T . x) over the M token rows (dy [M, N], x [M, K]): the
-    weight gradient of an nn.Linear, through the NT GEMM on transposed operands (the token axis
-    becomes the GEMM K, zero-padded to a multiple of 64). dyT: a precomputed _tpad(dy)."""
-    M = dy.shape[0]
-    npad = (M + 63) // 64 * 64
-    a = dyT if dyT is not None else _tpad(dy, npad)
-    w = _tpad(x, npad)
-    gemm(a, w, epilogue="accum", aux0=grad, out=grad)
+def wgrad_into(grad, dy, x, accumulate=True):
+    """grad [N, K] (bf16) (+)= dy^T . x over the M token rows (dy [M, N], x [M, K]): the weight
+    gradient of an nn.Linear. hipBLASLt reads both operands token-major (K-major), so there is no
+    transpose pass; f32 accumulation, rounded once into grad."""
+    M, N = dy.shape
+    M2, K = x.shape
+    if M != M2 or tuple(grad.shape) != (N, K):
+        raise ValueError(f"wgrad: shapes dy {tuple(dy.shape)} x {tuple(x.shape)} grad {tuple(grad.shape)}")
+    _need(dy, BF16, "wgrad dy")
+    _need(x, BF16, "wgrad x")
+    _need(grad, BF16, "wgrad grad")
+    call("ltx_gemm_blaslt_bf16", 1, 1, _p(dy), _rows(dy, "dy"), _p(x), _rows(x, "x"), _p(grad),
+         _rows(grad, "grad"), N, K, M, None, 1 if accumulate else 0, _s())
+    return grad
+
+
+def wgrad(dy, x):
+    """bf16 [N, K] = dy^T . x (a fresh weight gradient)."""
+    out = torch.empty(dy.shape[1], x.shape[1], dtype=BF16, device=dy.device)
+    return wgrad_into(out, dy, x, accumulate=False)
+

@@ -577,14 +577,9 @@ class _BlockFn(torch.autograd.Function):
         if full:  # attn1 q/k norm weights, to_q / to_k / to_v (fused dQKV^T . x1)
             ops.qk_norm_wgrad_into(dq1, qkv[:, :D], rq1, _pgrad(a1.q_norm.weight), dk1,
                                    qkv[:, D:2 * D], rk1, _pgrad(a1.k_norm.weight), rope=sh.rope)
-            npad = (M + 63) // 64 * 64
-            dqkvT = ops._tpad(dqkv, npad)
-            x1T = ops._tpad(x1, npad)
             for i, lin in enumerate((a1.to_q, a1.to_k, a1.to_v)):
-                g = _pgrad(lin.weight)
-                ops.gemm(dqkvT[i * D:(i + 1) * D], x1T, epilogue="accum", aux0=g, out=g)
+                ops.wgrad_into(_pgrad(lin.weight), dqkv[:, i * D:(i + 1) * D], x1)
                 ops.colsum_into(_pgrad(lin.bias), dqkv[:, i * D:(i + 1) * D])
-            del dqkvT, x1T
         del dq1, dk1
         dh = None
         if ctx.needs_input_grad[4] or full:  # (blk, sh, keep, skip, h, ...)
@@ -615,32 +610,17 @@ class _CaptionProjFn(torch.autograd.Function):
     def backward(ctx, dout):
         enc, pre, act, w2 = ctx.saved_tensors
         dout = dout.contiguous()
-        n = enc.shape[0]
-        npad = (n + 63) // 64 * 64  # GEMM K must be a multiple of 64: zero-pad the token axis
-
-        def tpad(x):
-            buf = torch.zeros(x.shape[1], npad, dtype=torch.bfloat16, device=x.device)
-            ops.transpose(x, out=buf[:, :n])
-            return buf
-
-        doT = tpad(dout)
-        dw2 = ops.gemm(doT, tpad(act))
+        dw2 = ops.wgrad(dout, act)  # token-major operands, no transpose pass
         db2 = ops.colsum(dout)
         dpre = ops.gemm(dout, ops.transpose(w2), epilogue="gelu_bwd", aux0=pre)
-        dpT = tpad(dpre)
-        dw1 = ops.gemm(dpT, tpad(enc))
+        dw1 = ops.wgrad(dpre, enc)
         db1 = ops.colsum(dpre)
         return None, dw1, db1, dw2, db2
 
 
-def _tpad_t(x):
-    """x [R, C] -> x^T zero-padded to [C, round_up(R, 64)] (GEMM K % 64 == 0)."""
-    return ops._tpad(x, (x.shape[0] + 63) // 64 * 64)
-
-
 def _lin_wgrad(dy, x):
     """nn.Linear weight grad dy^T . x over the rows (bf16, f32 accumulation)."""
-    return ops.gemm(_tpad_t(dy), _tpad_t(x))
+    return ops.wgrad(dy.contiguous(), x.contiguous())
 
 
 class _AdaModFn(torch.autograd.Function):
