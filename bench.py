@@ -199,7 +199,7 @@ def infer_main(args):
             lat = denoise_step(model, sch, lat, sch.timesteps[i], **kw)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-    fwd, _ = step_flops_per_sample(N)
+    fwd, _ = step_flops_per_sample(N, r=LORA_RANK)
     tflops = fwd * 3 * B * args.steps / (elapsed * 1e12)
     print(json.dumps({
         "metric": "LTX-2B inference denoising steps/sec (CFG+STG: transformer batch 3 x videos)",
@@ -228,11 +228,14 @@ def main():
                          "BASELINE configs[3], long-sequence stress)")
     ap.add_argument("--batch", type=int, default=None, help="micro-batch per GPU (default 8)")
     ap.add_argument("--grad-ckpt", action="store_true", help="per-block gradient checkpointing")
+    ap.add_argument("--lora-rank", type=int, default=16,
+                    help="LoRA rank (alpha = rank): 16 is the BASELINE config, 32 the yaml default")
     ap.add_argument("--mode", choices=["lora", "full"], default="lora",
                     help="full: train_mode='full' + ZeRO-2 AdamW (BASELINE configs[4], "
                          "ds_config_zero2.json: grad accumulation 3, clip 1.0)")
     args = ap.parse_args()
-    global F_LAT, H_LAT, W_LAT, B_PER_GPU, ACCUM
+    global F_LAT, H_LAT, W_LAT, B_PER_GPU, ACCUM, LORA_RANK
+    LORA_RANK = args.lora_rank
     if args.config == "x":
         F_LAT, H_LAT, W_LAT = 13, 24, 24
     if args.batch:
@@ -313,7 +316,7 @@ def main():
 
     samples = B_PER_GPU * args.steps * world
     value = samples / elapsed
-    fwd, bwd = step_flops_per_sample(N)
+    fwd, bwd = step_flops_per_sample(N, r=LORA_RANK)
     if full:  # + wgrad of every attention projection, adaln_single, proj_out (2*M*K*N each)
         bwd += 28 * (2 * N * 2048 * 2048 * 6 + 4 * L_TXT * 2048 * 2048) + 2 * N * 2048 * 128
     step_tflops = (fwd + bwd) * B_PER_GPU * args.steps / (elapsed * 1e12)  # per GPU
@@ -333,10 +336,11 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic latents/pose/ref/prompt of the configured shapes; random-init LTX-2B weights",
-        "config": {"workload": ("LTX-Video 2B train_mode='full' (attn*, scale_shift_table, adaln_single, "
+        "config": {"lora_rank": None if full else LORA_RANK,
+                   "workload": ("LTX-Video 2B train_mode='full' (attn*, scale_shift_table, adaln_single, "
                                 "caption_projection, proj_out; %.0fM params) + ZeRO-2 AdamW, "
                                 % (sum(p.numel() for p in trainable) / 1e6)
-                                if full else "LTX-Video 2B LoRA(r=16, attn2 q/k/v/out) + caption_projection ")
+                                if full else f"LTX-Video 2B LoRA(r={LORA_RANK}, attn2 q/k/v/out) + caption_projection ")
                                + ("train step, 49f 512x512 -> latent 7x16x16 (N=1792), 1xMI355X per rank"
                                   if args.config == "a" else
                                   "train step, 97f 768x768 -> latent 13x24x24 (N=7488), 1xMI355X per rank")

@@ -234,8 +234,10 @@ int ltx_colsum_bf16(const void* x, int64_t ldx, void* out, int64_t M, int64_t N,
 int ltx_batch_sum_bf16(const void* x, int64_t ldx, int64_t B, int64_t rows, int64_t cols,
                        void* out, int64_t ldo, void* stream);
 /* F.mse_loss(out, v) (mean) + its backward seed and std(v) (training.py:159-166):
- * stats[0] = sum (o-v)^2 in f32 over bf16-rounded squares, stats[1] = sum v, stats[2] = sum v^2
- * (f32 atomics into a zeroed 4-float buffer); dout = bf16(bf16(bf16(o-v) * 2/n) * gscale). */
+ * stats[0] = sum (o-v)^2 in f32 over bf16-rounded squares, stats[1] = sum v, stats[2] = sum v^2,
+ * stats[3] = 0; stats is f32[4 + 768]: the tail holds 256 per-block partials of each sum, added
+ * in a fixed order (deterministic). out / v / dout 16-B aligned.
+ * dout = bf16(bf16(bf16(o-v) * 2/n) * gscale). */
 int ltx_mse_fwd_bwd(const void* out, const void* v, void* dout, float* stats, int64_t n,
                     float grad_scale, void* stream);
 /* torch.optim.AdamW single-tensor step (training.py:270-271): f32 or bf16 param/state.

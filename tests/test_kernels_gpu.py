@@ -350,6 +350,16 @@ def test_mse_and_adamw():
     assert ulps_bad(dout, oo.grad, 1) < 1e-3
     std = torch.sqrt((stats[2] - stats[1] ** 2 / n) / (n - 1))
     assert abs(float(std) - float(v.float().std())) < 1e-3
+    # deterministic (fixed-order partials, no atomics), ragged size with a scalar tail
+    o2, v2 = g(3, 1001, 7, seed=4), g(3, 1001, 7, seed=5)
+    s_a, d_a = ops.mse_fwd_bwd(o2, v2)
+    s_b, d_b = ops.mse_fwd_bwd(o2, v2)
+    assert torch.equal(s_a, s_b) and torch.equal(d_a, d_b)
+    oo2 = o2.clone().requires_grad_(True)
+    l2 = F.mse_loss(oo2, v2)
+    l2.backward()
+    assert abs(float(s_a[0]) / o2.numel() - float(l2)) < 1e-2 * float(l2)
+    assert ulps_bad(d_a, oo2.grad, 1) < 1e-3
     for dtype in (torch.float32, torch.bfloat16):
         p0 = g(4096, dtype=dtype, seed=3)
         grads = [g(4096, dtype=dtype, seed=10 + i) for i in range(3)]

@@ -1,5 +1,5 @@
 """Training around the step (SURVEY 8c-5 loss curve, 8f row 3 formats), on the MI355X:
-  * loss curve: 10 optimizer steps of the tiny model -- train_step + FusedAdamW through the HIP
+  * loss curve (SURVEY 8c-5, K = 50): 50 optimizer steps of the tiny model -- train_step + FusedAdamW through the HIP
     library vs the pinned oracle's train_step + torch.optim.AdamW on the same device, same
     per-step t / noise streams; per-step loss within bf16 drift;
   * train_loop over precomputed .pt latents on disk (LatentPairDataset + LatentLoader) writes the
@@ -49,7 +49,7 @@ def test_loss_curve_matches_oracle():
     B, C = batch["latents"].shape[:2]
     N = batch["latents"][0, 0].numel()
     ours, refs = [], []
-    for step in range(10):
+    for step in range(50):
         t = torch.rand(B, generator=g, device=DEV) * 0.9 + 0.05
         noise = torch.randn(B, N, C, generator=g, device=DEV).bfloat16()
         loss, _, _, _ = train_step(model, batch, RectifiedFlowScheduler(), model.patchifier, tc,

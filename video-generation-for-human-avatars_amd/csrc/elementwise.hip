@@ -291,11 +291,32 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 
 // F.mse_loss forward statistics + backward seed (training.py:159-166; ATen mse kernel rounds the
 // bf16 difference and its square; mse_loss_backward = sub, * (2/n), * grad, each rounded).
+constexpr int MSE_BLOCKS = 256;  // fixed grid: the partials live in stats[4 .. 4 + 3 * MSE_BLOCKS)
 __global__ __launch_bounds__(256) void mse_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ v,
                                                   bf16_t* __restrict__ dout, float* __restrict__ stats,
                                                   int64_t n, float norm, float gscale) {
   float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t n8 = n / 8;  // 16-B vectors, then a scalar tail
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    const u32x4 ow = *(const u32x4*)(o + 8 * i), vw = *(const u32x4*)(v + 8 * i);
+    u32x4 dw;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      float d2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float ov = bf2f((bf16_t)(ow[h] >> (16 * e))), vv = bf2f((bf16_t)(vw[h] >> (16 * e)));
+        const float diff = rbf(ov - vv);
+        s0 += rbf(diff * diff);
+        s1 += vv;
+        s2 += vv * vv;
+        d2[e] = rbf(diff * norm) * gscale;
+      }
+      dw[h] = pack2(d2[0], d2[1]);
+    }
+    if (dout) *(u32x4*)(dout + 8 * i) = dw;
+  }
+  for (int64_t i = 8 * n8 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float ov = bf2f(o[i]), vv = bf2f(v[i]);
     const float diff = rbf(ov - vv);
     s0 += rbf(diff * diff);
@@ -306,11 +327,29 @@ __global__ __launch_bounds__(256) void mse_kernel(const bf16_t* __restrict__ o, 
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
   s2 = wave_sum(s2);
+  __shared__ float red[3][4];
+  const int w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
-    atomicAdd(stats + 0, s0);
-    atomicAdd(stats + 1, s1);
-    atomicAdd(stats + 2, s2);
+    red[0][w] = s0;
+    red[1][w] = s1;
+    red[2][w] = s2;
   }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    const int c = threadIdx.x;
+    stats[4 + c * MSE_BLOCKS + blockIdx.x] = red[c][0] + red[c][1] + red[c][2] + red[c][3];
+  }
+}
+
+// fixed-order sum of the per-block partials (deterministic, no atomics)
+__global__ __launch_bounds__(256) void mse_finish_kernel(float* __restrict__ stats) {
+  const int c = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (c >= 3) return;
+  float s = 0.f;
+  for (int b = lane; b < MSE_BLOCKS; b += 64) s += stats[4 + c * MSE_BLOCKS + b];
+  s = wave_sum(s);
+  if (lane == 0) stats[c] = s;
+  if (c == 0 && lane == 0) stats[3] = 0.f;
 }
 
 // torch.optim.AdamW, foreach implementation order (weight decay, lerp m, v*b2 + (1-b2) g g,
@@ -503,11 +542,11 @@ int ltx_batch_sum_bf16(const void* x, int64_t ldx, int64_t B, int64_t rows, int6
 int ltx_mse_fwd_bwd(const void* out, const void* v, void* dout, float* stats, int64_t n, float grad_scale,
                     void* stream) {
   LTX_CHECK_ARG(out && v && stats && n > 0, "mse: bad args");
-  hipError_t e = hipMemsetAsync(stats, 0, 4 * sizeof(float), (hipStream_t)stream);
-  if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+  LTX_CHECK_ARG(((uintptr_t)out | (uintptr_t)v | (uintptr_t)dout) % 16 == 0, "mse: operands must be 16-B aligned");
   const float norm = (float)(2.0 / (double)n);
-  hipLaunchKernelGGL(mse_kernel, dim3(grid_for(n, 256, 2048)), dim3(256), 0, (hipStream_t)stream,
-                     (const bf16_t*)out, (const bf16_t*)v, (bf16_t*)dout, stats, n, norm, grad_scale);
+  hipLaunchKernelGGL(mse_kernel, dim3(MSE_BLOCKS), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)out,
+                     (const bf16_t*)v, (bf16_t*)dout, stats, n, norm, grad_scale);
+  hipLaunchKernelGGL(mse_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, stats);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

@@ -487,11 +487,11 @@ def mse_fwd_bwd(out, v, grad_scale=1.0, want_grad=True):
     """Returns (stats[4] f32 device: sum sq-err, sum v, sum v^2, -, dout bf16 or None)."""
     n = out.numel()
     out, v = out.contiguous(), v.contiguous()
-    stats = torch.empty(4, dtype=F32, device=out.device)
+    stats = torch.empty(4 + 3 * 256, dtype=F32, device=out.device)  # + per-block partials
     dout = torch.empty(out.shape, dtype=BF16, device=out.device) if want_grad else None
     call("ltx_mse_fwd_bwd", _p(out), _p(v), _p(dout), _p(stats), n,
          float(grad_scale), _s())
-    return stats, dout
+    return stats[:4], dout
 
 
 def adamw_step(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step):
