@@ -23,6 +23,8 @@
 // dK^T += Q^T.dS). Recomputing S/dP in both costs two extra products per tile but removes the
 // f32 atomics a fused kernel needs for dQ (which on MI355X would be bound by the ~1.3 TB/s
 // atomic rate at these sizes).
+#include <cstdlib>
+
 #include "common.h"
 #include "ltx_hip.h"
 
@@ -120,6 +122,7 @@ struct AttnParams {
   int B, H, Nq, Nk;
   int kvb;                             // rows between batches of K, V and key_bias (Nk, or 0: shared)
   float scale;
+  int xcd_order;                       // 1: XCD-aware block order (xcd_block), 0: hardware order
 };
 
 // per-key additive term in log2 units for keys key0..key0+63 -> LDS
@@ -153,6 +156,28 @@ __device__ __forceinline__ float xor32_sum(float v) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// XCD-aware block order: the hardware deals consecutive workgroups round-robin over the 8 XCDs,
+// which would spread the blocks of one (batch, head) -- all reading the same K/V (or Q/dO) --
+// over 8 L2s and fetch those operands 8 times from beyond L2 (~1 GB per launch measured at
+// config A). Bijective remap: XCD x takes a contiguous range of the (x fastest, head, batch)
+// block order.
+__device__ __forceinline__ void xcd_block(int xcd_order, int& bx, int& by, int& bz) {
+  if (!xcd_order) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    bz = blockIdx.z;
+    return;
+  }
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int total = gx * gy * gridDim.z;
+  const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  const int q = total / 8, r = total % 8, xcd = L % 8, idx = L / 8;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  bx = wg % gx;
+  by = (wg / gx) % gy;
+  bz = wg / (gx * gy);
+}
+
 template <int HD, int MODE, bool BIAS>
 __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams p) {
   constexpr int KT = 64;                 // keys per tile
@@ -165,8 +190,9 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
   char* vtile = smem + TILE;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int q0 = bx * 128 + wave * 32;
   const int qi = q0 + (lane & 31);
   const int qc = min(qi, p.Nq - 1);
   const float c2 = p.scale * LOG2E;
@@ -397,8 +423,9 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   char* otile = smem + TILE;  // dO
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int hh = blockIdx.y, b = blockIdx.z;
-  const int key = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int key = bx * 128 + wave * 32 + (lane & 31);
   const int kc = min(key, p.Nk - 1);
   const float c2 = p.scale * LOG2E;
   float kbias = 0.f;
@@ -551,8 +578,18 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const AttnParams p, flo
 
 static inline bool needs_bias(const AttnParams& p) { return p.key_bias != nullptr || (p.Nk % 64) != 0; }
 
+static int xcd_order_flag() {  // LTX_ATTN_XCD=0: hardware block order (A/B measurement switch)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("LTX_ATTN_XCD");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v;
+}
+
 template <int HD>
-static int launch_fwd(const AttnParams& p, hipStream_t s) {
+static int launch_fwd(AttnParams p, hipStream_t s) {
+  p.xcd_order = xcd_order_flag();
   dim3 grid((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   if (needs_bias(p))
     hipLaunchKernelGGL((attn_q_kernel<HD, 0, true>), grid, dim3(ATT_THREADS), 0, s, p);
@@ -568,6 +605,7 @@ static int launch_bwd(AttnParams p, float* delta, hipStream_t s) {
                      delta);
   LTX_LAUNCH_CHECK();
   p.delta = delta;
+  p.xcd_order = xcd_order_flag();
   dim3 gq((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   dim3 gk((unsigned)((p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   if (needs_bias(p)) {
