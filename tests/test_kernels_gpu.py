@@ -69,7 +69,8 @@ def test_gemm_strided_views_and_no_bias():
     assert float(outbuf[:, :N].abs().max()) == 0.0
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 256, 256), (256, 512, 2048)])  # one pass / split-K
+@pytest.mark.parametrize("M,N,K", [(512, 256, 256), (256, 512, 2048),  # one pass / split-K
+                                   (5376, 2048, 512)])  # 192 224-row tiles: large tile under one round
 def test_gemm_epilogues(M, N, K):
     from ltx_amd import ops
     r, B = 16, 4

@@ -206,6 +206,37 @@ __global__ void ada_kernel(const bf16_t* __restrict__ sst, const bf16_t* __restr
   }
 }
 
+// 16-B form: a block per (b, j) row, 8 columns per lane (D, ld_tmod, ld_j % 8, 16-B aligned).
+// The per-token AdaLN of the inference step makes B = batch x tokens: ~400 MB moved per block.
+__global__ __launch_bounds__(256) void ada_v8_kernel(const bf16_t* __restrict__ sst, const bf16_t* __restrict__ tmod,
+                                                     int64_t ld_tmod, int64_t ld_j, bf16_t* __restrict__ out,
+                                                     bf16_t* __restrict__ onep, int B, int P, int D,
+                                                     unsigned scale_mask) {
+  const int64_t rows = (int64_t)B * P;
+  const int D8 = D / 8;
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int j = (int)(row % P);
+    const int64_t b = row / P;
+    const bf16_t* tp = tmod + b * ld_tmod + (int64_t)j * ld_j;
+    const bf16_t* sp = sst + (int64_t)j * D;
+    bf16_t* op = out + row * D;
+    const bool sc = onep && ((scale_mask >> j) & 1u);
+    for (int c = threadIdx.x; c < D8; c += 256) {
+      const u32x4 a = *(const u32x4*)(sp + 8 * c), t = *(const u32x4*)(tp + 8 * c);
+      u32x4 o, q;
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const float s0 = rbf(bf2f((bf16_t)(a[h] & 0xffff)) + bf2f((bf16_t)(t[h] & 0xffff)));
+        const float s1 = rbf(bf2f((bf16_t)(a[h] >> 16)) + bf2f((bf16_t)(t[h] >> 16)));
+        o[h] = pack2(s0, s1);
+        q[h] = pack2(1.0f + s0, 1.0f + s1);
+      }
+      *(u32x4*)(op + 8 * c) = o;
+      if (sc) *(u32x4*)(onep + row * D + 8 * c) = q;
+    }
+  }
+}
+
 // diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), f32 math
 // (embeddings.py:10-50 of the reference carries the same formula), preceded by
 // `timestep_scale_multiplier * timestep` (transformer3d.py:473-474), result cast to bf16.
@@ -481,6 +512,15 @@ int ltx_ada_modulation(const void* sst, const void* tmod, int64_t ld_tmod, int64
                        int64_t B, int64_t P, int64_t D, int64_t scale_mask, void* stream) {
   LTX_CHECK_ARG(sst && tmod && out && B > 0 && P > 0 && P <= 32 && D > 0, "ada_modulation: bad args");
   const int64_t total = B * P * D;
+  if (D % 8 == 0 && ld_tmod % 8 == 0 && ld_j % 8 == 0 &&
+      (((uintptr_t)sst | (uintptr_t)tmod | (uintptr_t)out | (uintptr_t)onep_out) % 16) == 0) {
+    const int64_t rows = B * P;
+    hipLaunchKernelGGL(ada_v8_kernel, dim3((unsigned)(rows < 16384 ? rows : 16384)), dim3(256), 0,
+                       (hipStream_t)stream, (const bf16_t*)sst, (const bf16_t*)tmod, ld_tmod, ld_j, (bf16_t*)out,
+                       (bf16_t*)onep_out, (int)B, (int)P, (int)D, (unsigned)scale_mask);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
   hipLaunchKernelGGL(ada_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)sst,
                      (const bf16_t*)tmod, ld_tmod, ld_j, (bf16_t*)out, (bf16_t*)onep_out, (int)B, (int)P, (int)D,
                      (unsigned)scale_mask);

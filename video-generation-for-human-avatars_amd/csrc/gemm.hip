@@ -1219,8 +1219,11 @@ static int launch(const GemmParams& p, hipStream_t s) {
     const char* e = getenv("LTX_GEMM_SMALL");
     g_force_small = (e && e[0] == '1') ? 1 : 0;
   }
-  // large tile once the grid still fills the chip with 256-row tiles
+  // large tile once the grid still fills the chip with 256-row tiles, or fills at least 160 CUs
+  // with 224-row tiles (one round at >= 62 %: the inference shapes, M = 3 x 1792 = 5376 -> 192
+  // tiles, run 1.3x faster there than as 672 128x128 tiles)
   const int64_t big_tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + BN2 - 1) / BN2);
+  const int64_t tiles224 = (int64_t)((p.M + 223) / 224) * ((p.N + BN2 - 1) / BN2);
   if constexpr ((EPI == LTX_EPI_STORE || EPI == LTX_EPI_ACCUM) && R == 0) {
     // under one round of 256x256 tiles with a long K (the full-mode weight gradients: [2048 x 2048]
     // over K = the token axis): split K over S slices of >= 16 K-tiles so the grid fills the chip
@@ -1249,7 +1252,7 @@ static int launch(const GemmParams& p, hipStream_t s) {
       }
     }
   }
-  if (!g_force_small && p.M >= BM2 && big_tiles >= 256) {
+  if (!g_force_small && p.M >= BM2 && (big_tiles >= 256 || (g_variant == 0 && tiles224 >= 160))) {
     static bool attr_set = false;
     if (!attr_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
