@@ -447,3 +447,27 @@ def test_gemm_blaslt_store_bias_and_wgrad(M, N, K):
     big = g(M, 3 * N, seed=46, scale=M ** -0.5)
     wg2 = ops.wgrad(big[:, N:2 * N], a)
     assert ulps_bad(wg2, (big[:, N:2 * N].float().t() @ a.float()).to(torch.bfloat16), 2) < 1e-3
+
+
+def test_gated_residual_library_route():
+    """Long-K gated residual (FF-down): hipBLASLt y = bf16(x.W^T + b), then ltx_gated_residual_bf16
+    with the fused epilogue's roundings; the pre-gate y store (full mode) too."""
+    from ltx_amd import ops
+    M, N, K, B = 1792 * 2, 2048, 8192, 2
+    a, w, b = g(M, K, seed=51), g(N, K, seed=52, scale=K ** -0.5), g(N, seed=53)
+    R, gate = g(M, N, seed=54), g(B, N, seed=55)
+    y = (a.float() @ w.float().t() + b.float()).to(torch.bfloat16)
+    ref = (R.float() + (gate.repeat_interleave(M // B, 0).float() * y.float()).to(torch.bfloat16).float()
+           ).to(torch.bfloat16)
+    ykeep = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out = ops.gemm(a, w, bias=b, epilogue="gated_residual", aux0=R, aux1=gate, aux2=ykeep,
+                   rows_per_batch=M // B)
+    assert ulps_bad(ykeep, y, 2) < 1e-3
+    assert ulps_bad(out, ref, 2) < 2e-3
+    ops._BLASLT[0] = False  # the fused hand-written epilogue agrees
+    try:
+        out2 = ops.gemm(a, w, bias=b, epilogue="gated_residual", aux0=R, aux1=gate,
+                        rows_per_batch=M // B)
+    finally:
+        ops._BLASLT[0] = True
+    assert ulps_bad(out2, ref, 2) < 2e-3

@@ -237,6 +237,37 @@ __global__ __launch_bounds__(256) void ada_v8_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// out = bf16(R + bf16(gate[b] * y)), b = m / rows_per_batch: the GATED_RESIDUAL epilogue
+// (attention.py:305-308) applied to a library GEMM's y = bf16(x.W^T + b); 8 columns per lane.
+// out may alias R.
+__global__ __launch_bounds__(256) void gated_residual_kernel(const bf16_t* r, int64_t ldr,
+                                                             const bf16_t* __restrict__ gate, int64_t ldg,
+                                                             const bf16_t* __restrict__ y, int64_t ldy, bf16_t* out,
+                                                             int64_t ldo, int64_t M, int N, int rpb) {
+  const int N8 = N / 8;
+  const int64_t total = M * N8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / N8;
+    const int c = (int)(i - m * N8) * 8;
+    const u32x4 r4 = *(const u32x4*)(r + m * ldr + c);
+    const u32x4 g4 = *(const u32x4*)(gate + (m / rpb) * ldg + c);
+    const u32x4 y4 = *(const u32x4*)(y + m * ldy + c);
+    u32x4 o;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      float v[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float rv = bf2f((bf16_t)(r4[h] >> (16 * e))), gv = bf2f((bf16_t)(g4[h] >> (16 * e)));
+        const float yv = bf2f((bf16_t)(y4[h] >> (16 * e)));
+        v[e] = rv + rbf(gv * yv);
+      }
+      o[h] = pack2(v[0], v[1]);
+    }
+    *(u32x4*)(out + m * ldo + c) = o;
+  }
+}
+
 // diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), f32 math
 // (embeddings.py:10-50 of the reference carries the same formula), preceded by
 // `timestep_scale_multiplier * timestep` (transformer3d.py:473-474), result cast to bf16.
@@ -532,6 +563,21 @@ int ltx_timestep_embedding(const float* t, float scale, void* out, int64_t B, in
   LTX_CHECK_ARG(t && out && B > 0 && dim > 0 && dim % 2 == 0, "timestep_embedding: bad args");
   hipLaunchKernelGGL(timestep_kernel, dim3(grid_for(B * dim)), dim3(256), 0, (hipStream_t)stream, t, scale,
                      (bf16_t*)out, (int)B, (int)dim);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_gated_residual_bf16(const void* r, int64_t ldr, const void* gate, int64_t ld_gate, const void* y,
+                            int64_t ldy, void* out, int64_t ldo, int64_t M, int64_t N, int64_t rows_per_batch,
+                            void* stream) {
+  LTX_CHECK_ARG(r && gate && y && out && M > 0 && N > 0 && N % 8 == 0, "gated_residual: bad args");
+  LTX_CHECK_ARG(ldr % 8 == 0 && ld_gate % 8 == 0 && ldy % 8 == 0 && ldo % 8 == 0 &&
+                    (((uintptr_t)r | (uintptr_t)gate | (uintptr_t)y | (uintptr_t)out) % 16) == 0,
+                "gated_residual: rows must be 16-B aligned");
+  const int rpb = (int)(rows_per_batch > 0 ? rows_per_batch : M);
+  hipLaunchKernelGGL(gated_residual_kernel, dim3(grid_for(M * N / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)r, ldr, (const bf16_t*)gate, ld_gate, (const bf16_t*)y, ldy, (bf16_t*)out, ldo,
+                     M, (int)N, rpb);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

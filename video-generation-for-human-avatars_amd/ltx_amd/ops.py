@@ -335,6 +335,8 @@ def _gemm_workspace(device):
 # plain-store GEMMs of at least this many MACs go to hipBLASLt (LTX_GEMM_BLASLT=0: hand-written
 # kernel for everything, for A/B); the fused-epilogue products always run the HIP kernels
 BLASLT_MIN_MNK = 1 << 30
+# below this K the fused epilogue wins (the extra y pass costs ~20 us); LTX_BLASLT_GRES_MIN_K for A/B
+BLASLT_GRES_MIN_K = int(os.environ.get("LTX_BLASLT_GRES_MIN_K", "4096"))
 _BLASLT = [os.environ.get("LTX_GEMM_BLASLT", "1") != "0"]
 
 
@@ -359,7 +361,16 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
         ev0.record()
     a2, w2 = ext if ext is not None else (None, None)
     K2 = a2.shape[1] if a2 is not None else 0
-    if (epilogue == "store" and a2 is None and aux0 is None and aux1 is None and aux2 is None
+    if (epilogue == "gated_residual" and a2 is None and _BLASLT[0] and K >= BLASLT_GRES_MIN_K
+            and M * N * K >= BLASLT_MIN_MNK):
+        # long-K gated residual (FF-down): library GEMM for y = bf16(x.W^T + b), then the gate and
+        # residual pass (the fused epilogue's exact roundings); aux2 = where y goes, if kept
+        y = aux2 if aux2 is not None else torch.empty(M, N, dtype=BF16, device=a.device)
+        call("ltx_gemm_blaslt_bf16", 0, 0, _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(y),
+             _rows(y, "y"), M, N, K, _p(bias), 0, _s())
+        call("ltx_gated_residual_bf16", _p(aux0), ld0, _p(aux1), ld1, _p(y), _rows(y, "y"),
+             _p(out), _rows(out, "out"), M, N, rows_per_batch, _s())
+    elif (epilogue == "store" and a2 is None and aux0 is None and aux1 is None and aux2 is None
             and _BLASLT[0] and M * N * K >= BLASLT_MIN_MNK):
         # no fused epilogue: the library GEMM (hipBLASLt, ltx_gemm_blaslt_bf16)
         call("ltx_gemm_blaslt_bf16", 0, 0, _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(out),
