@@ -95,6 +95,10 @@ int ltx_rmsnorm_modulate_bwd(const void* dy, const void* x, const float* rstd, c
 int ltx_ada_modulation(const void* sst, const void* tmod, int64_t ld_tmod, int64_t ld_j,
                        void* out, void* onep_out, int64_t B, int64_t P, int64_t D,
                        int64_t scale_mask, void* stream);
+/* out = bf16(x + y) row-wise (bf16 `.grad += new_grad`, torch's AccumulateGrad for a bf16 leaf):
+ * 16-B aligned rows, N % 8 == 0; out may alias x. */
+int ltx_add_bf16(const void* x, int64_t ldx, const void* y, int64_t ldy, void* out, int64_t ldo, int64_t M,
+                 int64_t N, void* stream);
 /* out = bf16(R + bf16(gate[m / rows_per_batch] * y)) (the LTX_EPI_GATED_RESIDUAL epilogue as its
  * own pass, attention.py:305-308): the FF-down product runs as a plain library GEMM (y = bf16(x.W^T
  * + b)) and this applies the gate and residual. 16-B aligned rows, N % 8 == 0; out may alias R. */

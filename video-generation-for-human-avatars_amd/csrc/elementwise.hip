@@ -268,6 +268,25 @@ __global__ __launch_bounds__(256) void gated_residual_kernel(const bf16_t* r, in
   }
 }
 
+// out = bf16(x + y) over rows (autograd's `.grad += new_grad` for bf16 tensors); 8 per lane,
+// out may alias x
+__global__ __launch_bounds__(256) void add_rows_kernel(const bf16_t* x, int64_t ldx, const bf16_t* __restrict__ y,
+                                                       int64_t ldy, bf16_t* out, int64_t ldo, int64_t M, int N) {
+  const int N8 = N / 8;
+  const int64_t total = M * N8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / N8;
+    const int c = (int)(i - m * N8) * 8;
+    const u32x4 a = *(const u32x4*)(x + m * ldx + c), b = *(const u32x4*)(y + m * ldy + c);
+    u32x4 o;
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      o[h] = pack2(bf2f((bf16_t)(a[h] & 0xffff)) + bf2f((bf16_t)(b[h] & 0xffff)),
+                   bf2f((bf16_t)(a[h] >> 16)) + bf2f((bf16_t)(b[h] >> 16)));
+    *(u32x4*)(out + m * ldo + c) = o;
+  }
+}
+
 // diffusers get_timestep_embedding(flip_sin_to_cos=True, downscale_freq_shift=0), f32 math
 // (embeddings.py:10-50 of the reference carries the same formula), preceded by
 // `timestep_scale_multiplier * timestep` (transformer3d.py:473-474), result cast to bf16.
@@ -563,6 +582,17 @@ int ltx_timestep_embedding(const float* t, float scale, void* out, int64_t B, in
   LTX_CHECK_ARG(t && out && B > 0 && dim > 0 && dim % 2 == 0, "timestep_embedding: bad args");
   hipLaunchKernelGGL(timestep_kernel, dim3(grid_for(B * dim)), dim3(256), 0, (hipStream_t)stream, t, scale,
                      (bf16_t*)out, (int)B, (int)dim);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_add_bf16(const void* x, int64_t ldx, const void* y, int64_t ldy, void* out, int64_t ldo, int64_t M,
+                 int64_t N, void* stream) {
+  LTX_CHECK_ARG(x && y && out && M > 0 && N > 0 && N % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && ldo % 8 == 0 &&
+                    (((uintptr_t)x | (uintptr_t)y | (uintptr_t)out) % 16) == 0,
+                "add_bf16: rows must be 16-B aligned, N % 8 == 0");
+  hipLaunchKernelGGL(add_rows_kernel, dim3(grid_for(M * N / 8)), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     ldx, (const bf16_t*)y, ldy, (bf16_t*)out, ldo, M, (int)N);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

@@ -679,3 +679,10 @@ def wgrad(dy, x):
     out = torch.empty(dy.shape[1], x.shape[1], dtype=BF16, device=dy.device)
     return wgrad_into(out, dy, x, accumulate=False)
 
+
+
+def add_into(x, y):
+    """x (bf16 [M, N]) = bf16(x + y): autograd's bf16 `.grad += new_grad`."""
+    M, N = x.shape
+    call("ltx_add_bf16", _p(x), _rows(x, "x"), _p(y), _rows(y, "y"), _p(x), _rows(x, "x"), M, N, _s())
+    return x

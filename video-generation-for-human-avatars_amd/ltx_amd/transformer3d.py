@@ -577,9 +577,13 @@ class _BlockFn(torch.autograd.Function):
         if full:  # attn1 q/k norm weights, to_q / to_k / to_v (fused dQKV^T . x1)
             ops.qk_norm_wgrad_into(dq1, qkv[:, :D], rq1, _pgrad(a1.q_norm.weight), dk1,
                                    qkv[:, D:2 * D], rk1, _pgrad(a1.k_norm.weight), rope=sh.rope)
+            # one [3D, D] weight-gradient GEMM for q/k/v (they share x1), rounded to bf16 and
+            # then added to each .grad: autograd's new_grad + AccumulateGrad roundings
+            dwqkv = ops.wgrad(dqkv, x1)
             for i, lin in enumerate((a1.to_q, a1.to_k, a1.to_v)):
-                ops.wgrad_into(_pgrad(lin.weight), dqkv[:, i * D:(i + 1) * D], x1)
+                ops.add_into(_pgrad(lin.weight), dwqkv[i * D:(i + 1) * D])
                 ops.colsum_into(_pgrad(lin.bias), dqkv[:, i * D:(i + 1) * D])
+            del dwqkv
         del dq1, dk1
         dh = None
         if ctx.needs_input_grad[4] or full:  # (blk, sh, keep, skip, h, ...)
