@@ -248,8 +248,16 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # rehearsal overrides for a one-GPU box (all ranks on cuda:0 over gloo); the driver's
+        # multi-GPU runs use the defaults: one GPU per rank, RCCL ("nccl")
+        backend = os.environ.get("LTX_BENCH_BACKEND", "nccl")
+        if os.environ.get("LTX_BENCH_SAME_DEVICE") == "1":
+            local_rank = 0
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     device = torch.device("cuda", torch.cuda.current_device())
