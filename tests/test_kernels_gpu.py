@@ -471,3 +471,15 @@ def test_gated_residual_library_route():
     finally:
         ops._BLASLT[0] = True
     assert ulps_bad(out2, ref, 2) < 2e-3
+
+
+def test_add_bf16_accumulate_grad_semantics():
+    """ltx_add_bf16: bf16(x + y) like autograd's bf16 AccumulateGrad, in place, strided rows."""
+    from ltx_amd import ops
+    big = g(300, 3 * 136, seed=61)
+    x = big[:, 136:272]
+    y = g(300, 136, seed=62)
+    exp = (x.float() + y.float()).to(torch.bfloat16)
+    ops.add_into(x, y)
+    assert torch.equal(x, exp)
+    assert torch.equal(big[:, :136], g(300, 3 * 136, seed=61)[:, :136])
