@@ -205,6 +205,9 @@ int ltx_gemm_set_variant(int variant);
  * library keeps the pointer until the next call (stream-ordered reuse by consecutive GEMMs on
  * one stream); bytes = 0 disables split-K. */
 int ltx_gemm_set_workspace(void* ptr, int64_t bytes);
+/* Split-K workspace for GEMMs launched on `stream` (overrides the default one for that stream):
+ * GEMMs on concurrent streams each need their own partials buffer. */
+int ltx_gemm_set_stream_workspace(void* stream, void* ptr, int64_t bytes);
 
 /* ---- LoRA skinny contractions in f32 (peft lora_A / lora_B, training.py:50-68) --------------- */
 /* out[m,j] = alpha * sum_k x[m,k] * Wr[j,k], Wr element (j,k) at Wr[j*wj + k*wk]; x bf16 [M,K]

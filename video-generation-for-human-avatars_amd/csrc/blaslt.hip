@@ -23,7 +23,7 @@ constexpr size_t kBlasltWs = 64u << 20;
 
 struct BlasltDev {
   hipblasLtHandle_t handle = nullptr;
-  void* ws = nullptr;
+  std::map<hipStream_t, void*> ws;  // one workspace per stream: concurrent streams never share it
 };
 
 struct BlasltPlan {
@@ -63,7 +63,10 @@ extern "C" int ltx_gemm_blaslt_bf16(int a_kmajor, int w_kmajor, const void* A, i
   if (!d.handle) {
     hipblasStatus_t st = hipblasLtCreate(&d.handle);
     if (st != HIPBLAS_STATUS_SUCCESS) return blas_fail(st, "create");
-    he = hipMalloc(&d.ws, kBlasltWs);
+  }
+  void*& ws = d.ws[(hipStream_t)stream];
+  if (!ws) {
+    he = hipMalloc(&ws, kBlasltWs);
     if (he != hipSuccess) return fail((int)he, hipGetErrorString(he));
   }
   const PlanKey key{dev, a_kmajor, w_kmajor, bias != nullptr, M, N, K, lda, ldw, ldc, accumulate, 0};
@@ -114,7 +117,7 @@ extern "C" int ltx_gemm_blaslt_bf16(int a_kmajor, int w_kmajor, const void* A, i
   }
   const float alpha = 1.0f, beta = accumulate ? 1.0f : 0.0f;
   hipblasStatus_t st = hipblasLtMatmul(d.handle, pl.desc, &alpha, W, pl.a, A, pl.b, &beta, C, pl.c, C, pl.c,
-                                       &pl.algo, d.ws, pl.ws, (hipStream_t)stream);
+                                       &pl.algo, ws, pl.ws, (hipStream_t)stream);
   if (st != HIPBLAS_STATUS_SUCCESS) return blas_fail(st, "matmul");
   return LTX_OK;
 }

@@ -14,6 +14,8 @@
 // 16x16x32 fragment reads) is applied to the per-lane SOURCE address and to the ds_read address.
 // Block order: XCD-aware (blocks b, b+8 share an XCD / L2) then grouped by 8 row-tiles.
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "common.h"
 #include "ltx_hip.h"
@@ -1205,8 +1207,21 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_p(const GemmParams p) {
 }
 
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
-static float* g_ws = nullptr;   // split-K workspace (caller-owned, ltx_gemm_set_workspace)
-static size_t g_ws_bytes = 0;
+// split-K workspaces (caller-owned): a default (ltx_gemm_set_workspace) and optional per-stream
+// ones (ltx_gemm_set_stream_workspace), so GEMMs running concurrently on two streams never share
+// a partials buffer
+struct SplitWs {
+  float* ptr = nullptr;
+  size_t bytes = 0;
+};
+static SplitWs g_ws_default;
+static std::mutex g_ws_mu;
+static std::map<hipStream_t, SplitWs> g_ws_stream;
+static SplitWs ws_for(hipStream_t s) {
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  auto it = g_ws_stream.find(s);
+  return it != g_ws_stream.end() ? it->second : g_ws_default;
+}
 static void* g_stamps = nullptr;  // diagnostic stamp buffer (variants 19/20)
 static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (t-kernel, auto tile height),
                                 // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split,
@@ -1231,7 +1246,8 @@ static int launch(const GemmParams& p, hipStream_t s) {
       const int nk = p.K / BK;
       int S = (int)std::min<int64_t>(8, 256 / big_tiles);
       while (S > 1 && nk / S < 16) --S;
-      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > g_ws_bytes) --S;
+      const SplitWs ws = ws_for(s);
+      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > ws.bytes) --S;
       if (S > 1 && big_tiles * S >= 128) {  // else the 128x128 kernel's split fills the chip better
         static bool sk_set = false;
         if (!sk_set) {
@@ -1240,7 +1256,7 @@ static int launch(const GemmParams& p, hipStream_t s) {
           sk_set = true;
         }
         GemmParams q = p;
-        q.ws = g_ws;
+        q.ws = ws.ptr;
         q.splitk = S;
         hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>), dim3((unsigned)(big_tiles * S)), dim3(512),
                            LDS2, s, q);
@@ -1356,11 +1372,12 @@ static int launch(const GemmParams& p, hipStream_t s) {
     if (tiles < 128 && nk >= 8) {
       S = min(min(8, nk / 4), (256 + tiles - 1) / tiles);
       // (capped at the 32 MiB the small-tile split-K was tuned and validated with)
-      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > std::min<size_t>(g_ws_bytes, 32u << 20)) --S;
+      const size_t cap = std::min<size_t>(ws_for(s).bytes, 32u << 20);
+      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > cap) --S;
     }
     if (S > 1) {
       GemmParams q = p;
-      q.ws = g_ws;
+      q.ws = ws_for(s).ptr;
       q.splitk = S;
       hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles * S), dim3(GEMM_THREADS), LDS_BYTES, s, q);
       LTX_LAUNCH_CHECK();
@@ -1402,8 +1419,17 @@ extern "C" int ltx_gemm_set_stamps(void* ptr) {
 extern "C" int ltx_gemm_set_workspace(void* ptr, int64_t bytes) {
   LTX_CHECK_ARG(bytes >= 0 && (ptr != nullptr || bytes == 0) && ((uintptr_t)ptr % 16) == 0,
                 "gemm_set_workspace: bad buffer");
-  g_ws = (float*)ptr;
-  g_ws_bytes = (size_t)bytes;
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  g_ws_default.ptr = (float*)ptr;
+  g_ws_default.bytes = (size_t)bytes;
+  return LTX_OK;
+}
+
+extern "C" int ltx_gemm_set_stream_workspace(void* stream, void* ptr, int64_t bytes) {
+  LTX_CHECK_ARG(bytes >= 0 && (ptr != nullptr || bytes == 0) && ((uintptr_t)ptr % 16) == 0,
+                "gemm_set_stream_workspace: bad buffer");
+  std::lock_guard<std::mutex> lock(g_ws_mu);
+  g_ws_stream[(hipStream_t)stream] = SplitWs{(float*)ptr, (size_t)bytes};
   return LTX_OK;
 }
 

@@ -322,12 +322,16 @@ GEMM_WS_BYTES = 128 << 20  # split-K partials: S x M x N f32 (S=4 at 2048 x 2048
 
 
 def _gemm_workspace(device):
-    """The split-K workspace handed to the library once per process (caller-owned memory)."""
-    key = str(device)
+    """The split-K workspace of the current stream, handed to the library once per (device,
+    stream) (caller-owned memory): the default stream's doubles as the library default, other
+    streams (the text side stream) get their own, so concurrent GEMMs never share partials."""
+    stream = _s()
+    key = (str(device), stream.value)
     if key not in _GEMM_WS:
         ws = torch.empty(GEMM_WS_BYTES // 4, dtype=F32, device=device)
-        call("ltx_gemm_set_workspace", _p(ws), GEMM_WS_BYTES)
-        _GEMM_WS.clear()
+        if not any(k[0] == key[0] for k in _GEMM_WS):
+            call("ltx_gemm_set_workspace", _p(ws), GEMM_WS_BYTES)
+        call("ltx_gemm_set_stream_workspace", stream, _p(ws), GEMM_WS_BYTES)
         _GEMM_WS[key] = ws
     return _GEMM_WS[key]
 
