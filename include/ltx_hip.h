@@ -258,6 +258,11 @@ int ltx_mse_fwd_bwd(const void* out, const void* v, void* dout, float* stats, in
 int ltx_adamw_step(void* param, const void* grad, void* exp_avg, void* exp_avg_sq, int64_t n,
                    int is_bf16, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int64_t step, void* stream);
+/* ltx_adamw_step for many tensors of one dtype in one launch (the LoRA / caption-projection
+ * optimizer step, training.py:270-271): table = device int64 [nchunks][6] of (param, grad,
+ * exp_avg, exp_avg_sq, first element, count <= 2048); all tensors at the same step. */
+int ltx_adamw_multi(const int64_t* table, int64_t nchunks, int is_bf16, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, int64_t step, void* stream);
 
 /* ---- train_mode='full' parameter gradients (csrc/paramgrad.hip) --------- */
 /* Weight gradient of the q/k RMSNorm weights: partials[(which * splits + s) * D + d] (f32) =

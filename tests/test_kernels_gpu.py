@@ -483,3 +483,23 @@ def test_add_bf16_accumulate_grad_semantics():
     ops.add_into(x, y)
     assert torch.equal(x, exp)
     assert torch.equal(big[:, :136], g(300, 3 * 136, seed=61)[:, :136])
+
+
+def test_fused_adamw_multi_tensor_bitwise():
+    """FusedAdamW's one-launch-per-dtype path (ltx_adamw_multi) == the per-tensor kernels, bitwise,
+    over mixed f32 (LoRA) / bf16 (caption projection) tensors, several steps."""
+    from ltx_amd.training import FusedAdamW
+    shapes = [((16, 2048), torch.float32), ((2048, 16), torch.float32), ((3000,), torch.bfloat16),
+              ((64, 130), torch.bfloat16), ((5,), torch.float32)]
+
+    def run(multi):
+        ps = [torch.nn.Parameter(g(*sh, dtype=dt, seed=70 + i)) for i, (sh, dt) in enumerate(shapes)]
+        opt = FusedAdamW(ps, lr=1e-2, multi_tensor=multi)
+        for k in range(3):
+            for i, p in enumerate(ps):
+                p.grad = g(*p.shape, dtype=p.dtype, seed=100 * k + i)
+            opt.step()
+        return [p.detach().clone() for p in ps]
+    a, b = run(True), run(False)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

@@ -436,32 +436,54 @@ __global__ __launch_bounds__(256) void mse_finish_kernel(float* __restrict__ sta
 // torch.optim.AdamW, foreach implementation order (weight decay, lerp m, v*b2 + (1-b2) g g,
 // sqrt, / sqrt(bc2), + eps, p += step_size * m / den), rounding every op for bf16 tensors.
 template <bool BF16>
+__device__ __forceinline__ void adamw_elem(void* __restrict__ param, const void* __restrict__ grad,
+                                           void* __restrict__ m_, void* __restrict__ v_, int64_t i, float decay,
+                                           float w1, float b2, float w2, float step_size, float bc2_sqrt, float eps) {
+  float p, g, m, v;
+  if (BF16) {
+    p = bf2f(((bf16_t*)param)[i]); g = bf2f(((const bf16_t*)grad)[i]);
+    m = bf2f(((bf16_t*)m_)[i]); v = bf2f(((bf16_t*)v_)[i]);
+  } else {
+    p = ((float*)param)[i]; g = ((const float*)grad)[i]; m = ((float*)m_)[i]; v = ((float*)v_)[i];
+  }
+  auto R = [](float x) { return BF16 ? rbf(x) : x; };
+  p = R(p * decay);
+  m = R(torch_lerp(m, g, w1));
+  v = R(v * b2);
+  v = R(v + w2 * g * g);
+  float den = R(sqrtf(v));
+  den = R(den / bc2_sqrt);
+  den = R(den + eps);
+  p = R(p + step_size * (m / den));
+  if (BF16) {
+    ((bf16_t*)param)[i] = f2bf(p); ((bf16_t*)m_)[i] = f2bf(m); ((bf16_t*)v_)[i] = f2bf(v);
+  } else {
+    ((float*)param)[i] = p; ((float*)m_)[i] = m; ((float*)v_)[i] = v;
+  }
+}
+
+template <bool BF16>
 __global__ void adamw_kernel(void* __restrict__ param, const void* __restrict__ grad, void* __restrict__ m_,
                              void* __restrict__ v_, int64_t n, float decay, float w1, float b2, float w2,
                              float step_size, float bc2_sqrt, float eps) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float p, g, m, v;
-    if (BF16) {
-      p = bf2f(((bf16_t*)param)[i]); g = bf2f(((const bf16_t*)grad)[i]);
-      m = bf2f(((bf16_t*)m_)[i]); v = bf2f(((bf16_t*)v_)[i]);
-    } else {
-      p = ((float*)param)[i]; g = ((const float*)grad)[i]; m = ((float*)m_)[i]; v = ((float*)v_)[i];
-    }
-    auto R = [](float x) { return BF16 ? rbf(x) : x; };
-    p = R(p * decay);
-    m = R(torch_lerp(m, g, w1));
-    v = R(v * b2);
-    v = R(v + w2 * g * g);
-    float den = R(sqrtf(v));
-    den = R(den / bc2_sqrt);
-    den = R(den + eps);
-    p = R(p + step_size * (m / den));
-    if (BF16) {
-      ((bf16_t*)param)[i] = f2bf(p); ((bf16_t*)m_)[i] = f2bf(m); ((bf16_t*)v_)[i] = f2bf(v);
-    } else {
-      ((float*)param)[i] = p; ((float*)m_)[i] = m; ((float*)v_)[i] = v;
-    }
-  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    adamw_elem<BF16>(param, grad, m_, v_, i, decay, w1, b2, w2, step_size, bc2_sqrt, eps);
+}
+
+// every trainable tensor of one dtype in one launch: a block per table entry
+// (param, grad, exp_avg, exp_avg_sq, first element, count <= 2048), the same per-element math
+template <bool BF16>
+__global__ __launch_bounds__(256) void adamw_multi_kernel(const int64_t* __restrict__ table, float decay, float w1,
+                                                          float b2, float w2, float step_size, float bc2_sqrt,
+                                                          float eps) {
+  const int64_t* e = table + (int64_t)blockIdx.x * 6;
+  void* param = (void*)e[0];
+  const void* grad = (const void*)e[1];
+  void* m = (void*)e[2];
+  void* v = (void*)e[3];
+  const int64_t start = e[4], end = e[4] + e[5];
+  for (int64_t i = start + threadIdx.x; i < end; i += 256)
+    adamw_elem<BF16>(param, grad, m, v, i, decay, w1, b2, w2, step_size, bc2_sqrt, eps);
 }
 
 static inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
@@ -663,6 +685,25 @@ int ltx_mse_fwd_bwd(const void* out, const void* v, void* dout, float* stats, in
   hipLaunchKernelGGL(mse_kernel, dim3(MSE_BLOCKS), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)out,
                      (const bf16_t*)v, (bf16_t*)dout, stats, n, norm, grad_scale);
   hipLaunchKernelGGL(mse_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, stats);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_adamw_multi(const int64_t* table, int64_t nchunks, int is_bf16, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, int64_t step, void* stream) {
+  LTX_CHECK_ARG(table && nchunks > 0 && nchunks < (1LL << 31) && step >= 1, "adamw_multi: bad args");
+  const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+  const float decay = (float)(1.0 - (double)lr * (double)weight_decay);
+  const float step_size = (float)(-((double)lr / bc1));
+  const float bc2_sqrt = (float)std::sqrt(bc2);
+  const float w1 = (float)(1.0 - (double)beta1), w2 = (float)(1.0 - (double)beta2);
+  if (is_bf16)
+    hipLaunchKernelGGL(adamw_multi_kernel<true>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, table,
+                       decay, w1, beta2, w2, step_size, bc2_sqrt, eps);
+  else
+    hipLaunchKernelGGL(adamw_multi_kernel<false>, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, table,
+                       decay, w1, beta2, w2, step_size, bc2_sqrt, eps);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

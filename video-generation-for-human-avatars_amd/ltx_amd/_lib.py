@@ -63,6 +63,7 @@ _SIGNATURES = {
     "ltx_colsum_bf16": [_p, _i64, _p, _i64, _i64, _p],
     "ltx_batch_sum_bf16": [_p, _i64, _i64, _i64, _i64, _p, _i64, _p],
     "ltx_mse_fwd_bwd": [_p, _p, _p, _p, _i64, _f32, _p],
+    "ltx_adamw_multi": [_p, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i64, _p],
     "ltx_adamw_step": [_p, _p, _p, _p, _i64, _i32, _f32, _f32, _f32, _f32, _f32, _i64, _p],
     "ltx_qk_norm_wgrad": [_p, _i64, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _p, _p, _p, _i64,
                           _i64, _i64, _i64, _i32, _i64, _p, _p],

@@ -78,13 +78,19 @@ class FusedAdamW(torch.optim.Optimizer):
     reference constructs AdamW(trainable, lr) at training.py:270-271) with one ltx_adamw_step
     kernel per tensor; f32 LoRA adapters and bf16 caption-projection params keep their dtype."""
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+    CHUNK = 2048  # elements per block of the multi-tensor kernel
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 multi_tensor=True):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self.multi_tensor = multi_tensor
+        self._tables = []  # pinned host tables of the last steps (alive until their H2D lands)
 
     @torch.no_grad()
     def step(self, closure=None):
         for group in self.param_groups:
             b1, b2 = group["betas"]
+            todo = []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -94,9 +100,34 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
-                ops.adamw_step(p, p.grad.contiguous(), st["exp_avg"], st["exp_avg_sq"], group["lr"],
-                               b1, b2, group["eps"], group["weight_decay"], st["step"])
+                todo.append((p, p.grad.contiguous(), st))
+            by_dtype = {}
+            for item in todo:
+                by_dtype.setdefault(item[0].dtype, []).append(item)
+            for dtype, items in by_dtype.items():
+                steps = {st["step"] for _, _, st in items}
+                if self.multi_tensor and len(items) > 1 and len(steps) == 1 and items[0][0].is_cuda:
+                    self._multi(items, dtype, group, b1, b2, steps.pop())
+                    continue
+                for p, g, st in items:
+                    ops.adamw_step(p, g, st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
+                                   group["eps"], group["weight_decay"], st["step"])
         ops.bump_weight_generation()  # in-place kernel updates: invalidate weight-derived caches
+
+    def _multi(self, items, dtype, group, b1, b2, step):
+        """One ltx_adamw_multi launch for all tensors of a dtype (bitwise the per-tensor math)."""
+        rows = []
+        for p, g, st in items:
+            ptrs = (p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr())
+            n = p.numel()
+            for start in range(0, n, self.CHUNK):
+                rows.append(ptrs + (start, min(self.CHUNK, n - start)))
+        host = torch.tensor(rows, dtype=torch.int64).pin_memory()
+        dev = host.to(items[0][0].device, non_blocking=True)
+        self._tables = (self._tables + [(host, dev, [g for _, g, _ in items])])[-2:]
+        ops.call("ltx_adamw_multi", ops._p(dev), len(rows), 1 if dtype == torch.bfloat16 else 0,
+                 float(group["lr"]), float(b1), float(b2), float(group["eps"]),
+                 float(group["weight_decay"]), int(step), ops._s())
 
 
 class GradAllReduce:
