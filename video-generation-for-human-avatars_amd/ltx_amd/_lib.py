@@ -99,7 +99,7 @@ def load(path: str = None):
     with _lock:
         if _lib is not None:
             return _lib
-        path = path or LIB_PATH
+        path = path or os.environ.get("LTX_HIP_LIB") or LIB_PATH  # override: A/B of two builds
         if not os.path.exists(path):
             raise LtxHipError(
                 f"libltxhip.so not found at {path}: build it with `make -C "
