@@ -135,7 +135,44 @@ def cpu_baseline(budget_layers=28, timed=2):
         for v in p.values():
             v.grad = None
     per_sample = sum(times[1:]) / timed * (28.0 / budget_layers)
+    # config T ("config A at B = 1 and config T"): the tiny 2-layer model, one
+    # 1x8x8 latent, steady-state median of 20 steps after 3 warm-ups
+    tcfg = {"num_layers": 2, "num_attention_heads": 4, "attention_head_dim": 32, "in_channels": 128,
+            "out_channels": 128, "cross_attention_dim": 128, "caption_channels": 64}
+    tcfg = {**OURS_TRANSFORMER_CONFIG, **tcfg}
+    tp = {}
+    for name, shape in O.param_shapes(tcfg, LORA_RANK).items():
+        t = torch.randn(shape, generator=g) * (1.0 / math.sqrt(shape[-1]) if len(shape) == 2 else 0.02)
+        if len(shape) == 1 and "norm" in name:
+            t = torch.ones(shape)
+        t = t.to(torch.float32 if "lora_" in name else torch.bfloat16)
+        if ("lora_" in name) or ("caption_projection" in name):
+            t.requires_grad_(True)
+        tp[name] = t
+    tl = [torch.randn(1, 128, 1, 8, 8, generator=g) for _ in range(3)]
+    tprompt = torch.randn(1, 4, 64, generator=g)
+    tmask = torch.ones(1, 4, dtype=torch.long)
+    tt = []
+    for i in range(23):
+        t0 = time.perf_counter()
+        r = O.train_step(tp, tcfg, tl[0], tl[1], tl[2], tprompt, tmask)
+        r["loss"].backward()
+        if i >= 3:
+            tt.append(time.perf_counter() - t0)
+        for v in tp.values():
+            v.grad = None
+    tt.sort()
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
     return {"value": 1.0 / per_sample, "unit": "samples/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model, "config_t_ms_per_step": round(tt[len(tt) // 2] * 1e3, 2),
             "tokens_per_s": F_LAT * H_LAT * W_LAT / per_sample,
             "sample": (f"oracle/ltx_oracle.py train_step fwd+bwd, B=1, N={F_LAT*H_LAT*W_LAT}, "
                        f"{budget_layers}/28 LTX-2B blocks, 1 warm-up + {timed} timed steps "
