@@ -391,7 +391,7 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
     return out
 
 
-def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False):
+def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_out=None):
     """out[m,j] = alpha * x[m,:] . Wr[j,:]; Wr = lora_A [r,K]; transposed=True takes lora_B [K,r]
     (i.e. uses B^T) for the dgrad w = s * dY . B. split=True also returns the activation
     K-extension operand of the rows (what lora_split(out, "act") makes), written by the same
@@ -404,12 +404,13 @@ def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False):
         r = wr.shape[0]
         wj, wk = wr.stride(0), 1
     out = torch.empty(M, r, dtype=F32, device=x.device) if out is None else out
-    sp, K2 = None, 0
-    if split:
+    sp, K2, lds = None, 0, 0
+    if split:  # split_out: a [M, K2] column block of a wider operand (the merged text K/V GEMMs)
         K2 = lora_k2(r)
-        sp = torch.empty(M, K2, dtype=BF16, device=x.device)
+        sp = torch.empty(M, K2, dtype=BF16, device=x.device) if split_out is None else split_out
+        lds = _rows(sp, "split_out")
     call("ltx_lora_down", _p(x), _rows(x, "x"), _p(wr), wj, wk, _p(out), _rows(out, "out"), M, K, r,
-         float(alpha), _p(sp), K2, K2, _s())
+         float(alpha), _p(sp), lds, K2, _s())
     return (out, sp) if split else out
 
 

@@ -278,10 +278,34 @@ class BasicTransformerBlock(nn.Module):
         p["out1_wT"] = ops.transpose(a1.to_out[0].weight)
         for name, lin in (("q2", a2.to_q), ("k2", a2.to_k), ("v2", a2.to_v), ("o2", a2.to_out[0])):
             p[name + "_wT"] = ops.transpose(_lin(lin)[0])
+        # text K and V as one [2D, D] projection (they share enc2): one GEMM each way
+        p["kv2_w"] = torch.cat([_lin(a2.to_k)[0], _lin(a2.to_v)[0]], 0).contiguous()
+        p["kv2_b"] = torch.cat([_lin(a2.to_k)[1], _lin(a2.to_v)[1]], 0).contiguous()
+        p["kv2_wT"] = torch.cat([p["k2_wT"], p["v2_wT"]], 1).contiguous()
+        self._kv_ext = None
         p["ff1_wT"] = ops.transpose(ff.net[0].proj.weight)
         p["ff2_wT"] = ops.transpose(ff.net[2].weight)
         self._pack, self._pack_key = p, key
         return p
+
+
+def _kv_ext(blk, lk, lv):
+    """K-extension weights of the merged text K/V GEMMs, rebuilt with the adapters: forward
+    [2D, 2 K2] block-diagonal (split(s B_k) | 0 ; 0 | split(s B_v)), backward [D, 2 K2] =
+    split(A_k^T) | split(A_v^T) (both adapters add into the encoder gradient)."""
+    fb, fv = lk.weight_split("B"), lv.weight_split("B")
+    ba, bv = lk.weight_split("A"), lv.weight_split("A")
+    key = tuple(id(t) for t in (fb, fv, ba, bv))  # the splits are replaced when an adapter changes
+    hit = getattr(blk, "_kv_ext", None)
+    if hit is not None and hit[0] == key:
+        return hit[1], hit[2]
+    D, K2 = fb.shape
+    fwd = torch.zeros(2 * D, 2 * K2, dtype=fb.dtype, device=fb.device)
+    fwd[:D, :K2] = fb
+    fwd[D:, K2:] = fv
+    bwd = torch.cat([ba, bv], 1).contiguous()
+    blk._kv_ext = (key, fwd, bwd, (fb, fv, ba, bv))  # hold the splits: ids stay unique
+    return fwd, bwd
 
 
 class TimestepEmbedding(nn.Module):
@@ -513,14 +537,20 @@ class _BlockFn(torch.autograd.Function):
             lin = a2.to_out[0]
             ops.wgrad_into(_pgrad(lin.weight), dh2, o2)
             ops.colsum_into(_pgrad(lin.bias), dh2)
-        dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
-                                     key_bias=sh.enc_bias, kv_shared=sh.text_shared)
-        del do2
+        # [dK_raw | dV] of the text rows side by side: the merged encoder-gradient GEMM's operand
+        dkv = torch.empty(k2raw.shape[0], 2 * D, dtype=torch.bfloat16, device=h.device)
         if sh.text_shared:  # gradient of the shared text rows = sum over the query batches
+            dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
+                                         key_bias=sh.enc_bias, kv_shared=True)
             dk2 = ops.batch_sum(dk2, B)
-            dv2 = ops.batch_sum(dv2, B)
+            dv2 = ops.batch_sum(dv2, B, out=dkv[:, D:])
+        else:
+            dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
+                                         key_bias=sh.enc_bias, dv=dkv[:, D:])
+        del do2
         dq2raw, _ = ops.qk_norm_rope_bwd(dq2, q2raw, a2.q_norm.weight, rq2, B=B, N=N)
-        dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=sh.Bt, N=L)
+        dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=sh.Bt, N=L,
+                                         dq_out=dkv[:, :D])
         if full:  # attn2 q/k norm weights, to_q / to_k / to_v
             ops.qk_norm_wgrad_into(dq2, q2raw, rq2, _pgrad(a2.q_norm.weight), B=B, N=N)
             ops.qk_norm_wgrad_into(dk2, k2raw, rk2, _pgrad(a2.k_norm.weight), B=sh.Bt, N=L)
@@ -537,24 +567,26 @@ class _BlockFn(torch.autograd.Function):
             ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
                            ext=(sw, lq.weight_split("A")))
+            K2 = ops.lora_k2(r)
+            swkv = torch.empty(dkv.shape[0], 2 * K2, dtype=torch.bfloat16, device=h.device)
             ops.lora_wgrad(dk2raw, u_k, alpha=s, out=_grad_buf(lk, "B"), accumulate=True)
-            w_k, sw = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True, split=True)
+            w_k, _ = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True, split=True,
+                                   split_out=swkv[:, :K2])
             ops.lora_wgrad(enc2, w_k, transpose_out=True, out=_grad_buf(lk, "A"), accumulate=True)
-            denc = ops.gemm(dk2raw, W["k2_wT"], ext=(sw, lk.weight_split("A")))
             ops.lora_wgrad(dv2, u_v, alpha=s, out=_grad_buf(lv, "B"), accumulate=True)
-            w_v, sw = ops.lora_down(dv2, Bv, alpha=s, transposed=True, split=True)
+            w_v, _ = ops.lora_down(dv2, Bv, alpha=s, transposed=True, split=True,
+                                   split_out=swkv[:, K2:])
             ops.lora_wgrad(enc2, w_v, transpose_out=True, out=_grad_buf(lv, "A"), accumulate=True)
-            ops.gemm(dv2, W["v2_wT"], epilogue="accum", aux0=denc, out=denc,
-                     ext=(sw, lv.weight_split("A")))
-            del sw
+            # denc = dK_raw.W_k + dV.W_v + both adapters' input-gradient terms, one GEMM
+            denc = ops.gemm(dkv, W["kv2_wT"], ext=(swkv, _kv_ext(blk, lk, lv)[1]))
+            del swkv
             # the adapter gradients went straight into .grad (accumulated across micro-steps by
             # the kernels' atomics); autograd gets None for them
             grads_lora = [None] * 8
         else:
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2)
-            denc = ops.gemm(dk2raw, W["k2_wT"])
-            ops.gemm(dv2, W["v2_wT"], epilogue="accum", aux0=denc, out=denc)
-        del dq2raw, dk2raw, dv2, dh2
+            denc = ops.gemm(dkv, W["kv2_wT"])
+        del dq2raw, dk2raw, dv2, dh2, dkv
         # ---- attn1: h1 = h + g_msa * to_out(sdpa(rope(qn(q)), rope(kn(k)), v))
         d_y1 = ops.gate_mul(dh1, mods[:, 2], rpm)
         do1 = ops.gemm(d_y1, W["out1_wT"])
@@ -636,19 +668,20 @@ def _text_kv(blk, sh, enc2, lora_ab):
     training.py:50-68, then the k RMSNorm): they depend only on enc2 and the block's weights, so
     _forward_tokens can compute them on a side stream one block ahead."""
     a2 = blk.attn2
-    wk, bk, _ = _lin(a2.to_k)
-    wv, bv, _ = _lin(a2.to_v)
+    W = blk.packed()
+    D = sh.D
     if lora_ab:
         lora = _lora_params(blk)
         _, _, Ak, _, Av, _, _, _ = lora_ab
-        u_k, su = ops.lora_down(enc2, Ak, split=True)
-        k2raw = ops.gemm(enc2, wk, bias=bk, ext=(su, lora[1].weight_split("B")))
-        u_v, su = ops.lora_down(enc2, Av, split=True)
-        v2 = ops.gemm(enc2, wv, bias=bv, ext=(su, lora[2].weight_split("B")))
+        K2 = ops.lora_k2(lora[1].r)
+        su = torch.empty(enc2.shape[0], 2 * K2, dtype=torch.bfloat16, device=enc2.device)
+        u_k, _ = ops.lora_down(enc2, Ak, split=True, split_out=su[:, :K2])
+        u_v, _ = ops.lora_down(enc2, Av, split=True, split_out=su[:, K2:])
+        kv = ops.gemm(enc2, W["kv2_w"], bias=W["kv2_b"], ext=(su, _kv_ext(blk, lora[1], lora[2])[0]))
     else:
         u_k = u_v = None
-        k2raw = ops.gemm(enc2, wk, bias=bk)
-        v2 = ops.gemm(enc2, wv, bias=bv)
+        kv = ops.gemm(enc2, W["kv2_w"], bias=W["kv2_b"])
+    k2raw, v2 = kv[:, :D], kv[:, D:]
     k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, a2.k_norm.weight, None, None, B=sh.Bt, N=sh.L)
     return k2raw, k2, rk2, v2, u_k, u_v
 
@@ -1025,6 +1058,11 @@ class Transformer3DModel(nn.Module):
 
             def prep(j):
                 bj = blocks[j]
+                with torch.no_grad():  # weight caches are built on the main stream
+                    bj.packed()
+                    lj = _lora_params(bj)
+                    if lj is not None:
+                        _kv_ext(bj, lj[1], lj[2])
                 with torch.no_grad(), torch.cuda.stream(side):
                     side.wait_event(ready)
                     vals = _text_kv(bj, sh, enc2, _lora_ab(bj))
