@@ -32,4 +32,16 @@ res = {"down_A_us": t(lambda: ops.lora_down(x, A)),
        "wgrad_A_us": t(lambda: ops.lora_wgrad(x, u, transpose_out=True, out=dA, accumulate=True))}
 ref = (x.float() @ A.t())
 res["down_rel"] = float((ops.lora_down(x, A) - ref).norm() / ref.norm())
+xs = x[:256].contiguous()
+us = u[:256].contiguous()
+res["text_down_A_us"] = t(lambda: ops.lora_down(xs, A, split=True))
+res["text_down_Bt_split_us"] = t(lambda: ops.lora_down(xs, Bm, alpha=0.5, transposed=True, split=True))
+res["text_wgrad_B_us"] = t(lambda: ops.lora_wgrad(xs, us, alpha=0.5, out=dB, accumulate=True))
+res["text_wgrad_A_us"] = t(lambda: ops.lora_wgrad(xs, us, transpose_out=True, out=dA, accumulate=True))
+refs = xs.float() @ A.t()
+res["text_down_rel"] = float((ops.lora_down(xs, A) - refs).norm() / refs.norm())
+dB0 = torch.zeros_like(dB)
+ops.lora_wgrad(xs, us, alpha=0.5, out=dB0, accumulate=True)
+refw = 0.5 * xs.float().t() @ us
+res["text_wgrad_rel"] = float((dB0 - refw).norm() / refw.norm())
 print(json.dumps({k: round(v, 7) for k, v in res.items()}), flush=True)
