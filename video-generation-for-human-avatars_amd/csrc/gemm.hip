@@ -185,8 +185,12 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
   }
 }
 
-template <int EPI, int R>
+// NST = LDS stages: 2 (one K-tile in flight while the other computes) or 3 / 4 (NST - 1 in
+// flight; for grids of at most one workgroup per CU, whose few K-tiles per workgroup are
+// load-latency-bound)
+template <int EPI, int R, int NST = 2>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmParams p) {
+  static_assert(NST >= 2 && NST <= 4, "gemm_nt_kernel: 2 to 4 stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -247,13 +251,36 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
   const int S = p.splitk > 1 ? p.splitk : 1;
   const int kt0 = (int)((int64_t)split * nk_all / S), nk = (int)((int64_t)(split + 1) * nk_all / S);
   stage(0, kt0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (NST > 2) {
+#pragma unroll
+    for (int st = 1; st < NST - 1; ++st)
+      if (kt0 + st < nk) stage(st, kt0 + st);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   const int frow = lane & 15;   // fragment row within a 16-row subtile
   const int fchunk = lane >> 4;  // fragment k-chunk (8 elements) within a 32-deep k-step
   for (int kt = kt0; kt < nk; ++kt) {
-    const int cur = (kt - kt0) & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    int cur;
+    if constexpr (NST > 2) {
+      // stages kt .. kt+NST-2 are in flight (8 direct-to-LDS loads per thread each): wait for
+      // kt's, then the barrier also retires every wave's reads of the buffer stage kt+NST-1
+      // overwrites (one asm statement with a raw s_barrier: __syncthreads' fence would wait for
+      // vmcnt(0))
+      cur = (kt - kt0) % NST;
+      const int ahead = min(NST - 2, nk - 1 - kt);  // stages issued after kt
+      if (ahead >= 2)
+        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (ahead == 1)
+        asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + NST - 1 < nk) stage((cur + NST - 1) % NST, kt + NST - 1);
+    } else {
+      cur = (kt - kt0) & 1;
+      if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    }
     const char* xs = smem + cur * STAGE_BYTES;
     const char* ws = xs + TILE_BYTES;
 #pragma unroll
@@ -275,9 +302,12 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (NST == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
+  if constexpr (NST > 2) __syncthreads();  // the epilogue's C image reuses stage 0
 
   if (S > 1) {  // split-K: raw f32 partial, 4 consecutive n per lane (16-B stores)
     float* part = p.ws + (int64_t)split * p.M * p.N;
@@ -1207,6 +1237,12 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_kernel_p(const GemmParams p) {
 }
 
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
+// LDS stages of the 128x128 kernel: 0 = auto (3 when the grid is at most one round), 2..4 forced
+// (LTX_GEMM_SMALL_STAGES, A/B tests)
+static const int g_small_stages = [] {
+  const char* e = getenv("LTX_GEMM_SMALL_STAGES");
+  return e ? atoi(e) : 0;
+}();
 // split-K workspaces (caller-owned): a default (ltx_gemm_set_workspace) and optional per-stream
 // ones (ltx_gemm_set_stream_workspace), so GEMMs running concurrently on two streams never share
 // a partials buffer
@@ -1375,14 +1411,36 @@ static int launch(const GemmParams& p, hipStream_t s) {
       const size_t cap = std::min<size_t>(ws_for(s).bytes, 32u << 20);
       while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > cap) --S;
     }
+    // at most one workgroup per CU: three LDS stages (two K-tiles in flight)
+    const int nst = g_small_stages >= 2 ? g_small_stages : ((int64_t)tiles * S <= 256 ? 3 : 2);
+    const bool deep = nst > 2;
+    if (deep) {
+      static bool d_set = false;
+      if (!d_set) {
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, R, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  3 * STAGE_BYTES);
+        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, R, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  4 * STAGE_BYTES);
+        d_set = true;
+      }
+    }
     if (S > 1) {
       GemmParams q = p;
       q.ws = ws_for(s).ptr;
       q.splitk = S;
-      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles * S), dim3(GEMM_THREADS), LDS_BYTES, s, q);
+      if (nst == 4)
+        hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 4>), dim3(tiles * S), dim3(GEMM_THREADS), 4 * STAGE_BYTES, s, q);
+      else if (deep)
+        hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 3>), dim3(tiles * S), dim3(GEMM_THREADS), 3 * STAGE_BYTES, s, q);
+      else
+        hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles * S), dim3(GEMM_THREADS), LDS_BYTES, s, q);
       LTX_LAUNCH_CHECK();
       const int64_t n8 = (int64_t)p.M * (p.N / 8);
       hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, R>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, q);
+    } else if (nst == 4) {
+      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 4>), dim3(tiles), dim3(GEMM_THREADS), 4 * STAGE_BYTES, s, p);
+    } else if (deep) {
+      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 3>), dim3(tiles), dim3(GEMM_THREADS), 3 * STAGE_BYTES, s, p);
     } else {
       hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles), dim3(GEMM_THREADS), LDS_BYTES, s, p);
     }
