@@ -122,6 +122,43 @@ def test_infer_forward_matches_reference(case):
     assert e_b <= 1.25 * e_r + 2e-3, f"{case}: build {e_b:.3e} vs reference bf16 noise {e_r:.3e}"
 
 
+def test_text_side_stream_after_weight_update():
+    """The inference text-K/V side stream must start after the main stream's weight-cache rebuilds
+    (cold cache, or after an optimizer step that bumps ops.weight_generation): outputs with the
+    side stream equal the inline path's bit for bit."""
+    import ltx_amd.transformer3d as T
+    from ltx_amd import ops
+    d, meta = _load("infer_step")
+    params, tmeta = _tiny()
+    model = build_model(meta["config"], params, tmeta["lora_rank"], device=DEV)
+    model.eval()
+    kw = dict(hidden_states=d["in.tokens"].to(DEV), indices_grid=d["in.indices_grid"].to(DEV),
+              ref_image_hidden_states=d["in.ref"].to(DEV), pose_hidden_states=d["in.pose"].to(DEV),
+              encoder_hidden_states=d["in.enc"].to(DEV),
+              encoder_attention_mask=d["in.enc_mask"].to(DEV), timestep=d["in.ts_tok"].to(DEV))
+
+    def run(side):
+        old = T._TEXT_STREAM
+        T._TEXT_STREAM = side
+        try:
+            with torch.no_grad():
+                return model(**kw).sample.clone()
+        finally:
+            T._TEXT_STREAM = old
+
+    cold = run(True)  # cold caches, built inside the side-stream forward
+    assert torch.equal(cold, run(False))
+    g = torch.Generator(device=DEV).manual_seed(5)
+    for n, p in model.named_parameters():
+        if "lora_B" in n:  # in-place update that torch's version counter does not see
+            p.data.copy_(torch.randn(p.shape, generator=g, device=DEV) * 0.05)
+    ops.bump_weight_generation()
+    a = run(True)
+    b = run(False)
+    assert not torch.equal(a, cold)
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("flags", [(True, False, 1.0, False), (True, True, 1.0, False),
                                    (True, True, 0.7, False), (True, True, 0.7, True),
                                    (False, True, 0.7, False), (False, False, 1.0, False)])

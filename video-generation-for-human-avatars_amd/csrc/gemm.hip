@@ -19,171 +19,12 @@
 
 #include "common.h"
 #include "ltx_hip.h"
+#include "gemm_common.h"
 
 namespace ltx {
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int GEMM_THREADS = 256;
-constexpr int TILE_BYTES = BM * BK * 2;           // 16 KiB per operand tile
-constexpr int STAGE_BYTES = 2 * TILE_BYTES;       // A + W
-constexpr int C_STRIDE = BN * 2 + 8;              // bf16 C image row stride (bytes), 8-B aligned
-constexpr int LDS_BYTES = (2 * STAGE_BYTES > BM * C_STRIDE) ? 2 * STAGE_BYTES : BM * C_STRIDE;
-
-struct GemmParams {
-  const bf16_t* A;  // [M, K] activations, row stride lda
-  const bf16_t* W;  // [N, K] weights (or W^T for dgrad), row stride ldw
-  bf16_t* C;        // [M, N], row stride ldc
-  int64_t lda, ldw, ldc;
-  int M, N, K;
-  const bf16_t* bias;  // [N] or null
-  // epilogue auxiliaries (meaning per epilogue, see ltx_hip.h)
-  const void* aux0;
-  int64_t ld0;
-  const void* aux1;
-  int64_t ld1;
-  const void* aux2;
-  int64_t ld2;
-  float alpha;
-  int rank;
-  int rows_per_batch;
-  // optional K extension (LoRA fused into the K loop): C += A2[M,K2] . W2[N,K2]^T
-  const bf16_t* A2;
-  const bf16_t* W2;
-  int64_t lda2, ldw2;
-  int K2;
-  // split-K (small grids): S partial f32 tiles [S][M][N] in a caller-provided workspace, summed by
-  // splitk_epilogue_kernel which then applies bias + the epilogue
-  float* ws;
-  int splitk;
-};
-
-__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds(gsrc, LDS_PTR(lds_wave_base), 16, 0, 0);
-}
-
-// byte offset of (row, logical 16-B chunk) inside a [128][64] bf16 swizzled tile image
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
-
-__device__ __forceinline__ void block_to_tile(int bid, int ntm, int ntn, int& tm, int& tn) {
-  const int nwg = ntm * ntn;
-  // bijective XCD remap: blocks dealt round-robin over 8 XCDs -> give each XCD a contiguous range
-  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  // grouped raster: 8 row-tiles share each W column panel
-  const int GROUP = 8;
-  const int group = wg / (GROUP * ntn);
-  const int first = group * GROUP;
-  const int gsize = min(ntm - first, GROUP);
-  tm = first + (wg % (GROUP * ntn)) % gsize;
-  tn = (wg % (GROUP * ntn)) / gsize;
-}
-
-template <int EPI, int R>
-__device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0, const bf16_t* cvals,
-                                              float* out8) {
-  // cvals: 8 bf16 of bf16(acc [+ bias]) for columns n0..n0+7 of row m
-  float v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = bf2f(cvals[j]);
-  if constexpr (EPI == LTX_EPI_STORE) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) out8[j] = v[j];
-  } else if constexpr (EPI == LTX_EPI_GELU) {
-    // aux0: optional pre-activation store (bf16, ld0) for the backward
-    if (p.aux0) {
-      u32x4 pk;
-      pk[0] = (unsigned)cvals[0] | ((unsigned)cvals[1] << 16);
-      pk[1] = (unsigned)cvals[2] | ((unsigned)cvals[3] << 16);
-      pk[2] = (unsigned)cvals[4] | ((unsigned)cvals[5] << 16);
-      pk[3] = (unsigned)cvals[6] | ((unsigned)cvals[7] << 16);
-      *(u32x4*)((bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0) = pk;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const f32x2 g = gelu_tanh_pk((f32x2){v[j], v[j + 1]});
-      out8[j] = g[0];
-      out8[j + 1] = g[1];
-    }
-  } else if constexpr (EPI == LTX_EPI_GATED_RESIDUAL) {
-    // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1);
-    // aux2 (optional, ld2): store of the pre-gate y (the gate's gradient in train_mode='full')
-    if (p.aux2) {
-      u32x4 pk;
-      pk[0] = (unsigned)cvals[0] | ((unsigned)cvals[1] << 16);
-      pk[1] = (unsigned)cvals[2] | ((unsigned)cvals[3] << 16);
-      pk[2] = (unsigned)cvals[4] | ((unsigned)cvals[5] << 16);
-      pk[3] = (unsigned)cvals[6] | ((unsigned)cvals[7] << 16);
-      *(u32x4*)((bf16_t*)p.aux2 + (int64_t)m * p.ld2 + n0) = pk;
-    }
-    const int b = m / p.rows_per_batch;
-    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
-    const u32x4 g4 = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)b * p.ld1 + n0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float r = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16)));
-      const float g = bf2f((bf16_t)(g4[j >> 1] >> ((j & 1) * 16)));
-      out8[j] = r + rbf(g * v[j]);
-    }
-  } else if constexpr (EPI == LTX_EPI_LORA || EPI == LTX_EPI_LORA_RESIDUAL) {
-    // peft: y = bf16(bf16(base) + alpha * U[m,:] . Lb[n,:]), U = aux1 f32 [M,rank] (ld1),
-    // Lb = aux2 f32 [N,rank] (ld2). LORA_RESIDUAL adds R = aux0 afterwards (bf16 add).
-    const float* u = (const float*)p.aux1 + (int64_t)m * p.ld1;
-    float ur[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) ur[r] = u[r];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float* lb = (const float*)p.aux2 + (int64_t)(n0 + j) * p.ld2;
-      float s = 0.f;
-#pragma unroll
-      for (int r = 0; r < R; ++r) s = fmaf(ur[r], lb[r], s);
-      out8[j] = v[j] + s * p.alpha;
-    }
-    if constexpr (EPI == LTX_EPI_LORA_RESIDUAL) {
-      const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + rbf(out8[j]);
-    }
-  } else if constexpr (EPI == LTX_EPI_GELU_BWD) {
-    // dF = bf16(bf16(acc) * gelu'(F)), F = aux0 pre-activation bf16 (ld0)
-    const u32x4 f4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const f32x2 f = {bf2f((bf16_t)f4[j >> 1]), bf2f((bf16_t)(f4[j >> 1] >> 16))};
-      const f32x2 g = (f32x2){v[j], v[j + 1]} * gelu_tanh_grad_pk(f);
-      out8[j] = g[0];
-      out8[j + 1] = g[1];
-    }
-  } else if constexpr (EPI == LTX_EPI_ACCUM) {
-    // out = R + bf16(acc): R = aux0 (ld0); C may alias R
-    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + v[j];
-  } else if constexpr (EPI == LTX_EPI_LORA_DGRAD_ACCUM) {
-    // out = [R +] bf16( bf16(acc) + bf16(alpha * Wd[m,:] . A[:,n]) ), Wd = aux1 f32 [M,rank]
-    // (ld1), A = aux2 f32 [rank, N] (ld2 = row stride of A), R = aux0 optional (ld0)
-    const float* w = (const float*)p.aux1 + (int64_t)m * p.ld1;
-    float wr[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) wr[r] = w[r];
-    float lo[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) lo[j] = 0.f;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const float* a = (const float*)p.aux2 + (int64_t)r * p.ld2 + n0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) lo[j] = fmaf(wr[r], a[j], lo[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) out8[j] = v[j] + rbf(lo[j] * p.alpha);
-    if (p.aux0) {
-      const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + rbf(out8[j]);
-    }
-  }
-}
+constexpr int WT2 = BN2 * BK * 2;  // W tile bytes of the 256-wide kernels (32 KiB)
+constexpr int LDS2 = (2 * (BM2 + BN2) * BK * 2 > BM2 * C_STRIDE2) ? 2 * (BM2 + BN2) * BK * 2 : BM2 * C_STRIDE2;
 
 // NST = LDS stages: 2 (one K-tile in flight while the other computes) or 3 / 4 (NST - 1 in
 // flight; for grids of at most one workgroup per CU, whose few K-tiles per workgroup are
@@ -399,321 +240,6 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p
   pk[2] = pack2(o[4], o[5]);
   pk[3] = pack2(o[6], o[7]);
   *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Large-tile kernel: 256 (m) x 256 (n) output tile, BK = 64, 512 threads = 8 waves as 4 (m) x 2
-// (n), each wave 64 m x 128 n = 4 x 8 tiles of v_mfma_f32_16x16x32_bf16 (128 accumulator VGPRs).
-// One workgroup per CU: two 64 KiB stages (X[256][64] + W[256][64] swizzled bf16), 131 FLOP per
-// staged byte (vs 87 for 256x128), which keeps the L2 demand near 11 TB/s at 1.5 PF.
-// Per K-tile a wave runs 4 quarters Q=(k-half h, n-half nh) of 16 MFMAs; every quarter first
-// issues the ds_reads of the NEXT quarter (A = W fragments per quarter, B = X fragments per
-// k-half), so LDS latency always hides under 16 MFMAs. Between Q2 and Q3 all reads of tile t are
-// done: counted wait (tile t+1 landed) + lgkmcnt(0) + raw s_barrier in one asm statement, then
-// tile t+2 is DMA'd into tile t's stage while Q3 computes from registers. All LDS is one dynamic
-// array, so hipcc never adds a vmcnt(0) before the ds_reads.
-// ---------------------------------------------------------------------------------------------
-constexpr int BM2 = 256, BN2 = 256;
-constexpr int XT2 = BM2 * BK * 2;   // 32 KiB
-constexpr int WT2 = BN2 * BK * 2;   // 32 KiB
-constexpr int ST2 = XT2 + WT2;      // 64 KiB per stage
-constexpr int C_STRIDE2 = BN2 * 2 + 8;
-constexpr int LDS2 = (2 * ST2 > BM2 * C_STRIDE2) ? 2 * ST2 : BM2 * C_STRIDE2;
-
-// VAR bit 0: split the tile-(t+2) DMA issue over Q3 (X) and the next Q0 (W); bit 1: static
-// priority (waves 4-7 at s_setprio 1 for the whole loop, no per-quarter flips;
-// MI355X_MICROARCH.md "Two waves per SIMD" item 4).
-template <int EPI, int R, int VAR>
-__global__ __launch_bounds__(512, 1) void gemm_nt_kernel_l(const GemmParams p) {
-  constexpr bool SPLIT = (VAR & 1) != 0;
-  constexpr bool SPRIO = (VAR & 2) != 0;
-  constexpr bool DBG_NODMA = (VAR & 4) != 0;   // measurement only (wrong results): no DMA past the prologue
-  constexpr bool DBG_NOBAR = (VAR & 8) != 0;   // measurement only: and no mid-loop wait/barrier
-  constexpr bool DBG_NOWAIT = (VAR & 16) != 0; // measurement only: DMA issued, never waited for in the loop
-  constexpr bool ASMDMA = (VAR & 32) != 0;     // scalar-base + 32-bit offset LDS-DMA (inline asm)
-  constexpr bool INTERLEAVE = ASMDMA && SPLIT && (VAR & 64) != 0;  // one DMA piece per 4 MFMAs
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int ntm = (p.M + BM2 - 1) / BM2, ntn = (p.N + BN2 - 1) / BN2;
-  int tm, tn;
-  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
-  const int m0 = tm * BM2, n0 = tn * BN2;
-
-  // DMA: wave w moves rows [32w, 32w+32) of the X tile and of the W tile (4 + 4 x 1 KiB)
-  const int lrow = lane >> 3;
-  const int pchunk = lane & 7;
-  const int nk_main = p.K / BK;
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-  // ASMDMA: global_load_lds_dwordx4 with a scalar (per-block, per-K-tile) base and a per-lane
-  // 32-bit offset (row clamp + source-side swizzle), M0 written in the same asm statement: one
-  // SALU add pair + the DMA per piece instead of 64-bit VALU address math + v_readfirstlane.
-  uint32_t xo[4], wo[4];
-  const char* xb = nullptr;
-  const char* wb = nullptr;
-  auto set_x = [&](bool ext) {
-    const int64_t ld = ext ? p.lda2 : p.lda;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (wave * 4 + i) * 8 + lrow;
-      xo[i] = (uint32_t)(((int64_t)(min(m0 + row, p.M - 1) - m0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
-    }
-    xb = (const char*)(ext ? p.A2 : p.A) + (int64_t)m0 * ld * 2;
-  };
-  auto set_w = [&](bool ext) {
-    const int64_t ld = ext ? p.ldw2 : p.ldw;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (wave * 4 + i) * 8 + lrow;
-      wo[i] = (uint32_t)(((int64_t)(min(n0 + row, p.N - 1) - n0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
-    }
-    wb = (const char*)(ext ? p.W2 : p.W) + (int64_t)n0 * ld * 2;
-  };
-  const uint32_t lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-  auto glds_s = [&](uint32_t voff, const char* sbase, uint32_t lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
-  };
-  const bf16_t* xsrc[4];
-  const bf16_t* wsrc[4];
-  if constexpr (ASMDMA) {
-    set_x(nk_main == 0);
-    set_w(nk_main == 0);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (wave * 4 + i) * 8 + lrow;
-      xsrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + ((pchunk ^ (row & 7)) * 8);
-      wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.ldw + ((pchunk ^ (row & 7)) * 8);
-    }
-  }
-  // K-extension tiles (LoRA fused into the K loop) read A2/W2 instead of A/W
-  auto xptr = [&](int i, int kt) -> const bf16_t* {
-    if (kt < nk_main) return xsrc[i] + kt * BK;
-    const int row = (wave * 4 + i) * 8 + lrow;
-    return p.A2 + (int64_t)min(m0 + row, p.M - 1) * p.lda2 + (kt - nk_main) * BK + ((pchunk ^ (row & 7)) * 8);
-  };
-  auto wptr = [&](int i, int kt) -> const bf16_t* {
-    if (kt < nk_main) return wsrc[i] + kt * BK;
-    const int row = (wave * 4 + i) * 8 + lrow;
-    return p.W2 + (int64_t)min(n0 + row, p.N - 1) * p.ldw2 + (kt - nk_main) * BK + ((pchunk ^ (row & 7)) * 8);
-  };
-  auto stage_x = [&](int st, int kt) {
-    if constexpr (ASMDMA) {
-      if (kt == nk_main && nk_main > 0) set_x(true);  // ext tiles come last, in issue order
-      const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-      const uint32_t l = lds0 + st * ST2 + wv * 4096;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds_s(xo[i], sb, l + i * 1024);
-    } else {
-      char* base = smem + st * ST2;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds16(xptr(i, kt), base + (wave * 4 + i) * 1024);
-    }
-  };
-  auto stage_w = [&](int st, int kt) {
-    if constexpr (ASMDMA) {
-      if (kt == nk_main && nk_main > 0) set_w(true);
-      const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-      const uint32_t l = lds0 + st * ST2 + XT2 + wv * 4096;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds_s(wo[i], sb, l + i * 1024);
-    } else {
-      char* base = smem + st * ST2;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) glds16(wptr(i, kt), base + XT2 + (wave * 4 + i) * 1024);
-    }
-  };
-  // one 1 KiB piece of a stage (ASMDMA): INTERLEAVE spreads a stage's 4 pieces between MFMA rows
-  auto piece_x = [&](int st, int kt, int i) {
-    if (i == 0 && kt == nk_main && nk_main > 0) set_x(true);
-    const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-    glds_s(xo[i], sb, lds0 + st * ST2 + wv * 4096 + i * 1024);
-  };
-  auto piece_w = [&](int st, int kt, int i) {
-    if (i == 0 && kt == nk_main && nk_main > 0) set_w(true);
-    const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-    glds_s(wo[i], sb, lds0 + st * ST2 + XT2 + wv * 4096 + i * 1024);
-  };
-  auto stage = [&](int st, int kt) {
-    stage_x(st, kt);
-    stage_w(st, kt);
-  };
-
-  const int wm = wave >> 1, wn = wave & 1;
-  f32x4 acc[8][4];  // [n-tile][m-tile]
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  const int frow = lane & 15;
-  const int fchunk = lane >> 4;
-  // A (W) fragment offsets per quarter q = 2h + nh, B (X) offsets per k-half h
-  int aoff[4][4], boff[2][4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      boff[h][i] = swz(wm * 64 + i * 16 + frow, h * 4 + fchunk);
-#pragma unroll
-      for (int nh = 0; nh < 2; ++nh) aoff[2 * h + nh][i] = XT2 + swz(wn * 128 + nh * 64 + i * 16 + frow, h * 4 + fchunk);
-    }
-  const int nk = nk_main + p.K2 / BK;
-  stage(0, 0);
-  if (nk > 1) {
-    stage(1, 1);
-    asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-  s16x8 aE[4], aO[4], b0[4], b1[4];  // A even/odd quarter sets, B per k-half
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    aE[i] = *(const s16x8*)(smem + aoff[0][i]);
-    b0[i] = *(const s16x8*)(smem + boff[0][i]);
-  }
-#define LTX_MFMA_Q(AS, BS, NH)                                                                        \
-  __builtin_amdgcn_sched_barrier(0);                                                                  \
-  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(1);                                                \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
-  _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
-    acc[(NH) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * 4 + i][j], 0, 0, 0); \
-  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(0);                                                \
-  __builtin_amdgcn_sched_barrier(0);
-#define LTX_MFMA_QI(AS, BS, NH, PIECE)                                                                \
-  __builtin_amdgcn_sched_barrier(0);                                                                  \
-  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(1);                                                \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                     \
-    _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                     \
-      acc[(NH) * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * 4 + i][j], 0, 0, 0); \
-    __builtin_amdgcn_sched_barrier(0);                                                                \
-    PIECE(i);                                                                                         \
-    __builtin_amdgcn_sched_barrier(0);                                                                \
-  }                                                                                                   \
-  if constexpr (!SPRIO) __builtin_amdgcn_s_setprio(0);                                                \
-  __builtin_amdgcn_sched_barrier(0);
-  if constexpr (SPRIO) {
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-  }
-
-  int cur = 0;
-  bool pend_w = false;  // SPLIT: W half of tile kt+1's DMA still to issue in Q0
-  for (int kt = 0; kt < nk; ++kt) {
-    const char* st = smem + cur * ST2;
-    // Q0 (h0, n0): prefetch A(Q1)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) aO[i] = *(const s16x8*)(st + aoff[1][i]);
-    if constexpr (INTERLEAVE) {
-      const bool pw_on = pend_w;
-      auto pw = [&](int i) {
-        if (pw_on) piece_w(cur ^ 1, kt + 1, i);
-      };
-      LTX_MFMA_QI(aE, b0, 0, pw)
-      pend_w = false;
-    } else {
-      if (SPLIT && pend_w && !DBG_NODMA) {
-        stage_w(cur ^ 1, kt + 1);
-        pend_w = false;
-      }
-      LTX_MFMA_Q(aE, b0, 0)
-    }
-    // Q1 (h0, n1): prefetch A(Q2), B(h1)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      aE[i] = *(const s16x8*)(st + aoff[2][i]);
-      b1[i] = *(const s16x8*)(st + boff[1][i]);
-    }
-    LTX_MFMA_Q(aO, b0, 1)
-    // Q2 (h1, n0): prefetch A(Q3)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) aO[i] = *(const s16x8*)(st + aoff[3][i]);
-    LTX_MFMA_Q(aE, b1, 0)
-    // all reads of tile t issued: wait tile t+1, free tile t's stage, DMA tile t+2 into it
-    if (kt + 1 < nk) {
-      if constexpr (DBG_NOBAR)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      else if constexpr (DBG_NOWAIT)
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (kt + 2 < nk && !DBG_NODMA) {
-        if (INTERLEAVE) {
-          pend_w = true;  // X pieces go out between Q3's MFMA rows below, W in Q0
-        } else if (SPLIT) {
-          stage_x(cur, kt + 2);
-          pend_w = true;
-        } else {
-          stage(cur, kt + 2);
-        }
-      }
-      const char* sn = smem + (cur ^ 1) * ST2;
-      // Q3 (h1, n1) of tile t: prefetch A(Q0), B(h0) of tile t+1
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        aE[i] = *(const s16x8*)(sn + aoff[0][i]);
-        b0[i] = *(const s16x8*)(sn + boff[0][i]);
-      }
-    }
-    if constexpr (INTERLEAVE) {
-      const bool px_on = kt + 2 < nk;
-      auto px = [&](int i) {
-        if (px_on) piece_x(cur, kt + 2, i);
-      };
-      LTX_MFMA_QI(aO, b1, 1, px)
-    } else {
-      LTX_MFMA_Q(aO, b1, 1)
-    }
-    cur ^= 1;
-  }
-#undef LTX_MFMA_Q
-#undef LTX_MFMA_QI
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-
-  // epilogue stage 1: bf16(acc + bias) -> LDS image [256 m][256 n]
-  char* cimg = smem;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int nl = wn * 128 + i * 16 + (lane >> 4) * 4;
-    float b4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias) {
-      const int gn = n0 + nl;
-      if (gn + 3 < p.N) {
-        const u32x2 bb = *(const u32x2*)(p.bias + gn);
-        b4[0] = bf2f((bf16_t)bb[0]); b4[1] = bf2f((bf16_t)(bb[0] >> 16));
-        b4[2] = bf2f((bf16_t)bb[1]); b4[3] = bf2f((bf16_t)(bb[1] >> 16));
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int ml = wm * 64 + j * 16 + (lane & 15);
-      u32x2 pk;
-      pk[0] = pack2(acc[i][j][0] + b4[0], acc[i][j][1] + b4[1]);
-      pk[1] = pack2(acc[i][j][2] + b4[2], acc[i][j][3] + b4[3]);
-      *(u32x2*)(cimg + ml * C_STRIDE2 + nl * 2) = pk;
-    }
-  }
-  __syncthreads();
-  const int cgrp = tid & 31;
-  for (int rr = tid >> 5; rr < BM2; rr += 512 / 32) {
-    const int m = m0 + rr;
-    const int n = n0 + cgrp * 8;
-    if (m >= p.M || n >= p.N) continue;
-    const u32x2 lo = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16);
-    const u32x2 hi = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16 + 8);
-    bf16_t cv[8] = {(bf16_t)lo[0], (bf16_t)(lo[0] >> 16), (bf16_t)lo[1], (bf16_t)(lo[1] >> 16),
-                    (bf16_t)hi[0], (bf16_t)(hi[0] >> 16), (bf16_t)hi[1], (bf16_t)(hi[1] >> 16)};
-    float o[8];
-    epilogue_row8<EPI, R>(p, m, n, cv, o);
-    u32x4 pk;
-    pk[0] = pack2(o[0], o[1]);
-    pk[1] = pack2(o[2], o[3]);
-    pk[2] = pack2(o[4], o[5]);
-    pk[3] = pack2(o[6], o[7]);
-    *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -997,245 +523,6 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Ping-pong large-tile kernel: 256x256 tile, BK = 64, 8 waves in two groups G0 = waves 0-3 and
-// G1 = waves 4-7 (each SIMD holds one wave of each group). G1 runs one barrier behind G0, so on
-// every SIMD one wave computes (16 MFMAs) while its partner reads its LDS fragments and issues its
-// LDS-DMA (MI355X_MICROARCH.md "Two waves per SIMD"; cdna_hip_programming.md "The 256^2 8-phase
-// template"). A phase computes one 128x128 C quadrant of the block over the whole K-tile, each
-// wave a 64 (m) x 32 (n) piece of it. The quadrant order (0,0),(0,1),(1,1),(1,0) reuses fragments
-// from registers (X half 0 in phases 0-1, X half 1 in 2-3, W half 0 in 0 and 3, W half 1 in 1-2),
-// so each staged 16 KiB piece (X0, X1, W0, W1 of a K-tile) is read in ONE phase and refilled two
-// phases later: exactly one piece (2 DMA instructions per wave) per phase, issued 5-6 phases
-// before its first read; counted vmcnt (never 0 in the loop) + raw s_barrier.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ const char* sgpr_ptr(const char* ptr) {  // wave-uniform pointer -> SGPR pair
-  const uint64_t v = (uint64_t)ptr;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return (const char*)(((uint64_t)hi << 32) | lo);
-}
-
-constexpr int PIECE = 128 * BK * 2;  // 16 KiB: 128 rows x 64 k, swizzled like the 128x64 tiles
-constexpr int BUF_P = 4 * PIECE;     // one K-tile: [X0, X1, W0, W1]
-
-__device__ __forceinline__ void wait_vm_pieces(int n) {  // n = pieces allowed in flight (x2 DMA each)
-  switch (n) {
-    case 4: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-struct PPDma {
-  uint32_t xo[2][2], wo[2][2];    // main operands: per-lane byte offsets [half][j]
-  uint32_t xoe[2][2], woe[2][2];  // K-extension operands
-  const char* xb;
-  const char* wb;
-  const char* xbe;
-  const char* wbe;
-  uint32_t lds0;
-  int wv, nk_main;
-};
-
-__device__ __forceinline__ void pp_glds(uint32_t voff, const char* sbase, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
-}
-
-// piece T of K-tile kt: 0 X0, 1 W0, 2 W1, 3 X1 (the issue order within a K-tile)
-__device__ __forceinline__ void pp_issue(const PPDma& d, int kt, int T) {
-  const bool is_x = (T == 0 || T == 3);
-  const int h = (T == 0 || T == 1) ? 0 : 1;
-  const bool ext = kt >= d.nk_main;
-  const int kk = ext ? kt - d.nk_main : kt;
-  const char* base = is_x ? (ext ? d.xbe : d.xb) : (ext ? d.wbe : d.wb);
-  const char* sb = sgpr_ptr(base + kk * (BK * 2));
-  const int slot = is_x ? h : 2 + h;
-  const uint32_t l = (uint32_t)__builtin_amdgcn_readfirstlane(d.lds0 + (kt & 1) * BUF_P + slot * PIECE + d.wv * 2048);
-  uint32_t o0, o1;
-  if (is_x) {
-    o0 = ext ? (h ? d.xoe[1][0] : d.xoe[0][0]) : (h ? d.xo[1][0] : d.xo[0][0]);
-    o1 = ext ? (h ? d.xoe[1][1] : d.xoe[0][1]) : (h ? d.xo[1][1] : d.xo[0][1]);
-  } else {
-    o0 = ext ? (h ? d.woe[1][0] : d.woe[0][0]) : (h ? d.wo[1][0] : d.wo[0][0]);
-    o1 = ext ? (h ? d.woe[1][1] : d.woe[0][1]) : (h ? d.wo[1][1] : d.wo[0][1]);
-  }
-  pp_glds(o0, sb, l);
-  pp_glds(o1, sb, l + 1024);
-}
-
-template <int EPI, int R>
-__global__ __launch_bounds__(512, 1) void gemm_nt_kernel_p(const GemmParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-  const bool g1 = wv >= 4;
-  const int ntm = (p.M + BM2 - 1) / BM2, ntn = (p.N + BN2 - 1) / BN2;
-  int tm, tn;
-  block_to_tile(blockIdx.x, ntm, ntn, tm, tn);
-  const int m0 = tm * BM2, n0 = tn * BN2;
-  const int nk_main = __builtin_amdgcn_readfirstlane(p.K / BK);
-  const int nk = __builtin_amdgcn_readfirstlane(p.K / BK + p.K2 / BK);
-
-  // ---- DMA bookkeeping: wave w moves piece rows h*128 + 16w + 8j + (lane>>3), j = 0, 1
-  PPDma d;
-  {
-    const int lrow = lane >> 3, pchunk = lane & 7;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = h * 128 + wave * 16 + j * 8 + lrow;
-        const int sw = (pchunk ^ (row & 7)) * 8;
-        const int64_t xr = min(m0 + row, p.M - 1) - m0, wr = min(n0 + row, p.N - 1) - n0;
-        d.xo[h][j] = (uint32_t)((xr * p.lda + sw) * 2);
-        d.wo[h][j] = (uint32_t)((wr * p.ldw + sw) * 2);
-        d.xoe[h][j] = (uint32_t)((xr * p.lda2 + sw) * 2);
-        d.woe[h][j] = (uint32_t)((wr * p.ldw2 + sw) * 2);
-      }
-    d.xb = (const char*)p.A + (int64_t)m0 * p.lda * 2;
-    d.wb = (const char*)p.W + (int64_t)n0 * p.ldw * 2;
-    d.xbe = (const char*)p.A2 + (int64_t)m0 * p.lda2 * 2;
-    d.wbe = (const char*)p.W2 + (int64_t)n0 * p.ldw2 * 2;
-    d.lds0 = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)smem);
-    d.wv = wv;
-    d.nk_main = nk_main;
-  }
-  // phase q issues piece (q + 6) & 3 of K-tile (q + 6) >> 2 while that tile exists
-  auto issue_phase = [&](int q) {
-    const int kt = (q + 6) >> 2;
-    if (kt < nk) pp_issue(d, kt, (q + 6) & 3);
-  };
-  // pieces allowed in flight after phase q's issue: those of phases q-3..q that issued
-  auto inflight = [&](int q) { return min(4, max(0, 4 * nk - 6 - (q - 3))); };
-
-  const int wm = wave >> 2, wn = wave & 3;
-  const int frow = lane & 15, fchunk = lane >> 4;
-  f32x4 acc[4][2][4];  // [quadrant phase][n-frag j][m-frag i]
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[a][j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  s16x8 xf[4][2], wf0[2][2], wf1[2][2];  // [frag][k-step]
-  auto read_x = [&](const char* piece) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) xf[i][ks] = *(const s16x8*)(piece + swz(wm * 64 + i * 16 + frow, ks * 4 + fchunk));
-  };
-  auto read_w = [&](const char* piece, s16x8 (&wf)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) wf[j][ks] = *(const s16x8*)(piece + swz(wn * 32 + j * 16 + frow, ks * 4 + fchunk));
-  };
-#define LTX_PP_MFMA(QA, WF)                                                                           \
-  __builtin_amdgcn_sched_barrier(0);                                                                  \
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                  \
-  __builtin_amdgcn_s_setprio(1);                                                                      \
-  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                                    \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                       \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                       \
-    acc[QA][j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WF[j][ks], xf[i][ks], acc[QA][j][i], 0, 0, 0); \
-  __builtin_amdgcn_s_setprio(0);                                                                      \
-  __builtin_amdgcn_sched_barrier(0);
-#define LTX_PP_BAR() asm volatile("s_barrier" ::: "memory")
-
-  // ---- prologue: the pieces of phases -6..-1 (X0, W0, W1, X1 of tile 0; X0, W0 of tile 1)
-  for (int q = -6; q < 0; ++q) issue_phase(q);
-  wait_vm_pieces(inflight(-1));
-  LTX_PP_BAR();
-  if (g1) LTX_PP_BAR();  // the stagger: G1 runs one barrier behind G0
-
-  for (int t = 0; t < nk; ++t) {
-    const char* buf = smem + (t & 1) * BUF_P;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = 4 * t + r;
-      // load segment: this phase's fragments, then its DMA piece
-      if (r == 0) {
-        read_x(buf);
-        read_w(buf + 2 * PIECE, wf0);
-      } else if (r == 1) {
-        read_w(buf + 3 * PIECE, wf1);
-      } else if (r == 2) {
-        read_x(buf + PIECE);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      issue_phase(q);
-      if (g1) wait_vm_pieces(inflight(q));
-      LTX_PP_BAR();
-      // compute segment: quadrant r
-      if (r == 0) { LTX_PP_MFMA(0, wf0) }
-      else if (r == 1) { LTX_PP_MFMA(1, wf1) }
-      else if (r == 2) { LTX_PP_MFMA(2, wf1) }
-      else { LTX_PP_MFMA(3, wf0) }
-      if (!g1) wait_vm_pieces(inflight(q));
-      LTX_PP_BAR();
-    }
-  }
-  if (!g1) LTX_PP_BAR();  // match G1's stagger barrier
-#undef LTX_PP_MFMA
-#undef LTX_PP_BAR
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-
-  // epilogue stage 1: bf16(acc + bias) -> LDS image [256 m][256 n]
-  char* cimg = smem;
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int qm = (a >= 2) ? 1 : 0;
-    const int qn = (a == 1 || a == 2) ? 1 : 0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int nl = qn * 128 + wn * 32 + j * 16 + (lane >> 4) * 4;
-      float b4[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias) {
-        const int gn = n0 + nl;
-        if (gn + 3 < p.N) {
-          const u32x2 bb = *(const u32x2*)(p.bias + gn);
-          b4[0] = bf2f((bf16_t)bb[0]); b4[1] = bf2f((bf16_t)(bb[0] >> 16));
-          b4[2] = bf2f((bf16_t)bb[1]); b4[3] = bf2f((bf16_t)(bb[1] >> 16));
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ml = qm * 128 + wm * 64 + i * 16 + (lane & 15);
-        u32x2 pk;
-        pk[0] = pack2(acc[a][j][i][0] + b4[0], acc[a][j][i][1] + b4[1]);
-        pk[1] = pack2(acc[a][j][i][2] + b4[2], acc[a][j][i][3] + b4[3]);
-        *(u32x2*)(cimg + ml * C_STRIDE2 + nl * 2) = pk;
-      }
-    }
-  }
-  __syncthreads();
-  const int cgrp = tid & 31;
-  for (int rr = tid >> 5; rr < BM2; rr += 512 / 32) {
-    const int m = m0 + rr;
-    const int n = n0 + cgrp * 8;
-    if (m >= p.M || n >= p.N) continue;
-    const u32x2 lo = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16);
-    const u32x2 hi = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16 + 8);
-    bf16_t cv[8] = {(bf16_t)lo[0], (bf16_t)(lo[0] >> 16), (bf16_t)lo[1], (bf16_t)(lo[1] >> 16),
-                    (bf16_t)hi[0], (bf16_t)(hi[0] >> 16), (bf16_t)hi[1], (bf16_t)(hi[1] >> 16)};
-    float o[8];
-    epilogue_row8<EPI, R>(p, m, n, cv, o);
-    u32x4 pk;
-    pk[0] = pack2(o[0], o[1]);
-    pk[1] = pack2(o[2], o[3]);
-    pk[2] = pack2(o[4], o[5]);
-    pk[3] = pack2(o[6], o[7]);
-    *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
-  }
-}
-
 static int g_force_small = -1;  // LTX_GEMM_SMALL=1 forces the 128x128 kernel (A/B tests)
 // LDS stages of the 128x128 kernel: 0 = auto (3 when the grid is at most one round), 2..4 forced
 // (LTX_GEMM_SMALL_STAGES, A/B tests)
@@ -1258,11 +545,8 @@ static SplitWs ws_for(hipStream_t s) {
   auto it = g_ws_stream.find(s);
   return it != g_ws_stream.end() ? it->second : g_ws_default;
 }
-static void* g_stamps = nullptr;  // diagnostic stamp buffer (variants 19/20)
-static int g_variant = 0;       // tuning knob (ltx_gemm_set_variant): 0 default (t-kernel, auto tile height),
-                                // 1 single burst, 2 split + static prio, 8/9 asm DMA (+prio), 10 builtin split,
-                                // 11 ping-pong, 12 interleaved DMA, 13/14/15 t-kernel 256/224/auto,
-                                // 16 l-kernel default of before; 4-7 measurement-only (wrong results)
+static int g_variant = 0;  // tuning knob (ltx_gemm_set_variant): 0 default, 13 / 14 t-kernel with 256 / 224-row
+                           // tiles, 30 / 31 / 32 w4 kernel (auto / 256 / 224-row tiles)
 
 template <int EPI, int R = 0>
 static int launch(const GemmParams& p, hipStream_t s) {
@@ -1305,100 +589,28 @@ static int launch(const GemmParams& p, hipStream_t s) {
     }
   }
   if (!g_force_small && p.M >= BM2 && (big_tiles >= 256 || (g_variant == 0 && tiles224 >= 160))) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 33>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 35>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 99>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-      attr_set = true;
+    const int64_t ntn = (p.N + BN2 - 1) / BN2;
+    const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
+    // fraction of the last round of 256 CUs that has work, per tile height
+    auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
+    if (g_variant >= 33 && g_variant <= 36) return launch_w4(EPI, 32 - g_variant, p, s);  // measurement
+    if (g_variant >= 30 && g_variant <= 32) {  // one-wave-per-SIMD kernel: 30 auto, 31 BMT 256, 32 BMT 224
+      const bool use224 = g_variant == 32 || (g_variant == 30 && fill(t224) > fill(t256) + 0.02);
+      return launch_w4(EPI, use224 ? 224 : 256, p, s);
     }
-    if constexpr (EPI == LTX_EPI_STORE && R == 0) {
-      if (g_variant == 19 || g_variant == 20) {  // stamp diagnostics (19: 224-row, 20: 256-row tiles)
-        if (!g_stamps) return fail(LTX_ERR_BAD_ARG, "gemm variant 19/20: ltx_gemm_set_stamps first");
-        GemmParams q = p;
-        q.ws = (float*)g_stamps;
-        const int64_t ntn = (p.N + BN2 - 1) / BN2;
-        if (g_variant == 19) {
-          (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4, 1>), dim3((unsigned)(((p.M + 223) / 224) * ntn)), dim3(512), LDS2, s, q);
-        } else {
-          (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 1>), dim3((unsigned)(((p.M + 255) / 256) * ntn)), dim3(512), LDS2, s, q);
-        }
-        LTX_LAUNCH_CHECK();
-        return LTX_OK;
-      }
+    // gemm_nt_kernel_t with the tile height that fills the last round best; 13 forces BMT 256,
+    // 14 forces BMT 224
+    static bool t_set = false;
+    if (!t_set) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      t_set = true;
     }
-    if (g_variant == 16)  // previous default: l-kernel, asm DMA, split issue, static priority
-      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant == 0 || (g_variant >= 13 && g_variant <= 15) || g_variant == 17) {
-      // default (0 = 15): gemm_nt_kernel_t with the tile height that fills the last round best;
-      // 13 forces BMT 256, 14 forces BMT 224
-      static bool t_set = false;
-      if (!t_set) {
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        t_set = true;
-      }
-      const int64_t ntn = (p.N + BN2 - 1) / BN2;
-      const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
-      // fraction of the last round of 256 CUs that has work, per tile height
-      auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
-      const bool use224 = g_variant == 14 || ((g_variant == 15 || g_variant == 0 || g_variant == 17) &&
-                                              fill(t224) > fill(t256) + 0.02);
-      if (g_variant == 17) {  // DMA issued by waves 0-3 only
-        if (use224)
-          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
-        else
-          hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 4>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
-      } else if (use224) {  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
-        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
-      } else {
-        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
-      }
-    }
-    else if (g_variant == 11) {  // ping-pong 8-phase kernel
-      static bool pp_set = false;
-      if (!pp_set) {
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_p<EPI, R>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        pp_set = true;
-      }
-      hipLaunchKernelGGL((gemm_nt_kernel_p<EPI, R>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    } else if (g_variant == 10)  // previous default: builtin DMA, split issue
-      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 1>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant == 2)
-      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 3>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant == 8)
-      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 33>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant == 9)
-      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 35>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant == 12)  // asm DMA pieces interleaved between MFMA rows
-      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 99>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-    else if (g_variant >= 4) {
-      if constexpr (EPI == LTX_EPI_STORE && R == 0) {  // measurement-only variants
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 13>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 17>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_l<EPI, R, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-        if (g_variant == 4)
-          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 5>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-        else if (g_variant == 6)
-          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 17>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-        else if (g_variant == 7)
-          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 16>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-        else
-          hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 13>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
-      } else {
-        return fail(LTX_ERR_BAD_ARG, "gemm: measurement variants exist for the plain store epilogue only");
-      }
-    }
+    const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
+    if (use224)  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
+      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel_l<EPI, R, 0>), dim3((unsigned)big_tiles), dim3(512), LDS2, s, p);
+      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
   } else {
     const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
     const int tiles = ntm * ntn;
@@ -1468,11 +680,6 @@ extern "C" int ltx_gemm_set_variant(int variant) {
   return LTX_OK;
 }
 
-// diagnostic: stamp buffer of 8 u64 per workgroup for variants 19/20 (not in ltx_hip.h: tooling only)
-extern "C" int ltx_gemm_set_stamps(void* ptr) {
-  g_stamps = ptr;
-  return LTX_OK;
-}
 
 extern "C" int ltx_gemm_set_workspace(void* ptr, int64_t bytes) {
   LTX_CHECK_ARG(bytes >= 0 && (ptr != nullptr || bytes == 0) && ((uintptr_t)ptr % 16) == 0,

@@ -1,0 +1,177 @@
+// Shared pieces of the bf16 GEMM kernels (gemm.hip, gemm_w4.hip): parameters, block order,
+// fused epilogues.
+#pragma once
+#include "common.h"
+#include "ltx_hip.h"
+
+namespace ltx {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int GEMM_THREADS = 256;
+constexpr int TILE_BYTES = BM * BK * 2;           // 16 KiB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;       // A + W
+constexpr int C_STRIDE = BN * 2 + 8;              // bf16 C image row stride (bytes), 8-B aligned
+constexpr int LDS_BYTES = (2 * STAGE_BYTES > BM * C_STRIDE) ? 2 * STAGE_BYTES : BM * C_STRIDE;
+
+struct GemmParams {
+  const bf16_t* A;  // [M, K] activations, row stride lda
+  const bf16_t* W;  // [N, K] weights (or W^T for dgrad), row stride ldw
+  bf16_t* C;        // [M, N], row stride ldc
+  int64_t lda, ldw, ldc;
+  int M, N, K;
+  const bf16_t* bias;  // [N] or null
+  // epilogue auxiliaries (meaning per epilogue, see ltx_hip.h)
+  const void* aux0;
+  int64_t ld0;
+  const void* aux1;
+  int64_t ld1;
+  const void* aux2;
+  int64_t ld2;
+  float alpha;
+  int rank;
+  int rows_per_batch;
+  // optional K extension (LoRA fused into the K loop): C += A2[M,K2] . W2[N,K2]^T
+  const bf16_t* A2;
+  const bf16_t* W2;
+  int64_t lda2, ldw2;
+  int K2;
+  // split-K (small grids): S partial f32 tiles [S][M][N] in a caller-provided workspace, summed by
+  // splitk_epilogue_kernel which then applies bias + the epilogue
+  float* ws;
+  int splitk;
+};
+
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(gsrc, LDS_PTR(lds_wave_base), 16, 0, 0);
+}
+
+// byte offset of (row, logical 16-B chunk) inside a [128][64] bf16 swizzled tile image
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+__device__ __forceinline__ void block_to_tile(int bid, int ntm, int ntn, int& tm, int& tn) {
+  const int nwg = ntm * ntn;
+  // bijective XCD remap: blocks dealt round-robin over 8 XCDs -> give each XCD a contiguous range
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8, idx = bid / 8;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  // grouped raster: 8 row-tiles share each W column panel
+  const int GROUP = 8;
+  const int group = wg / (GROUP * ntn);
+  const int first = group * GROUP;
+  const int gsize = min(ntm - first, GROUP);
+  tm = first + (wg % (GROUP * ntn)) % gsize;
+  tn = (wg % (GROUP * ntn)) / gsize;
+}
+
+template <int EPI, int R>
+__device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0, const bf16_t* cvals,
+                                              float* out8) {
+  // cvals: 8 bf16 of bf16(acc [+ bias]) for columns n0..n0+7 of row m
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(cvals[j]);
+  if constexpr (EPI == LTX_EPI_STORE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out8[j] = v[j];
+  } else if constexpr (EPI == LTX_EPI_GELU) {
+    // aux0: optional pre-activation store (bf16, ld0) for the backward
+    if (p.aux0) {
+      u32x4 pk;
+      pk[0] = (unsigned)cvals[0] | ((unsigned)cvals[1] << 16);
+      pk[1] = (unsigned)cvals[2] | ((unsigned)cvals[3] << 16);
+      pk[2] = (unsigned)cvals[4] | ((unsigned)cvals[5] << 16);
+      pk[3] = (unsigned)cvals[6] | ((unsigned)cvals[7] << 16);
+      *(u32x4*)((bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0) = pk;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 g = gelu_tanh_pk((f32x2){v[j], v[j + 1]});
+      out8[j] = g[0];
+      out8[j + 1] = g[1];
+    }
+  } else if constexpr (EPI == LTX_EPI_GATED_RESIDUAL) {
+    // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1);
+    // aux2 (optional, ld2): store of the pre-gate y (the gate's gradient in train_mode='full')
+    if (p.aux2) {
+      u32x4 pk;
+      pk[0] = (unsigned)cvals[0] | ((unsigned)cvals[1] << 16);
+      pk[1] = (unsigned)cvals[2] | ((unsigned)cvals[3] << 16);
+      pk[2] = (unsigned)cvals[4] | ((unsigned)cvals[5] << 16);
+      pk[3] = (unsigned)cvals[6] | ((unsigned)cvals[7] << 16);
+      *(u32x4*)((bf16_t*)p.aux2 + (int64_t)m * p.ld2 + n0) = pk;
+    }
+    const int b = m / p.rows_per_batch;
+    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    const u32x4 g4 = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)b * p.ld1 + n0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float r = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16)));
+      const float g = bf2f((bf16_t)(g4[j >> 1] >> ((j & 1) * 16)));
+      out8[j] = r + rbf(g * v[j]);
+    }
+  } else if constexpr (EPI == LTX_EPI_LORA || EPI == LTX_EPI_LORA_RESIDUAL) {
+    // peft: y = bf16(bf16(base) + alpha * U[m,:] . Lb[n,:]), U = aux1 f32 [M,rank] (ld1),
+    // Lb = aux2 f32 [N,rank] (ld2). LORA_RESIDUAL adds R = aux0 afterwards (bf16 add).
+    const float* u = (const float*)p.aux1 + (int64_t)m * p.ld1;
+    float ur[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) ur[r] = u[r];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float* lb = (const float*)p.aux2 + (int64_t)(n0 + j) * p.ld2;
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) s = fmaf(ur[r], lb[r], s);
+      out8[j] = v[j] + s * p.alpha;
+    }
+    if constexpr (EPI == LTX_EPI_LORA_RESIDUAL) {
+      const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + rbf(out8[j]);
+    }
+  } else if constexpr (EPI == LTX_EPI_GELU_BWD) {
+    // dF = bf16(bf16(acc) * gelu'(F)), F = aux0 pre-activation bf16 (ld0)
+    const u32x4 f4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 f = {bf2f((bf16_t)f4[j >> 1]), bf2f((bf16_t)(f4[j >> 1] >> 16))};
+      const f32x2 g = (f32x2){v[j], v[j + 1]} * gelu_tanh_grad_pk(f);
+      out8[j] = g[0];
+      out8[j + 1] = g[1];
+    }
+  } else if constexpr (EPI == LTX_EPI_ACCUM) {
+    // out = R + bf16(acc): R = aux0 (ld0); C may alias R
+    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + v[j];
+  } else if constexpr (EPI == LTX_EPI_LORA_DGRAD_ACCUM) {
+    // out = [R +] bf16( bf16(acc) + bf16(alpha * Wd[m,:] . A[:,n]) ), Wd = aux1 f32 [M,rank]
+    // (ld1), A = aux2 f32 [rank, N] (ld2 = row stride of A), R = aux0 optional (ld0)
+    const float* w = (const float*)p.aux1 + (int64_t)m * p.ld1;
+    float wr[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) wr[r] = w[r];
+    float lo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lo[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float* a = (const float*)p.aux2 + (int64_t)r * p.ld2 + n0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) lo[j] = fmaf(wr[r], a[j], lo[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out8[j] = v[j] + rbf(lo[j] * p.alpha);
+    if (p.aux0) {
+      const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + rbf(out8[j]);
+    }
+  }
+}
+
+constexpr int BM2 = 256, BN2 = 256;
+constexpr int C_STRIDE2 = BN2 * 2 + 8;  // bf16 C image row stride of the 256-wide tiles
+
+int launch_w4(int epi, int bmt, const GemmParams& p, hipStream_t s);  // gemm_w4.hip
+
+}  // namespace ltx

@@ -1052,8 +1052,6 @@ class Transformer3DModel(nn.Module):
             # M = L GEMM, LoRA and norm launches fill CUs the main stream leaves idle)
             side = _side_stream(h.device)
             main = torch.cuda.current_stream()
-            ready = torch.cuda.Event()
-            ready.record(main)
             sh.text_pre = {}
 
             def prep(j):
@@ -1063,6 +1061,10 @@ class Transformer3DModel(nn.Module):
                     lj = _lora_params(bj)
                     if lj is not None:
                         _kv_ext(bj, lj[1], lj[2])
+                # the side stream starts only after everything main has enqueued so far: enc2 and
+                # the caches just (re)built above (cold cache, or after an optimizer step)
+                ready = torch.cuda.Event()
+                ready.record(main)
                 with torch.no_grad(), torch.cuda.stream(side):
                     side.wait_event(ready)
                     vals = _text_kv(bj, sh, enc2, _lora_ab(bj))
