@@ -125,6 +125,12 @@ int ltx_layernorm_modulate_bwd(const void* dy, const void* x, const float* mean,
  * rounded to bf16 as the reference's tables are; grid is [B,3,N] int64 (grid_is_float == 0) or
  * f32. Output cs [B*N, D/2] u32 = bf16 cos | bf16 sin << 16 per element pair (16-B aligned).
  * Pass B = 1 when all batches share their coordinates (then cs_batch_rows = 0 below). */
+/* Packs the reference's own RoPE pair (cos, sin) of precompute_freqs_cis (transformer3d.py:270-277:
+ * bf16 [rows, D] with row stride ld, every value repeated for the element pair 2i, 2i+1) into the
+ * table layout of ltx_rope_table: cs[r, i] = cos[r, 2i] | sin[r, 2i] << 16 (the operator-level
+ * Attention.set_processor plug-in, attention.py:532-552, receives freqs_cis as that pair). */
+int ltx_rope_pack_bf16(const void* cos, const void* sin, int64_t ld, int64_t rows, int64_t D, uint32_t* cs,
+                       void* stream);
 int ltx_rope_table(const void* indices_grid, int grid_is_float, int64_t B, int64_t N, int64_t D,
                    const float* omega, float max_pos_t, float max_pos_h, float max_pos_w, uint32_t* cs,
                    void* stream);

@@ -32,6 +32,10 @@ Fixtures (safetensors + a JSON sidecar each):
                     scale-shift tables, caption projection, proj_out trainable): all grads.
   ckpt_export       save_training_checkpoint of the tiny model: lora_audio (peft merge) and full
                     (state dict) safetensors, tensors + metadata (torch_utils.py:39-133).
+  attn_processor    the reference Attention + AttnProcessor2_0 of the tiny model's block 0 (self
+                    with RoPE; cross with mask bias + peft LoRA): outputs and input/LoRA grads.
+
+    python oracle/gen_golden.py attn       # regenerates one fixture (gen_<name>)
 """
 import dataclasses
 import json
@@ -425,6 +429,61 @@ def gen_full():
     _save("tiny_full_step", tensors, meta)
 
 
+def gen_attn():
+    """Operator-level plug-in fixture (Attention.set_processor, attention.py:532-552): the
+    reference Attention modules of the tiny model's block 0 with AttnProcessor2_0
+    (attention.py:935-1114) -- attn1 (self-attention, q/k RMSNorm + RoPE from the (cos, sin) pair
+    of precompute_freqs_cis) and attn2 (cross-attention, key-padding mask bias prepared as in
+    transformer3d.py:441-445, peft LoRA r=16 on to_q/to_k/to_v/to_out.0) -- forward and backward
+    (seeded output gradients), in bf16 and with fp32 copies of the same weights (noise floor).
+    The metadata lists the reference Attention's attribute and submodule names."""
+    seed, rank, B, N, L = 1234, 16, 2, 64, 4
+    g = torch.Generator().manual_seed(5)
+    out = {}
+    meta = {"config": TINY_CONFIG, "param_seed": seed, "lora_rank": rank, "lora_alpha": rank,
+            "source": "reference attention.py:325-1114 (Attention + AttnProcessor2_0) via oracle/shim"}
+    x = torch.randn(B, N, 128, generator=g)
+    enc = torch.randn(B, L, 128, generator=g)
+    m = torch.tensor([[1, 1, 1, 0], [1, 1, 0, 0]], dtype=torch.long)
+    pf = SymmetricPatchifier(1)
+    grid = pf.get_latent_coords(1, 8, 8, B, "cpu")
+    d1 = torch.randn(B, N, 128, generator=g)
+    d2 = torch.randn(B, N, 128, generator=g)
+    for tag, dt in (("bf16", torch.bfloat16), ("fp32", torch.float32)):
+        model, _ = _build(TINY_CONFIG, seed, dt, rank)
+        core = model.base_model.model
+        blk = core.transformer_blocks[0]
+        cos, sin = core.precompute_freqs_cis(grid)
+        bias = ((1 - m.to(dt)) * -10000.0).unsqueeze(1)  # transformer3d.py:441-445
+        if tag == "bf16":
+            for name, a in (("attn1", blk.attn1), ("attn2", blk.attn2)):
+                meta[f"{name}_attributes"] = sorted(k for k in vars(a) if not k.startswith("_"))
+                meta[f"{name}_modules"] = sorted(a._modules)
+                meta[f"{name}_processor"] = type(a.processor).__name__
+            out.update({"in.x": x.to(dt), "in.enc": enc.to(dt), "in.mask": m, "in.mask_bias": bias,
+                        "in.cos": cos, "in.sin": sin, "in.dout1": d1.to(dt), "in.dout2": d2.to(dt),
+                        "in.indices_grid": grid})
+            for n, p in core.named_parameters():
+                if n.startswith("transformer_blocks.0.attn"):
+                    out["w." + P.canonical_name(n)] = p.detach().clone()
+        xs = x.to(dt).requires_grad_()
+        o1 = blk.attn1(xs, freqs_cis=(cos, sin))
+        o1.backward(d1.to(dt))
+        out[f"out.{tag}.o1"] = o1.detach()
+        out[f"grad.{tag}.x1"] = xs.grad.detach()
+        xs2 = x.to(dt).requires_grad_()
+        es = enc.to(dt).requires_grad_()
+        o2 = blk.attn2(xs2, freqs_cis=(cos, sin), encoder_hidden_states=es, attention_mask=bias)
+        o2.backward(d2.to(dt))
+        out[f"out.{tag}.o2"] = o2.detach()
+        out[f"grad.{tag}.x2"] = xs2.grad.detach()
+        out[f"grad.{tag}.enc2"] = es.grad.detach()
+        for n, p in blk.attn2.named_parameters():
+            if p.requires_grad:
+                out[f"grad.{tag}.attn2.{P.canonical_name(n)}"] = p.grad.detach().clone()
+    _save("attn_processor", out, meta)
+
+
 def gen_config():
     cfg = load_train_config_from_yaml(os.path.join(REF, "configs", "train-avatars.yaml"))
     d = dataclasses.asdict(cfg)
@@ -436,6 +495,10 @@ def gen_config():
 if __name__ == "__main__":
     torch.set_num_threads(8)
     print("generating goldens into", OUT)
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()["gen_" + name]()
+        raise SystemExit(0)
     gen_config()
     gen_patchify()
     gen_rf()
@@ -445,3 +508,4 @@ if __name__ == "__main__":
     gen_infer()
     gen_ckpt()
     gen_full()
+    gen_attn()

@@ -286,6 +286,18 @@ __global__ __launch_bounds__(256) void rope_table_kernel(const void* grid, int i
   cs[idx] = (uint32_t)f2bf(c) | ((uint32_t)f2bf(s) << 16);
 }
 
+// the same packed table from the reference's own (cos, sin) pair (precompute_freqs_cis output,
+// transformer3d.py:270-277: bf16 [rows, D], each value repeated for the element pair 2i, 2i+1), as
+// the Attention.set_processor plug-in receives it
+__global__ __launch_bounds__(256) void rope_pack_kernel(const bf16_t* __restrict__ cosv, const bf16_t* __restrict__ sinv,
+                                                        int64_t ld, int half, int64_t total, uint32_t* __restrict__ cs) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int64_t row = idx / half;
+  const int64_t e = row * ld + 2 * (idx - row * half);
+  cs[idx] = (uint32_t)cosv[e] | ((uint32_t)sinv[e] << 16);
+}
+
 __device__ __forceinline__ void cs4(const uint32_t* __restrict__ cs, int64_t rowbase, int e, float* c, float* s) {
   const u32x4 v = *(const u32x4*)(cs + rowbase + (e >> 1));
 #pragma unroll
@@ -541,6 +553,16 @@ int ltx_layernorm_modulate_bwd(const void* dy, const void* x, const float* mean,
   return LTX_OK;
 }
 
+int ltx_rope_pack_bf16(const void* cos, const void* sin, int64_t ld, int64_t rows, int64_t D, uint32_t* cs,
+                       void* stream) {
+  LTX_CHECK_ARG(cos && sin && cs && rows > 0 && D % 8 == 0 && D <= 2048 && ld >= D, "rope_pack: bad args");
+  const int64_t total = rows * (D / 2);
+  hipLaunchKernelGGL(rope_pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)cos, (const bf16_t*)sin, ld, (int)(D / 2), total, cs);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
 int ltx_rope_table(const void* indices_grid, int grid_is_float, int64_t B, int64_t N, int64_t D,
                    const float* omega, float max_pos_t, float max_pos_h, float max_pos_w, uint32_t* cs,
                    void* stream) {
@@ -584,6 +606,12 @@ int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const
   LTX_CHECK_ARG(!rope || (rope_cs && ((uintptr_t)rope_cs % 16) == 0), "qk_norm_rope_bwd: rope needs a 16-B aligned table");
   const bool has_k = dk_in != nullptr;
   LTX_CHECK_ARG(!has_k || (k_raw && k_weight && rstd_k && dk_out), "qk_norm_rope_bwd: incomplete k operands");
+  // 16-B vector loads/stores at m * ld + e: bf16 rows need ld % 8, f32 gradient rows ld % 4
+  LTX_CHECK_ARG(ldq_in % (dq_is_f32 ? 4 : 8) == 0 && ldq_raw % 8 == 0 && ldq_out % 8 == 0 &&
+                    (!has_k || (ldk_in % (dk_is_f32 ? 4 : 8) == 0 && ldk_raw % 8 == 0 && ldk_out % 8 == 0)),
+                "qk_norm_rope_bwd: leading dims must keep 16-B rows (bf16 % 8, f32 % 4)");
+  LTX_CHECK_ARG((((uintptr_t)dq_in | (uintptr_t)q_raw | (uintptr_t)dq_out | (uintptr_t)dk_in | (uintptr_t)k_raw |
+                  (uintptr_t)dk_out) % 16) == 0, "qk_norm_rope_bwd: operands must be 16-B aligned");
   const int nsel = has_k ? 2 : 1;
   const int64_t M = B * N;
   hipLaunchKernelGGL(qk_norm_rope_bwd_kernel, dim3(row_blocks(M * nsel)), dim3(ROW_THREADS), 0,
@@ -604,6 +632,11 @@ int ltx_qk_norm_wgrad(const void* dq_in, int64_t ldq_in, int dq_is_f32, const vo
   LTX_CHECK_ARG(!rope || (rope_cs && ((uintptr_t)rope_cs % 16) == 0), "qk_norm_wgrad: rope needs a 16-B aligned table");
   const bool has_k = dk_in != nullptr;
   LTX_CHECK_ARG(!has_k || (k_raw && rstd_k), "qk_norm_wgrad: incomplete k operands");
+  LTX_CHECK_ARG(ldq_in % (dq_is_f32 ? 4 : 8) == 0 && ldq_raw % 8 == 0 &&
+                    (!has_k || (ldk_in % (dk_is_f32 ? 4 : 8) == 0 && ldk_raw % 8 == 0)),
+                "qk_norm_wgrad: leading dims must keep 16-B rows (bf16 % 8, f32 % 4)");
+  LTX_CHECK_ARG((((uintptr_t)dq_in | (uintptr_t)q_raw | (uintptr_t)dk_in | (uintptr_t)k_raw) % 16) == 0,
+                "qk_norm_wgrad: operands must be 16-B aligned");
   hipLaunchKernelGGL(qk_norm_wgrad_kernel, dim3((unsigned)splits, has_k ? 2u : 1u), dim3(256), 0, (hipStream_t)stream,
                      dq_in, ldq_in, dq_is_f32, dk_in, ldk_in, dk_is_f32, (const bf16_t*)q_raw, ldq_raw,
                      (const bf16_t*)k_raw, ldk_raw, rstd_q, rstd_k, rope_cs, cs_batch_rows, (int)N, (int)(B * N),

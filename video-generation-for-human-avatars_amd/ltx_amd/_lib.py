@@ -35,6 +35,7 @@ _SIGNATURES = {
     "ltx_layernorm_modulate_fwd": [_p, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _f32, _p],
     "ltx_layernorm_modulate_bwd": [_p, _p, _p, _p, _p, _i64, _p, _i64, _i64, _i64, _p],
     "ltx_rope_table": [_p, _i32, _i64, _i64, _i64, _p, _f32, _f32, _f32, _p, _p],
+    "ltx_rope_pack_bf16": [_p, _p, _i64, _i64, _i64, _p, _p],
     "ltx_qk_norm_rope_fwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _p, _i64,
                              _i64, _i64, _i64, _i32, _f32, _p],
     "ltx_qk_norm_rope_bwd": [_p, _i64, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _p, _p, _p, _p,

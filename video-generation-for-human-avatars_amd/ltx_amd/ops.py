@@ -209,6 +209,28 @@ class RopeSpec:
              self.max_pos[0], self.max_pos[1], self.max_pos[2], _p(self.cs), _s())
 
 
+class RopePair:
+    """RoPE state from the reference's own (cos, sin) pair (precompute_freqs_cis's return value,
+    transformer3d.py:270-277: bf16 [B, N, D], each value repeated for the element pair 2i, 2i+1),
+    packed by ltx_rope_pack_bf16 into the ltx_rope_table layout: what the Attention.set_processor
+    plug-in receives as freqs_cis (attention.py:1010-1012). A batch-broadcast pair (stride 0 on
+    dim 0) packs one batch shared by all (cs_batch_rows = 0)."""
+
+    def __init__(self, cos, sin):
+        if cos.shape != sin.shape or cos.dim() != 3:
+            raise ValueError(f"freqs_cis: (cos, sin) of equal [B, N, D] shape expected, got "
+                             f"{tuple(cos.shape)} / {tuple(sin.shape)}")
+        _need(cos, BF16, "freqs_cis cos")
+        _need(sin, BF16, "freqs_cis sin")
+        self.B, self.N, self.D = cos.shape
+        shared = self.B > 1 and cos.stride(0) == 0 and sin.stride(0) == 0
+        c = (cos[:1] if shared else cos).reshape(-1, self.D).contiguous()
+        s = (sin[:1] if shared else sin).reshape(-1, self.D).contiguous()
+        self.cs_batch_rows = 0 if shared else self.N
+        self.cs = torch.empty(c.shape[0], self.D // 2, dtype=torch.int32, device=cos.device)
+        call("ltx_rope_pack_bf16", _p(c), _p(s), self.D, c.shape[0], self.D, _p(self.cs), _s())
+
+
 def qk_norm_rope_fwd(q_in, k_in, q_w, k_w, rope: RopeSpec = None, B=None, N=None, eps=1e-5,
                      q_out=None, k_out=None):
     """q_in/k_in [M,D] row views -> (q_out, k_out, rstd_q, rstd_k). k_in may be None."""
