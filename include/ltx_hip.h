@@ -177,17 +177,6 @@ int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
 /* ---- bf16 MFMA GEMM: C[M,N] = epilogue(A[M,K] . W[N,K]^T) ------------------------------------ */
 /* nn.Linear forward (W as stored) and dgrad (W^T packed once: frozen weights). K % 64 == 0,
  * N % 8 == 0, leading dims % 8 == 0, 16-B aligned operands. rank in {8,16,32} for LoRA. */
-/* Plain bf16 GEMM through hipBLASLt (library GEMM for products with no fused epilogue):
- * C[M,N] (+)= A[M,K] . W[N,K]^T (+ bias[N]), f32 accumulation, one rounding to bf16.
- * a_kmajor / w_kmajor = 1: that operand is stored [K,M] / [K,N] row-major (token-major
- * activations and gradients for a weight gradient, K = tokens: no transpose pass).
- * accumulate = 1: C = bf16(C + acc) (the .grad += of train_mode='full'); not with bias.
- * Replaces the F.linear / autograd matmuls of attention.py:996-1014 (to_q/k/v), :1089 (to_out)
- * and FeedForward.forward (attention.py:1257) for the unfused products. */
-int ltx_gemm_blaslt_bf16(int a_kmajor, int w_kmajor, const void* A, int64_t lda, const void* W,
-                         int64_t ldw, void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                         const void* bias, int accumulate, void* stream);
-
 int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
                      int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue,
                      const void* bias, const void* aux0, int64_t ld0, const void* aux1,

@@ -49,7 +49,6 @@ _SIGNATURES = {
     "ltx_gemm_set_variant": [_i32],
     "ltx_add_bf16": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _p],
     "ltx_gated_residual_bf16": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p],
-    "ltx_gemm_blaslt_bf16": [_i32, _i32, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i32, _p],
     "ltx_gemm_set_workspace": [_p, _i64],
     "ltx_gemm_set_stream_workspace": [_p, _p, _i64],
     "ltx_gemm_bf16_nt_ext": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64,

@@ -358,14 +358,6 @@ def _gemm_workspace(device):
     return _GEMM_WS[key]
 
 
-# plain-store GEMMs of at least this many MACs go to hipBLASLt (LTX_GEMM_BLASLT=0: hand-written
-# kernel for everything, for A/B); the fused-epilogue products always run the HIP kernels
-BLASLT_MIN_MNK = 1 << 30
-# below this K the fused epilogue wins (the extra y pass costs ~20 us); LTX_BLASLT_GRES_MIN_K for A/B
-BLASLT_GRES_MIN_K = int(os.environ.get("LTX_BLASLT_GRES_MIN_K", "4096"))
-_BLASLT = [os.environ.get("LTX_GEMM_BLASLT", "1") != "0"]
-
-
 def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2=None,
          alpha=1.0, rank=0, rows_per_batch=0, ext=None):
     """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias) [+ a2 . w2^T]); see LTX_EPI_* in ltx_hip.h.
@@ -387,26 +379,10 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
         ev0.record()
     a2, w2 = ext if ext is not None else (None, None)
     K2 = a2.shape[1] if a2 is not None else 0
-    if (epilogue == "gated_residual" and a2 is None and _BLASLT[0] and K >= BLASLT_GRES_MIN_K
-            and M * N * K >= BLASLT_MIN_MNK):
-        # long-K gated residual (FF-down): library GEMM for y = bf16(x.W^T + b), then the gate and
-        # residual pass (the fused epilogue's exact roundings); aux2 = where y goes, if kept
-        y = aux2 if aux2 is not None else torch.empty(M, N, dtype=BF16, device=a.device)
-        call("ltx_gemm_blaslt_bf16", 0, 0, _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(y),
-             _rows(y, "y"), M, N, K, _p(bias), 0, _s())
-        call("ltx_gated_residual_bf16", _p(aux0), ld0, _p(aux1), ld1, _p(y), _rows(y, "y"),
-             _p(out), _rows(out, "out"), M, N, rows_per_batch, _s())
-    elif (epilogue == "store" and a2 is None and aux0 is None and aux1 is None and aux2 is None
-            and _BLASLT[0] and M * N * K >= BLASLT_MIN_MNK):
-        # no fused epilogue: the library GEMM (hipBLASLt, ltx_gemm_blaslt_bf16)
-        call("ltx_gemm_blaslt_bf16", 0, 0, _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(out),
-             _rows(out, "out"), M, N, K, _p(bias), 0, _s())
-    else:
-        call("ltx_gemm_bf16_nt_ext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
-             _rows(a2, "a2") if a2 is not None else 0, _p(w2),
-             _rows(w2, "w2") if w2 is not None else 0, K2, _p(out), _rows(out, "out"), M, N, K,
-             EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1), ld1, _p(aux2), ld2, float(alpha),
-             rank, rows_per_batch, _s())
+    call("ltx_gemm_bf16_nt_ext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
+         _rows(a2, "a2") if a2 is not None else 0, _p(w2), _rows(w2, "w2") if w2 is not None else 0,
+         K2, _p(out), _rows(out, "out"), M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1),
+         ld1, _p(aux2), ld2, float(alpha), rank, rows_per_batch, _s())
     if timed:
         ev1.record()
         _timer.pairs.append((ev0, ev1))
@@ -687,8 +663,10 @@ def _tpad(x, npad):
 
 def wgrad_into(grad, dy, x, accumulate=True):
     """grad [N, K] (bf16) (+)= dy^T . x over the M token rows (dy [M, N], x [M, K]): the weight
-    gradient of an nn.Linear. hipBLASLt reads both operands token-major (K-major), so there is no
-    transpose pass; f32 accumulation, rounded once into grad."""
+    gradient of an nn.Linear. Both operands are transposed token-major ([N, M'], [K, M'], the
+    token axis zero-padded to a multiple of 64) so the token axis becomes the NT GEMM's K; the
+    product is rounded to bf16 once and accumulated as autograd's AccumulateGrad does
+    (grad = bf16(grad + bf16(dy^T x)), the LTX_EPI_ACCUM epilogue)."""
     M, N = dy.shape
     M2, K = x.shape
     if M != M2 or tuple(grad.shape) != (N, K):
@@ -696,9 +674,11 @@ def wgrad_into(grad, dy, x, accumulate=True):
     _need(dy, BF16, "wgrad dy")
     _need(x, BF16, "wgrad x")
     _need(grad, BF16, "wgrad grad")
-    call("ltx_gemm_blaslt_bf16", 1, 1, _p(dy), _rows(dy, "dy"), _p(x), _rows(x, "x"), _p(grad),
-         _rows(grad, "grad"), N, K, M, None, 1 if accumulate else 0, _s())
-    return grad
+    mp = (M + 63) // 64 * 64
+    dyT, xT = _tpad(dy, mp), _tpad(x, mp)
+    if accumulate:
+        return gemm(dyT, xT, epilogue="accum", aux0=grad, out=grad)
+    return gemm(dyT, xT, out=grad)
 
 
 def wgrad(dy, x):
