@@ -1,0 +1,186 @@
+"""LTX-2B-width parity on the MI355X for the configurations BASELINE.json names:
+
+  * config X attention: self-attention at B=1, H=32, Nq=Nk=7488, d=64 (97 frames at 768^2) vs the
+    reference's own op, F.scaled_dot_product_attention (attention.py:1057-1064), in bf16 and fp32;
+  * config X block: one LTX-2B block at latent 13x24x24 (N=7488) through train_step vs the oracle;
+  * config A path: a 2-block LTX-2B-width model at B=8 with ONE prompt expanded over the batch
+    (the bench's text_shared path: shared text K/V, batch-summed dK/dV, caption projection run
+    once) vs the oracle run per sample -- out.sample, every LoRA and caption-projection gradient,
+    and the loss;
+  * LTX-2B loss curve: 20 seeded optimizer steps of that 2-block model (LoRA r=16, shared prompt,
+    B=8) -- train_step + FusedAdamW vs the oracle + torch AdamW in bf16 and in fp32.
+
+Criterion: err(build_bf16, ref_fp32) <= 1.25 * err(ref_bf16, ref_fp32) + slack,
+rel-Frobenius, with the oracle / torch's own bf16 op as the bf16 reference; loss scalars (f32
+means, not the bf16-rounded scalar) within 1e-3 relative of the fp32 reference or within the
+reference's own bf16 noise on that loss, whichever is larger.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import ltx_oracle as O
+from model_utils import build_model, grads_by_canonical, rel
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _crit(name, build, ref16, ref32, factor=1.25, slack=2e-3):
+    e_b, e_r = rel(build.float(), ref32.float()), rel(ref16.float(), ref32.float())
+    assert e_b <= factor * e_r + slack, f"{name}: build err {e_b:.3e} vs reference bf16 noise {e_r:.3e}"
+    return e_b, e_r
+
+
+def _loss_crit(name, lb, l16, l32):
+    e_b, e_r = abs(lb - l32) / abs(l32), abs(l16 - l32) / abs(l32)
+    assert e_b <= max(1e-3, 1.25 * e_r + 1e-4), f"{name}: loss {lb} vs fp32 {l32} (bf16 ref {l16})"
+
+
+def _sdpa(q, k, v, B, H, d):
+    N = q.shape[0] // B
+    sh = lambda x: x.view(B, N, H, d).transpose(1, 2)
+    o = F.scaled_dot_product_attention(sh(q), sh(k), sh(v))
+    return o.transpose(1, 2).reshape(B * N, H * d)
+
+
+def test_attention_config_x_self_7488():
+    """Config X's SDPA (B=1, 32 heads, Nq=Nk=7488, d=64): forward, lse, dQ/dK/dV."""
+    from ltx_amd import ops
+    B, H, N, d = 1, 32, 7488, 64
+    g = torch.Generator(device=DEV).manual_seed(71)
+    q, k, v, do = (torch.randn(B * N, H * d, generator=g, device=DEV).bfloat16() for _ in range(4))
+    o, lse = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5)
+    dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, d ** -0.5)
+    outs = {}
+    for dt in (torch.bfloat16, torch.float32):
+        qq, kk, vv = (t.to(dt).clone().requires_grad_(True) for t in (q, k, v))
+        oo = _sdpa(qq, kk, vv, B, H, d)
+        oo.backward(do.to(dt))
+        outs[dt] = (oo.detach(), qq.grad, kk.grad, vv.grad)
+        del qq, kk, vv, oo
+        torch.cuda.empty_cache()
+    for i, (name, mine) in enumerate((("o", o), ("dq", dq), ("dk", dk), ("dv", dv))):
+        _crit(f"X attention {name}", mine, outs[torch.bfloat16][i], outs[torch.float32][i])
+    # lse (log2 units) against the fp32 logsumexp of the scaled scores, per head
+    qh = q.float().view(N, H, d).transpose(0, 1)
+    kh = k.float().view(N, H, d).transpose(0, 1)
+    for h in (0, 17, 31):
+        ref = torch.logsumexp((qh[h] @ kh[h].t()) * d ** -0.5, -1) / torch.log(torch.tensor(2.0))
+        assert float((lse[0, h] - ref).abs().max()) < 1e-2
+
+
+def _inputs(B, F_, H_, W_, L, n_valid, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    d = {"in.latents": torch.randn(B, 128, F_, H_, W_, generator=g, device=DEV),
+         "in.ref_image_latents": torch.randn(B, 128, 1, H_, W_, generator=g, device=DEV),
+         "in.pose_latents": torch.randn(B, 128, F_, H_, W_, generator=g, device=DEV),
+         "in.prompt_embeds": torch.randn(1, L, 4096, generator=g, device=DEV),
+         "in.prompt_attention_mask": (torch.arange(L, device=DEV) < n_valid).long().view(1, L),
+         "out.t": torch.rand(B, generator=g, device=DEV) * 0.9 + 0.05}
+    d["out.noise"] = torch.randn(B, F_ * H_ * W_, 128, generator=g, device=DEV).bfloat16()
+    return d
+
+
+def _oracle(params, cfg, d, dtype):
+    q = {k: v.detach().to(DEV).to(torch.float32 if ("lora_" in k or dtype == torch.float32) else dtype)
+         .requires_grad_(("lora_" in k) or ("caption_projection" in k)) for k, v in params.items()}
+    r = O.train_step(q, cfg, d["in.latents"], d["in.ref_image_latents"], d["in.pose_latents"],
+                     d["in.prompt_embeds"], d["in.prompt_attention_mask"], t=d["out.t"],
+                     noise=d["out.noise"].to(dtype))
+    r["loss"].backward()
+    loss32 = float(((r["sample"].float() - r["v_target"].float()) ** 2).mean())
+    return r["sample"].detach(), {k: v.grad for k, v in q.items() if v.requires_grad}, loss32
+
+
+def _build_step(model, d):
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    from ltx_amd.training import train_step
+    tc = TrainConfig(checkpoint_path="-", gradient_accumulation_steps=1)
+    loss, _, _, ld = train_step(model, {"latents": d["in.latents"], "ref_image_latents": d["in.ref_image_latents"],
+                                        "pose_latents": d["in.pose_latents"]},
+                                RectifiedFlowScheduler(), model.patchifier, tc, d["in.prompt_embeds"],
+                                d["in.prompt_attention_mask"], t=d["out.t"], noise=d["out.noise"])
+    return float(ld["_mse_f32"])
+
+
+def _sample(model, d):
+    B = d["in.latents"].shape[0]
+    tok, coords = O.patchify(d["in.latents"].bfloat16())
+    x = O.add_noise(tok, d["out.noise"], d["out.t"]).bfloat16()
+    with torch.no_grad():
+        return model(hidden_states=x, indices_grid=coords.to(DEV),
+                     ref_image_hidden_states=d["in.ref_image_latents"].bfloat16(),
+                     pose_hidden_states=d["in.pose_latents"].bfloat16(),
+                     encoder_hidden_states=d["in.prompt_embeds"].bfloat16().expand(B, -1, -1),
+                     timestep=d["out.t"], encoder_attention_mask=d["in.prompt_attention_mask"].expand(B, -1)).sample
+
+
+def _compare_model(tag, cfg, params, d, grad_names=None):
+    model = build_model(cfg, params, 16, device=DEV)
+    out = _sample(model, d)
+    lb = _build_step(model, d)
+    g = grads_by_canonical(model)
+    s32, g32, l32 = _oracle(params, cfg, d, torch.float32)
+    s16, g16, l16 = _oracle(params, cfg, d, torch.bfloat16)
+    _crit(f"{tag} sample", out, s16, s32)
+    _loss_crit(tag, lb, l16, l32)
+    for name in grad_names or g32:
+        _crit(f"{tag} {name}", g[name], g16[name], g32[name], slack=5e-3)
+    return model
+
+
+def test_block2b_config_x_latent():
+    """One LTX-2B block at config X's latent 13x24x24 (N = 7488), B = 1, 256 text tokens (16 valid)."""
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    cfg = dict(OURS_TRANSFORMER_CONFIG, num_layers=1)
+    params = O.make_params(cfg, 29, lora_rank=16, requires_grad=False)
+    d = _inputs(1, 13, 24, 24, 256, 16, seed=5)
+    _compare_model("X block", cfg, params, d)
+
+
+def test_two_blocks_b8_shared_prompt():
+    """Config A's exact path at LTX-2B widths: B = 8 samples of 7x16x16 (N = 1792), ONE prompt
+    of 256 tokens (16 valid) expanded over the batch -> text_shared (shared text K/V,
+    batch-summed dK/dV, caption projection once) vs the oracle's per-sample computation; every
+    LoRA (2 x 8 tensors) and caption-projection gradient."""
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    cfg = dict(OURS_TRANSFORMER_CONFIG, num_layers=2)
+    params = O.make_params(cfg, 31, lora_rank=16, requires_grad=False)
+    d = _inputs(8, 7, 16, 16, 256, 16, seed=9)
+    _compare_model("A 2-block B8", cfg, params, d)
+
+
+def test_ltx2b_loss_curve_shared_prompt():
+    """SURVEY 8(c)-5 at LTX-2B widths: 20 optimizer steps (2 blocks, LoRA r=16, B=8 with one
+    shared prompt, lr 1e-4): train_step + FusedAdamW vs the oracle + torch AdamW in bf16 and
+    fp32 from the same weights, with the same per-step (latents, t, noise) streams."""
+    from ltx_amd.training import FusedAdamW
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    cfg = dict(OURS_TRANSFORMER_CONFIG, num_layers=2)
+    params = O.make_params(cfg, 37, lora_rank=16, requires_grad=False)
+    model = build_model(cfg, params, 16, device=DEV)
+    model.train()
+    opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    refs = {}
+    for dt in (torch.bfloat16, torch.float32):
+        q = {k: v.detach().to(DEV).to(torch.float32 if ("lora_" in k or dt == torch.float32) else dt)
+             .requires_grad_(("lora_" in k) or ("caption_projection" in k)) for k, v in params.items()}
+        refs[dt] = (q, torch.optim.AdamW([v for v in q.values() if v.requires_grad], lr=1e-4, foreach=False))
+    curves = {"build": [], torch.bfloat16: [], torch.float32: []}
+    for step in range(20):
+        d = _inputs(8, 7, 16, 16, 256, 16, seed=1000 + step)
+        curves["build"].append(_build_step(model, d))
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        for dt, (q, ropt) in refs.items():
+            r = O.train_step(q, cfg, d["in.latents"], d["in.ref_image_latents"], d["in.pose_latents"],
+                             d["in.prompt_embeds"], d["in.prompt_attention_mask"], t=d["out.t"],
+                             noise=d["out.noise"].to(dt))
+            r["loss"].backward()
+            ropt.step()
+            ropt.zero_grad(set_to_none=True)
+            curves[dt].append(float(((r["sample"].float() - r["v_target"].float()) ** 2).mean()))
+    for i in range(20):
+        _loss_crit(f"step {i}", curves["build"][i], curves[torch.bfloat16][i], curves[torch.float32][i])

@@ -70,7 +70,9 @@ def train_step(model, batch, scheduler, patchifier, config, prompt_embeds, promp
     nrmse = torch.sqrt(loss) / (std + 1e-12)
     if backward:
         out.backward(dout)
-    return loss, rel_mse, nrmse, {"transformer_mse": mse}
+    # "_mse_f32": the unrounded f32 mean (parity tests compare losses at 1e-3, below the bf16
+    # rounding of the reference's loss scalar); underscore keys are not logged
+    return loss, rel_mse, nrmse, {"transformer_mse": mse, "_mse_f32": stats[0] / n}
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -202,7 +204,8 @@ def train_one_epoch(model, dataloader, optimizer, scheduler, patchifier, device,
                            "train/nrmse": float(nrmse), "train/epoch": epoch,
                            "train/lr": optimizer.param_groups[0]["lr"]}
                 for k, v in (loss_dict or {}).items():
-                    payload[f"train/{k}"] = float(v)
+                    if not k.startswith("_"):
+                        payload[f"train/{k}"] = float(v)
                 log_fn(payload, global_step)
     epoch_loss = float(torch.stack(losses).mean()) if losses else 0.0
     return global_step, epoch_loss
