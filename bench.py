@@ -13,8 +13,9 @@ forward + backward (train_step); every 16th step also runs the DP gradient all-r
 AdamW update (gradient_accumulation_steps 16, train-avatars.yaml:23), inside the timed region.
 
 Prints ONE JSON line (rank 0): value = samples/s summed over ranks (= tokens/s / 1792), plus the
-roofline of the dominant kernel (the FF-up GEMM, 2*M*N*K flops per launch, timed live with HIP
-events on its stream) and the CPU baseline (the oracle restatement, rank 0 at N=1 only).
+roofline of the dominant kernel (the kernel class with the most launch time in the timed region,
+timed live with HIP events on its stream; algorithmic FLOPs per launch), a per-kernel table, and
+the CPU baseline (the oracle restatement, rank 0 at N=1 only).
 """
 import argparse
 import json
@@ -99,15 +100,15 @@ def synthetic_batch(device, rank):
     return batch, prompt, mask
 
 
-def cpu_baseline(budget_layers=28, timed=2):
-    """The oracle restatement (oracle/ltx_oracle.py) on the host cores: config A at B=1,
-    N = 1792, `budget_layers` of the 28 blocks (all of them by default), one warm-up + `timed`
-    timed fwd+bwd steps (~10-20 s of CPU work); per-sample time = mean timed step
-    x(28/budget_layers)."""
+def cpu_baseline(budget_layers=28, warmup=2, timed=5):
+    """The oracle restatement (oracle/ltx_oracle.py) on the host cores, as BASELINE.md 4 plans it:
+    config A at B=1, N = 1792, all 28 blocks, `warmup` untimed + `timed` timed fwd+bwd steps, the
+    MEDIAN timed step is the per-sample time (~35 s of CPU work). Threads: the box's CPU share
+    for one GPU (16; os.cpu_count() reports the whole host, shared with the other GPUs' jobs)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import ltx_oracle as O
     from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("LTX_CPU_BASELINE_THREADS", min(16, os.cpu_count() or 1)))
     torch.set_num_threads(threads)
     cfg = dict(OURS_TRANSFORMER_CONFIG)
     cfg["num_layers"] = budget_layers
@@ -127,14 +128,15 @@ def cpu_baseline(budget_layers=28, timed=2):
     prompt = torch.randn(1, L_TXT, 4096, generator=g)
     mask = (torch.arange(L_TXT) < 16).long().view(1, L_TXT)
     times = []
-    for _ in range(1 + timed):
+    for _ in range(warmup + timed):
         t0 = time.perf_counter()
         r = O.train_step(p, cfg, lat, ref, pose, prompt, mask)
         r["loss"].backward()
         times.append(time.perf_counter() - t0)
         for v in p.values():
             v.grad = None
-    per_sample = sum(times[1:]) / timed * (28.0 / budget_layers)
+    steady = sorted(times[warmup:])
+    per_sample = steady[len(steady) // 2] * (28.0 / budget_layers)
     # config T ("config A at B = 1 and config T"): the tiny 2-layer model, one
     # 1x8x8 latent, steady-state median of 20 steps after 3 warm-ups
     tcfg = {"num_layers": 2, "num_attention_heads": 4, "attention_head_dim": 32, "in_channels": 128,
@@ -171,23 +173,32 @@ def cpu_baseline(budget_layers=28, timed=2):
                     break
     except OSError:
         pass
-    return {"value": 1.0 / per_sample, "unit": "samples/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model, "config_t_ms_per_step": round(tt[len(tt) // 2] * 1e3, 2),
+    return {"value": 1.0 / per_sample, "unit": "samples/s", "cores": torch.get_num_threads(),
+            "kind": "port", "host_cpu_count": os.cpu_count(), "cpu_model": cpu_model,
+            "step_s": [round(x, 3) for x in times], "median_step_s": round(per_sample, 3),
+            "config_t_ms_per_step": round(tt[len(tt) // 2] * 1e3, 2),
             "tokens_per_s": F_LAT * H_LAT * W_LAT / per_sample,
             "sample": (f"oracle/ltx_oracle.py train_step fwd+bwd, B=1, N={F_LAT*H_LAT*W_LAT}, "
-                       f"{budget_layers}/28 LTX-2B blocks, 1 warm-up + {timed} timed steps "
-                       f"({sum(times[1:]):.1f} s timed), scaled x{28/budget_layers:g}; torch "
-                       f"{torch.__version__} CPU, {threads} threads, cpu_count={os.cpu_count()}")}
+                       f"{budget_layers}/28 LTX-2B blocks, {warmup} warm-up + {timed} timed steps, "
+                       f"median ({sum(times[warmup:]):.1f} s timed); torch {torch.__version__} CPU, "
+                       f"{torch.get_num_threads()} threads = the gpurun box's CPU share for one GPU "
+                       f"(os.cpu_count()={os.cpu_count()} is the whole shared host)")}
 
 
-def load_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary (or None)."""
-    path = os.path.join(REPO, "profiles", "pmc_dominant_gemm.json")
+def load_traffic(label):
+    """Measured HBM bytes per launch of the kernel(s) behind `label` from the committed PMC
+    summary (tools/kernel_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or None."""
+    path = os.path.join(REPO, "profiles", "r02_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
+            table = json.load(f)["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
         return None
+    names = [n.split("(")[0].strip() for n in label.split(": ", 1)[-1].split(" + ")]
+    vals = [table.get(n) for n in names]
+    if any(v is None for v in vals):
+        return None
+    return float(sum(vals))
 
 
 def infer_main(args):
@@ -267,6 +278,9 @@ def main():
     ap.add_argument("--grad-ckpt", action="store_true", help="per-block gradient checkpointing")
     ap.add_argument("--lora-rank", type=int, default=16,
                     help="LoRA rank (alpha = rank): 16 is the BASELINE config, 32 the yaml default")
+    ap.add_argument("--fixed-global-batch", action="store_true",
+                    help="scale gradient accumulation 16 -> 16/N so the global batch per optimizer "
+                         "step stays 128 samples (SURVEY 8e: loss-curve parity with 1 GPU)")
     ap.add_argument("--mode", choices=["lora", "full"], default="lora",
                     help="full: train_mode='full' + ZeRO-2 AdamW (BASELINE configs[4], "
                          "ds_config_zero2.json: grad accumulation 3, clip 1.0)")
@@ -308,6 +322,8 @@ def main():
     full = args.mode == "full"
     if full:
         ACCUM = 3  # ds_config_zero2.json gradient_accumulation_steps
+    elif args.fixed_global_batch:
+        ACCUM = max(1, ACCUM // world)
     model = build_model(device, mode="full" if full else "lora_audio")
     model.gradient_checkpointing = bool(args.grad_ckpt)
     batch, prompt, mask = synthetic_batch(device, rank)
@@ -322,20 +338,27 @@ def main():
         reducer = lambda: None  # noqa: E731  (the reduce-scatter is inside Zero2AdamW.step)
     else:
         opt = FusedAdamW(trainable, lr=cfg.learning_rate)
-        reducer = GradAllReduce(trainable)
+        # bucketed all-reduce overlapped with the last micro-step's backward (grads live in the
+        # reducer's buckets; zero_grad keeps them there)
+        reducer = GradAllReduce(trainable, order=model.grad_ready_order()).install(model)
+        reducer.zero_grad()
     torch.manual_seed(20251015 + rank)
 
     N = F_LAT * H_LAT * W_LAT
-    M = B_PER_GPU * N
-    dom_key = (M, 8192, 2048, "gelu")  # FF-up GEMM (x2 [M,2048] . W1^T -> [M,8192] + tanh-GELU)
-    timer = ops.LaunchTimer(dom_key)
+    timer = ops.LaunchTimer()
 
     def one_step(i):
+        last = (i + 1) % ACCUM == 0
+        if last and not full:
+            reducer.arm()
         train_step(model, batch, sched, model.patchifier, cfg, prompt, mask, device)
-        if (i + 1) % ACCUM == 0:
+        if last:
             reducer()
             opt.step()
-            opt.zero_grad(set_to_none=True)
+            if full:
+                opt.zero_grad(set_to_none=True)
+            else:
+                reducer.zero_grad()
 
     for i in range(args.warmup):
         one_step(i)
@@ -343,7 +366,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    ops.set_launch_timer(timer)
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         one_step(i)
@@ -352,12 +374,27 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ops.set_launch_timer(None)
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    dom_ms = timer.mean_ms()
+    # per-kernel durations with HIP events on the launch stream, in further steps of the same loop
+    # right after the timed region (an event pair around every launch costs the step ~5 %, so the
+    # timed region stays un-instrumented): one step with every GEMM / attention launch bracketed
+    # ranks the kernels; then `prof_steps` steps bracket only the dominant one (few events, the
+    # per-launch figure the roofline uses)
+    i0 = args.warmup + args.steps
+    ops.set_launch_timer(timer)
+    one_step(i0)
+    ops.set_launch_timer(None)
+    kernels = timer.summary()
+    prof_steps = min(args.steps, 4)
+    dom_timer = ops.LaunchTimer(only=kernels[0]["kernel"])
+    ops.set_launch_timer(dom_timer)
+    for i in range(i0 + 1, i0 + 1 + prof_steps):
+        one_step(i)
+    ops.set_launch_timer(None)
+    dom = dom_timer.summary()[0]
 
     samples = B_PER_GPU * args.steps * world
     value = samples / elapsed
@@ -365,8 +402,11 @@ def main():
     if full:  # + wgrad of every attention projection, adaln_single, proj_out (2*M*K*N each)
         bwd += 28 * (2 * N * 2048 * 2048 * 6 + 4 * L_TXT * 2048 * 2048) + 2 * N * 2048 * 128
     step_tflops = (fwd + bwd) * B_PER_GPU * args.steps / (elapsed * 1e12)  # per GPU
-    dom_flops = 2.0 * dom_key[0] * dom_key[1] * dom_key[2]
-    achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+    # the dominant kernel = the class with the most HIP-event time in the ranking step (all of them
+    # are hand-written); its algorithmic TFLOP/s = its FLOPs / its summed launch durations
+    for k in kernels + [dom]:
+        k["tflops"] = k["flops"] / (k["ms"] * 1e-3) / 1e12
+    achieved = dom["tflops"]
     line = {
         "metric": f"LTX-2B {'full (ZeRO-2)' if full else 'LoRA'} train-step samples/sec (latent-tokens/sec = samples/sec x {N})",
         "value": round(value, 4),
@@ -395,10 +435,18 @@ def main():
                    "grad_accum": ACCUM, "parallelism": f"zero2-dp{world}" if full else f"dp{world}"},
         "step_tflops_per_gpu": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-        "roofline": {"bound": "mfma", "kernel": f"gemm_nt_kernel_t<GELU> FF-up [{M}x2048].[8192x2048]^T",
+        "roofline": {"bound": "mfma", "kernel": dom["kernel"],
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": load_traffic() if args.config == "a" and not full else None,
-                     "launch_ms": round(dom_ms, 4), "launches": len(timer.pairs)},
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
+                     "traffic": (load_traffic(dom["kernel"]) if args.config == "a" and not full else None),
+                     "launch_ms": round(dom["ms"] / dom["launches"], 4), "launches": dom["launches"],
+                     "share_of_step": round(dom["ms"] / prof_steps / (elapsed * 1e3 / args.steps), 4),
+                     "timing": f"HIP events around each of its launches in {prof_steps} steps after the timed region",
+                     "flops_per_launch": dom["flops"] / dom["launches"]},
+        # every GEMM / attention kernel class by total time (one step, every launch bracketed)
+        "kernels": [{"kernel": k["kernel"], "launches_per_step": k["launches"],
+                     "ms_per_step": round(k["ms"], 3), "tflops": round(k["tflops"], 1),
+                     "frac": round(k["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4)} for k in kernels[:10]],
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "a" and not full:
         try:

@@ -67,6 +67,12 @@ int ltx_latent_coords(int64_t* coords, int64_t B, int64_t F, int64_t H, int64_t 
 /* x_t = bf16((1-t)x0 + t*eps), v = bf16(eps - x0) in f32; x0/eps [B,N,C] bf16, t [B] f32 */
 int ltx_rf_noise_velocity(const void* tokens, const void* noise, const float* t, void* x_t,
                           void* v_target, int64_t B, int64_t NC, void* stream);
+/* The same arithmetic with f32 results, as the reference's RectifiedFlowScheduler.add_noise /
+ * build_velocity_target return them (rf.py:376-386, 400-426: f32 [B] timesteps promote the
+ * result); tokens / noise bf16 or f32 (the *_f32 flags). x_t or v_target may be null. */
+int ltx_rf_noise_velocity_f32(const void* tokens, int tokens_f32, const void* noise, int noise_f32,
+                              const float* t, float* x_t, float* v_target, int64_t B, int64_t NC,
+                              void* stream);
 /* ---- K2: conditioning lerp of Transformer3DModel.forward (transformer3d.py:447-466) ----------- */
 /* tokens [B,F*H*W,C] -> out tokens: frame 0 = lerp(x, ref, 0.85), frames >=1 lerp(x, pose, 0.5),
  * torch.lerp float formula, bf16 result. ref [B,C,1,H,W], pose [B,C,F,H,W]. out may alias tokens. */
@@ -196,6 +202,11 @@ int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, int64_t ldw,
 /* Tuning knob for A/B measurements of GEMM schedules (0: per-tile DMA split over two quarters,
  * the default; 1: one burst). Process-global. */
 int ltx_gemm_set_variant(int variant);
+/* The demangled name (as rocprofv3 prints it) of the main kernel ltx_gemm_bf16_nt_ext would launch
+ * for this call on `stream` (the dispatcher's tile / split-K choice); bench.py groups its
+ * per-launch HIP-event timings by it. Writes a NUL-terminated string of at most len bytes. */
+int ltx_gemm_describe(int64_t M, int64_t N, int64_t K, int64_t K2, int epilogue, int64_t rank,
+                      void* stream, char* buf, int64_t len);
 /* Caller-owned f32 workspace for split-K on small grids (e.g. the M = 256 text-side GEMMs): the
  * library keeps the pointer until the next call (stream-ordered reuse by consecutive GEMMs on
  * one stream); bytes = 0 disables split-K. */

@@ -37,3 +37,22 @@ def test_ops_refuse_cpu_tensors():
     x = torch.zeros(128, 64, dtype=torch.bfloat16)
     with pytest.raises(_lib.LtxHipError):
         ops.gemm(x, x)
+
+
+def test_gemm_describe_names_the_dispatched_kernel():
+    """ltx_gemm_describe (host-only: the dispatcher's plan, no launch) names the kernel rocprof
+    reports for the config-A shapes, which is what bench.py's roofline attributes timings to."""
+    import ctypes
+    from ltx_amd import _lib
+    lib = _lib.load()
+
+    def name(M, N, K, K2=0, epi="store", rank=0):
+        buf = ctypes.create_string_buffer(256)
+        assert lib.ltx_gemm_describe(M, N, K, K2, _lib.EPI[epi], rank, None, buf, 256) == 0
+        return buf.value.decode()
+    M = 8 * 1792
+    # N = 2048 tiles: 64 x 8 = 512 of 224 rows fill two rounds exactly
+    assert name(M, 2048, 8192) == "ltx::gemm_nt_kernel_t<0, 0, 224, 4, 0, 0, 8>(ltx::GemmParams)"
+    assert name(M, 8192, 2048, epi="gelu") == "ltx::gemm_nt_kernel_t<1, 0, 256, 8, 0, 0, 8>(ltx::GemmParams)"
+    # the text side (M = 256 rows) runs the 128x128 kernel with three LDS stages
+    assert name(256, 4096, 2048, K2=128).startswith("ltx::gemm_nt_kernel<0, 0, 3>")

@@ -279,6 +279,114 @@ def test_grad_allreduce_gloo_world2():
     assert math.isfinite(float(expect[0].sum()))
 
 
+class _FakeBlockFn(torch.autograd.Function):
+    """y = x . W with W's grad written straight into .grad and the block's ready hooks called at
+    the end of backward: the contract of transformer3d._BlockFn for the LoRA adapters."""
+
+    @staticmethod
+    def forward(ctx, blk, x):
+        ctx.blk = blk
+        ctx.save_for_backward(x)
+        return x @ blk.w
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        blk = ctx.blk
+        with torch.no_grad():
+            if blk.w.grad is None:
+                blk.w.grad = torch.zeros_like(blk.w)
+            blk.w.grad.add_(x.t() @ dy)
+        for cb in getattr(blk, "_grad_ready_hooks", ()):
+            cb(blk)
+        return None, dy @ blk.w.t()
+
+
+class _FakeModel(torch.nn.Module):
+    """caption (bf16, autograd-accumulated) -> 3 blocks (f32 grads written by the 'kernel')."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(3)
+        self.cap = torch.nn.Parameter(torch.randn(8, 8, generator=g).to(torch.bfloat16))
+        self.transformer_blocks = torch.nn.ModuleList()
+        for _ in range(3):
+            b = torch.nn.Module()
+            b.w = torch.nn.Parameter(torch.randn(8, 8, generator=g) * 0.3)
+            self.transformer_blocks.append(b)
+
+    def forward(self, x):
+        h = (x.to(torch.bfloat16) @ self.cap).float()
+        for b in self.transformer_blocks:
+            h = _FakeBlockFn.apply(b, h)
+        return h
+
+    def grad_ready_order(self):
+        return [b.w for b in reversed(self.transformer_blocks)] + [self.cap]
+
+
+def _dp_overlap_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from ltx_amd.training import GradAllReduce
+        res = {}
+        for mode in ("overlap", "posthoc"):
+            m = _FakeModel()
+            params = [p for p in m.parameters()]
+            launched_at_cap, box = [], []
+            # registered first: runs before the reducer's own hook on the caption grad
+            m.cap.register_post_accumulate_grad_hook(lambda p: launched_at_cap.append(box[0]._launched))
+            red = GradAllReduce(params, bucket_mb=1e-4, order=m.grad_ready_order()).install(m)
+            box.append(red)
+            assert len(red.buckets) == 4  # one param each: blocks 2, 1, 0, caption
+            red.zero_grad()
+            g = torch.Generator().manual_seed(100 + rank)
+            for step in range(3):  # three micro-steps, the last one armed
+                if mode == "overlap" and step == 2:
+                    red.arm()
+                x = torch.randn(4, 8, generator=g)
+                m(x).square().sum().backward()
+            red()
+            res[mode] = {"grads": [p.grad.clone() for p in params],
+                         "views": all(p.grad.data_ptr() == red._view(*[(b, j) for b in red.buckets
+                                      for j, q in enumerate(b["params"]) if q is p][0]).data_ptr()
+                                      for p in params),
+                         "launched_at_cap": launched_at_cap[-1]}
+            # local (unreduced) grads of this rank for the expected average
+            m2 = _FakeModel()
+            g = torch.Generator().manual_seed(100 + rank)
+            for step in range(3):
+                m2(torch.randn(4, 8, generator=g)).square().sum().backward()
+            res[mode]["local"] = [p.grad.clone() for p in m2.parameters()]
+        torch.save(res, os.path.join(out_dir, f"o{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_overlapped_with_backward_gloo_world2():
+    """GradAllReduce armed for the last micro-step launches the block buckets from the blocks'
+    backward hooks (before the caption grad exists) and ends bitwise equal to the post-backward
+    reduction, equal to the f32 mean of the ranks' grads, with .grad kept as bucket views."""
+    world = 2
+    with tempfile.TemporaryDirectory() as td:
+        mp.start_processes(_dp_overlap_worker, args=(world, _free_port(), td), nprocs=world,
+                           start_method="spawn", join=True)
+        res = [torch.load(os.path.join(td, f"o{r}.pt"), weights_only=True) for r in range(world)]
+    for r in range(world):
+        ov, ph = res[r]["overlap"], res[r]["posthoc"]
+        assert ov["launched_at_cap"] == 3, "the three block buckets launch during the backward"
+        assert ph["launched_at_cap"] == 0
+        assert ov["views"] and ph["views"]
+        for a, b in zip(ov["grads"], ph["grads"]):
+            assert torch.equal(a, b)
+    for i in range(len(res[0]["overlap"]["grads"])):
+        exp = sum(res[r]["overlap"]["local"][i].float() for r in range(world)) / world
+        exp = exp.to(res[0]["overlap"]["grads"][i].dtype)
+        for r in range(world):
+            assert torch.equal(res[r]["overlap"]["grads"][i], exp), (r, i)
+
+
 # ------------------------------------------------------------------ ZeRO-2 (gloo, world size 2)
 ZSHAPES = [(16, 64), (64,), (300,), (7, 5), (1001,)]
 Z_LR, Z_CLIP, Z_STEPS = 1e-2, 0.5, 3

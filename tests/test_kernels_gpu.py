@@ -295,6 +295,22 @@ def test_rf_prepare_tokens():
     assert torch.equal(x2, x_ref) and torch.equal(v2, v_ref)
 
 
+def test_scheduler_add_noise_and_velocity_are_f32_like_the_reference():
+    """RectifiedFlowScheduler.add_noise / build_velocity_target (rf.py:376-386, 400-426) return
+    f32 for f32 timesteps: bitwise the oracle's f32 values, bf16 or f32 inputs."""
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    sch = RectifiedFlowScheduler()
+    t = torch.tensor([0.3, 0.77, 0.05], device=DEV)
+    for dt in (torch.bfloat16, torch.float32):
+        tok = g(3, 192, 128, seed=5).to(dt)
+        noise = g(3, 192, 128, seed=6).to(dt)
+        x = sch.add_noise(tok, noise, t)
+        v = sch.build_velocity_target(tok, noise, t)
+        assert x.dtype == torch.float32 and v.dtype == torch.float32
+        assert torch.equal(x, O.add_noise(tok, noise, t))
+        assert torch.equal(v, O.velocity_target(tok, noise, t))
+
+
 def test_timestep_silu_transpose_colsum():
     from ltx_amd import ops
     t = torch.tensor([0.01, 0.5, 0.999, 0.25], device=DEV)

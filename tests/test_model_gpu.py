@@ -95,6 +95,37 @@ def test_tiny_model_matches_reference_goldens():
             _check_noise_criterion(name, g[name], v.to(DEV), gref32[name], slack=5e-3)
 
 
+def test_seeded_train_step_draws_t_and_noise_like_the_reference():
+    """training.py:124-139 draw order on the device: LogNormal(mu, sigma).sample((B,)) ->
+    r/(1+r) -> quantile clamp (float bounds) -> shift -> randn_like(tokens). A seeded train_step
+    with t=None / noise=None must give exactly the loss of the same step fed those draws."""
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.scheduler import RectifiedFlowScheduler
+    from ltx_amd.training import train_step
+    d, meta = _load("tiny_train_step")
+    params = {k[2:]: v for k, v in d.items() if k.startswith("w.")}
+    model = build_model(meta["config"], params, meta["lora_rank"])
+    tc = TrainConfig(checkpoint_path="-", rf_log_normal_mu=-0.5, rf_log_normal_sigma=1.0)
+    sched = RectifiedFlowScheduler()
+    batch = {k: d["in." + k].to(DEV) for k in ("latents", "ref_image_latents", "pose_latents")}
+    B, C, F, H, W = batch["latents"].shape
+    args = (sched, model.patchifier, tc, d["in.prompt_embeds"].to(DEV), d["in.prompt_attention_mask"].to(DEV))
+    torch.manual_seed(1234)
+    # the reference's own sequence, restated (training.py:124-139)
+    logn = torch.distributions.LogNormal(torch.tensor(tc.rf_log_normal_mu, device=DEV),
+                                         torch.tensor(tc.rf_log_normal_sigma, device=DEV))
+    raw = logn.sample((B,))
+    t_raw = raw / (1 + raw)
+    t = t_raw.clamp(min=float(torch.quantile(t_raw, tc.rf_quantile_min)),
+                    max=float(torch.quantile(t_raw, tc.rf_quantile_max)))
+    tokens = torch.empty(B, F * H * W, C, dtype=torch.bfloat16, device=DEV)
+    noise = torch.randn_like(tokens)
+    ref_loss = train_step(model, batch, *args, t=t, noise=noise, backward=False)[3]["_mse_f32"]
+    torch.manual_seed(1234)
+    loss = train_step(model, batch, *args, backward=False)[3]["_mse_f32"]
+    assert torch.equal(loss, ref_loss), (float(loss), float(ref_loss))
+
+
 def test_shared_prompt_path_matches_per_sample_path():
     """train_step hands the model one prompt expanded over the batch (stride-0 view): the text
     side then runs once and the cross-attention reads shared K/V, with the text-side gradients

@@ -22,6 +22,12 @@ python3 $R/tools/pmc_summary.py stats $RAW/trace/run_kernel_stats.csv $OUT/kerne
 cp $RAW/trace/run_kernel_stats.csv $OUT/kernel_stats.csv
 python3 $R/tools/pmc_summary.py traffic $RAW/pmc_f/run_counter_collection.csv $RAW/pmc_w/run_counter_collection.csv \
     $OUT/pmc_dominant_gemm.json > /dev/null
+timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT \
+    --kernel-trace --output-format csv -d $RAW/pmc_sq -o run -- \
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $RAW/pmc_sq.log 2>&1
+python3 $R/tools/pmc_table.py $RAW/pmc_sq/run_counter_collection.csv > $OUT/pmc_sq.md
+python3 $R/tools/kernel_traffic.py $RAW/pmc_f/run_counter_collection.csv $RAW/pmc_w/run_counter_collection.csv \
+    $OUT/traffic.json > /dev/null
 python3 $R/tools/hbm_table.py $RAW/pmc_f/run_counter_collection.csv $RAW/pmc_w/run_counter_collection.csv \
     $RAW/short/run_results.db 4 $OUT/hbm_per_kernel.md > /dev/null
 ls -la $OUT

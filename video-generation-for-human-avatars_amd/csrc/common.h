@@ -28,6 +28,8 @@ __device__ __forceinline__ unsigned pack2(float lo, float hi) {
 }
 // value rounded through bf16 and back (mirrors an eager bf16 op boundary)
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
+__device__ __forceinline__ float to_f32(bf16_t x) { return bf2f(x); }
+__device__ __forceinline__ float to_f32(float x) { return x; }
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

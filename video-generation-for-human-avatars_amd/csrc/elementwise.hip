@@ -187,6 +187,21 @@ __global__ void rf_noise_velocity_kernel(const bf16_t* __restrict__ x0, const bf
   }
 }
 
+// f32-result form of the same arithmetic: the reference's add_noise / build_velocity_target
+// return f32 (f32 [B] timesteps promote the product, rf.py:376-386, 400-426). Inputs bf16 or f32.
+template <typename TX, typename TE>
+__global__ void rf_noise_velocity_f32_kernel(const TX* __restrict__ x0, const TE* __restrict__ eps,
+                                             const float* __restrict__ t, float* __restrict__ x_t,
+                                             float* __restrict__ v, int64_t NC, int64_t total) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float tb = t[i / NC];
+    const float a = to_f32(x0[i]), e = to_f32(eps[i]);
+    if (x_t) x_t[i] = (1.0f - tb) * a + tb * e;
+    if (v) v[i] = (-1.0f) * a + 1.0f * e;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // AdaLN modulation rows (attention.py:229-239; transformer3d.py:554-560):
 //   out[b,j,d] = bf16(sst[j,d] + tmod[b, j*D + d]); onep[b,j,d] = bf16(1 + out) for scale rows
@@ -549,6 +564,29 @@ int ltx_rf_noise_velocity(const void* tokens, const void* noise, const float* t,
   const int64_t total = B * NC;
   hipLaunchKernelGGL(rf_noise_velocity_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)tokens, (const bf16_t*)noise, t, (bf16_t*)x_t, (bf16_t*)v_target, NC, total);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_rf_noise_velocity_f32(const void* tokens, int tokens_f32, const void* noise, int noise_f32,
+                              const float* t, float* x_t, float* v_target, int64_t B, int64_t NC,
+                              void* stream) {
+  LTX_CHECK_ARG(tokens && noise && t && (x_t || v_target) && B > 0 && NC > 0, "rf_noise_velocity_f32: bad args");
+  const int64_t total = B * NC;
+  const dim3 g(grid_for(total)), blk(256);
+  hipStream_t s = (hipStream_t)stream;
+  if (tokens_f32 && noise_f32)
+    hipLaunchKernelGGL((rf_noise_velocity_f32_kernel<float, float>), g, blk, 0, s, (const float*)tokens,
+                       (const float*)noise, t, x_t, v_target, NC, total);
+  else if (tokens_f32)
+    hipLaunchKernelGGL((rf_noise_velocity_f32_kernel<float, bf16_t>), g, blk, 0, s, (const float*)tokens,
+                       (const bf16_t*)noise, t, x_t, v_target, NC, total);
+  else if (noise_f32)
+    hipLaunchKernelGGL((rf_noise_velocity_f32_kernel<bf16_t, float>), g, blk, 0, s, (const bf16_t*)tokens,
+                       (const float*)noise, t, x_t, v_target, NC, total);
+  else
+    hipLaunchKernelGGL((rf_noise_velocity_f32_kernel<bf16_t, bf16_t>), g, blk, 0, s, (const bf16_t*)tokens,
+                       (const bf16_t*)noise, t, x_t, v_target, NC, total);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

@@ -13,6 +13,7 @@
 // image is lane-linear in LDS, so the XOR swizzle (16-B chunk ^= row & 7, conflict-free for the
 // 16x16x32 fragment reads) is applied to the per-lane SOURCE address and to the ds_read address.
 // Block order: XCD-aware (blocks b, b+8 share an XCD / L2) then grouped by 8 row-tiles.
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -548,18 +549,28 @@ static SplitWs ws_for(hipStream_t s) {
 static int g_variant = 0;  // tuning knob (ltx_gemm_set_variant): 0 default, 13 / 14 t-kernel with 256 / 224-row
                            // tiles, 30 / 31 / 32 w4 kernel (auto / 256 / 224-row tiles)
 
-template <int EPI, int R = 0>
-static int launch(const GemmParams& p, hipStream_t s) {
+// The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can
+// attribute its per-launch timings to the kernel rocprof will name).
+enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_W4 = 2, PATH_SMALL = 3 };
+struct GemmPlan {
+  GemmPath path;
+  int bmt;     // PATH_T / PATH_W4: tile height (256 or 224)
+  int splitk;  // PATH_SPLIT_T / PATH_SMALL: K slices (1 = none)
+  int nst;     // PATH_SMALL: LDS stages
+};
+
+static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
   if (g_force_small < 0) {
     const char* e = getenv("LTX_GEMM_SMALL");
     g_force_small = (e && e[0] == '1') ? 1 : 0;
   }
+  GemmPlan pl{PATH_SMALL, 0, 1, 2};
   // large tile once the grid still fills the chip with 256-row tiles, or fills at least 160 CUs
   // with 224-row tiles (one round at >= 62 %: the inference shapes, M = 3 x 1792 = 5376 -> 192
   // tiles, run 1.3x faster there than as 672 128x128 tiles)
   const int64_t big_tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + BN2 - 1) / BN2);
   const int64_t tiles224 = (int64_t)((p.M + 223) / 224) * ((p.N + BN2 - 1) / BN2);
-  if constexpr ((EPI == LTX_EPI_STORE || EPI == LTX_EPI_ACCUM) && R == 0) {
+  if ((epi == LTX_EPI_STORE || epi == LTX_EPI_ACCUM) && R == 0) {
     // under one round of 256x256 tiles with a long K (the full-mode weight gradients: [2048 x 2048]
     // over K = the token axis): split K over S slices of >= 16 K-tiles so the grid fills the chip
     if (!g_force_small && g_variant == 0 && p.K2 == 0 && p.M >= BM2 && p.N >= BN2 && big_tiles < 256) {
@@ -568,24 +579,8 @@ static int launch(const GemmParams& p, hipStream_t s) {
       while (S > 1 && nk / S < 16) --S;
       const SplitWs ws = ws_for(s);
       while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > ws.bytes) --S;
-      if (S > 1 && big_tiles * S >= 128) {  // else the 128x128 kernel's split fills the chip better
-        static bool sk_set = false;
-        if (!sk_set) {
-          (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-          sk_set = true;
-        }
-        GemmParams q = p;
-        q.ws = ws.ptr;
-        q.splitk = S;
-        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>), dim3((unsigned)(big_tiles * S)), dim3(512),
-                           LDS2, s, q);
-        LTX_LAUNCH_CHECK();
-        const int64_t n8 = (int64_t)p.M * (p.N / 8);
-        hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, R>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, q);
-        LTX_LAUNCH_CHECK();
-        return LTX_OK;
-      }
+      if (S > 1 && big_tiles * S >= 128)  // else the 128x128 kernel's split fills the chip better
+        return GemmPlan{PATH_SPLIT_T, 256, S, 2};
     }
   }
   if (!g_force_small && p.M >= BM2 && (big_tiles >= 256 || (g_variant == 0 && tiles224 >= 160))) {
@@ -593,69 +588,125 @@ static int launch(const GemmParams& p, hipStream_t s) {
     const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
     // fraction of the last round of 256 CUs that has work, per tile height
     auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
-    if (g_variant >= 33 && g_variant <= 36) return launch_w4(EPI, 32 - g_variant, p, s);  // measurement
+    if (g_variant >= 33 && g_variant <= 36) return GemmPlan{PATH_W4, 32 - g_variant, 1, 2};  // measurement
     if (g_variant >= 30 && g_variant <= 32) {  // one-wave-per-SIMD kernel: 30 auto, 31 BMT 256, 32 BMT 224
       const bool use224 = g_variant == 32 || (g_variant == 30 && fill(t224) > fill(t256) + 0.02);
-      return launch_w4(EPI, use224 ? 224 : 256, p, s);
+      return GemmPlan{PATH_W4, use224 ? 224 : 256, 1, 2};
     }
-    // gemm_nt_kernel_t with the tile height that fills the last round best; 13 forces BMT 256,
-    // 14 forces BMT 224
+    // the tile height that fills the last round best; variant 13 forces BMT 256, 14 forces 224
+    const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
+    return GemmPlan{PATH_T, use224 ? 224 : 256, 1, 2};
+  }
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int tiles = ntm * ntn;
+  const int nk = p.K / BK + p.K2 / BK;
+  // split-K when the grid leaves most CUs idle and each slice keeps >= 4 K-tiles
+  int S = 1;
+  if (tiles < 128 && nk >= 8) {
+    S = min(min(8, nk / 4), (256 + tiles - 1) / tiles);
+    // (capped at the 32 MiB the small-tile split-K was tuned and validated with)
+    const size_t cap = std::min<size_t>(ws_for(s).bytes, 32u << 20);
+    while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > cap) --S;
+  }
+  // at most one workgroup per CU: three LDS stages (two K-tiles in flight)
+  pl.splitk = S;
+  pl.nst = g_small_stages >= 2 ? g_small_stages : ((int64_t)tiles * S <= 256 ? 3 : 2);
+  return pl;
+}
+
+// rocprof's demangled name of the main kernel plan_gemm picks (the split-K tail kernel, when
+// there is one, is not named)
+static void describe_plan(const GemmPlan& pl, int epi, int R, char* buf, size_t len) {
+  switch (pl.path) {
+    case PATH_SPLIT_T:
+      snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, 256, 8, 0, 1, 8>(ltx::GemmParams)", epi, R);
+      break;
+    case PATH_T:
+      snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0, 0, 8>(ltx::GemmParams)", epi, R, pl.bmt,
+               pl.bmt == 224 ? 4 : 8);
+      break;
+    case PATH_W4:
+      snprintf(buf, len, "ltx::gemm_w4 (BMT %d)", pl.bmt);
+      break;
+    default:
+      snprintf(buf, len, "ltx::gemm_nt_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.nst);
+      break;
+  }
+}
+
+template <int EPI, int R = 0>
+static int launch(const GemmParams& p, hipStream_t s) {
+  const GemmPlan pl = plan_gemm(p, EPI, R, s);
+  if (pl.path == PATH_SPLIT_T) {
+    static bool sk_set = false;
+    if (!sk_set) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      sk_set = true;
+    }
+    const int64_t big_tiles = (int64_t)((p.M + BM2 - 1) / BM2) * ((p.N + BN2 - 1) / BN2);
+    GemmParams q = p;
+    q.ws = ws_for(s).ptr;
+    q.splitk = pl.splitk;
+    hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>), dim3((unsigned)(big_tiles * pl.splitk)), dim3(512),
+                       LDS2, s, q);
+    LTX_LAUNCH_CHECK();
+    const int64_t n8 = (int64_t)p.M * (p.N / 8);
+    hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, R>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, q);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+  if (pl.path == PATH_W4) return launch_w4(EPI, pl.bmt, p, s);
+  if (pl.path == PATH_T) {
     static bool t_set = false;
     if (!t_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       t_set = true;
     }
-    const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
-    if (use224)  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
-      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)t224), dim3(512), LDS2, s, p);
+    const int64_t ntn = (p.N + BN2 - 1) / BN2;
+    if (pl.bmt == 224)  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
+      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)(((p.M + 223) / 224) * ntn)), dim3(512),
+                         LDS2, s, p);
     else
-      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), dim3((unsigned)t256), dim3(512), LDS2, s, p);
+      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), dim3((unsigned)(((p.M + 255) / 256) * ntn)), dim3(512),
+                         LDS2, s, p);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+  const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
+  const int tiles = ntm * ntn;
+  const int S = pl.splitk, nst = pl.nst;
+  const bool deep = nst > 2;
+  if (deep) {
+    static bool d_set = false;
+    if (!d_set) {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, R, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                3 * STAGE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, R, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                4 * STAGE_BYTES);
+      d_set = true;
+    }
+  }
+  if (S > 1) {
+    GemmParams q = p;
+    q.ws = ws_for(s).ptr;
+    q.splitk = S;
+    if (nst == 4)
+      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 4>), dim3(tiles * S), dim3(GEMM_THREADS), 4 * STAGE_BYTES, s, q);
+    else if (deep)
+      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 3>), dim3(tiles * S), dim3(GEMM_THREADS), 3 * STAGE_BYTES, s, q);
+    else
+      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles * S), dim3(GEMM_THREADS), LDS_BYTES, s, q);
+    LTX_LAUNCH_CHECK();
+    const int64_t n8 = (int64_t)p.M * (p.N / 8);
+    hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, R>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, q);
+  } else if (nst == 4) {
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 4>), dim3(tiles), dim3(GEMM_THREADS), 4 * STAGE_BYTES, s, p);
+  } else if (deep) {
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 3>), dim3(tiles), dim3(GEMM_THREADS), 3 * STAGE_BYTES, s, p);
   } else {
-    const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
-    const int tiles = ntm * ntn;
-    const int nk = p.K / BK + p.K2 / BK;
-    // split-K when the grid leaves most CUs idle and each slice keeps >= 4 K-tiles
-    int S = 1;
-    if (tiles < 128 && nk >= 8) {
-      S = min(min(8, nk / 4), (256 + tiles - 1) / tiles);
-      // (capped at the 32 MiB the small-tile split-K was tuned and validated with)
-      const size_t cap = std::min<size_t>(ws_for(s).bytes, 32u << 20);
-      while (S > 1 && (size_t)S * p.M * p.N * sizeof(float) > cap) --S;
-    }
-    // at most one workgroup per CU: three LDS stages (two K-tiles in flight)
-    const int nst = g_small_stages >= 2 ? g_small_stages : ((int64_t)tiles * S <= 256 ? 3 : 2);
-    const bool deep = nst > 2;
-    if (deep) {
-      static bool d_set = false;
-      if (!d_set) {
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, R, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  3 * STAGE_BYTES);
-        (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, R, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  4 * STAGE_BYTES);
-        d_set = true;
-      }
-    }
-    if (S > 1) {
-      GemmParams q = p;
-      q.ws = ws_for(s).ptr;
-      q.splitk = S;
-      if (nst == 4)
-        hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 4>), dim3(tiles * S), dim3(GEMM_THREADS), 4 * STAGE_BYTES, s, q);
-      else if (deep)
-        hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 3>), dim3(tiles * S), dim3(GEMM_THREADS), 3 * STAGE_BYTES, s, q);
-      else
-        hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles * S), dim3(GEMM_THREADS), LDS_BYTES, s, q);
-      LTX_LAUNCH_CHECK();
-      const int64_t n8 = (int64_t)p.M * (p.N / 8);
-      hipLaunchKernelGGL((splitk_epilogue_kernel<EPI, R>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, q);
-    } else if (nst == 4) {
-      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 4>), dim3(tiles), dim3(GEMM_THREADS), 4 * STAGE_BYTES, s, p);
-    } else if (deep) {
-      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R, 3>), dim3(tiles), dim3(GEMM_THREADS), 3 * STAGE_BYTES, s, p);
-    } else {
-      hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles), dim3(GEMM_THREADS), LDS_BYTES, s, p);
-    }
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, R>), dim3(tiles), dim3(GEMM_THREADS), LDS_BYTES, s, p);
   }
   LTX_LAUNCH_CHECK();
   return LTX_OK;
@@ -680,6 +731,17 @@ extern "C" int ltx_gemm_set_variant(int variant) {
   return LTX_OK;
 }
 
+
+extern "C" int ltx_gemm_describe(int64_t M, int64_t N, int64_t K, int64_t K2, int epilogue, int64_t rank,
+                                 void* stream, char* buf, int64_t len) {
+  LTX_CHECK_ARG(buf && len > 0 && M > 0 && N > 0 && K > 0, "gemm_describe: bad args");
+  GemmParams p{};
+  p.M = (int)M; p.N = (int)N; p.K = (int)K; p.K2 = (int)K2;
+  const int R = (epilogue == LTX_EPI_LORA || epilogue == LTX_EPI_LORA_RESIDUAL ||
+                 epilogue == LTX_EPI_LORA_DGRAD_ACCUM) ? (int)rank : 0;
+  describe_plan(plan_gemm(p, epilogue, R, (hipStream_t)stream), epilogue, R, buf, (size_t)len);
+  return LTX_OK;
+}
 
 extern "C" int ltx_gemm_set_workspace(void* ptr, int64_t bytes) {
   LTX_CHECK_ARG(bytes >= 0 && (ptr != nullptr || bytes == 0) && ((uintptr_t)ptr % 16) == 0,

@@ -26,6 +26,7 @@ _SIGNATURES = {
     "ltx_unpatchify_bf16": [_p, _p, _i64, _i64, _i64, _i64, _i64, _p],
     "ltx_latent_coords": [_p, _i64, _i64, _i64, _i64, _p],
     "ltx_rf_noise_velocity": [_p, _p, _p, _p, _p, _i64, _i64, _p],
+    "ltx_rf_noise_velocity_f32": [_p, _i32, _p, _i32, _p, _p, _p, _i64, _i64, _p],
     "ltx_condition_lerp": [_p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p],
     "ltx_rf_prepare_tokens": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p],
     "ltx_rmsnorm_modulate_fwd": [_p, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _p],
@@ -47,6 +48,7 @@ _SIGNATURES = {
     "ltx_gemm_bf16_nt": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i32, _p, _p, _i64, _p,
                          _i64, _p, _i64, _f32, _i64, _i64, _p],
     "ltx_gemm_set_variant": [_i32],
+    "ltx_gemm_describe": [_i64, _i64, _i64, _i64, _i32, _i64, _p, _p, _i64],
     "ltx_add_bf16": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _p],
     "ltx_gated_residual_bf16": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p],
     "ltx_gemm_set_workspace": [_p, _i64],

@@ -97,6 +97,28 @@ def rf_noise_velocity(tokens, noise, t):
     return x_t, v
 
 
+def rf_noise_velocity_f32(tokens, noise, t, want_x=True, want_v=True):
+    """(x_t, v) in f32, the reference scheduler's result dtype (rf.py:376-386, 400-426): tokens /
+    noise bf16 or f32 [B, ...], t [B]. Returns None for the quantity not wanted."""
+    for x, n in ((tokens, "tokens"), (noise, "noise")):
+        if x.dtype not in (BF16, F32):
+            raise TypeError(f"{n}: bf16 or f32 expected, got {x.dtype}")
+        if not x.is_cuda:
+            raise _lib.LtxHipError(f"{n}: tensor is not on a ROCm device (no CPU fallback)")
+    if noise.shape != tokens.shape:
+        raise ValueError("rf_noise_velocity_f32: tokens and noise shapes differ")
+    B = tokens.shape[0]
+    t = t.to(device=tokens.device, dtype=F32).reshape(-1)
+    if t.numel() != B:
+        raise ValueError(f"rf_noise_velocity_f32: {t.numel()} timesteps for batch {B}")
+    x_t = torch.empty(tokens.shape, dtype=F32, device=tokens.device) if want_x else None
+    v = torch.empty(tokens.shape, dtype=F32, device=tokens.device) if want_v else None
+    call("ltx_rf_noise_velocity_f32", _p(tokens.contiguous()), 1 if tokens.dtype == F32 else 0,
+         _p(noise.contiguous()), 1 if noise.dtype == F32 else 0, _p(t.contiguous()), _p(x_t), _p(v),
+         B, tokens[0].numel(), _s())
+    return x_t, v
+
+
 def condition_lerp(tokens, ref, pose, out=None):
     """transformer3d.py:447-466 on token-major input (returns a new tensor unless out given)."""
     _need(tokens, BF16, "tokens")
@@ -282,8 +304,14 @@ def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
     Nk = k.shape[0] if kv_shared else k.shape[0] // B
     o = torch.empty(B * Nq, H * d, dtype=BF16, device=q.device) if out is None else out
     lse = torch.empty(B, H, Nq, dtype=F32, device=q.device)
+    bias = "true" if key_bias is not None else "false"
+    label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}>"
+    timer = _timer if (_timer is not None and _timer.wants(label)) else None
+    ev0 = timer.start() if timer is not None else None
     call("ltx_attn_fwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
          _rows(o, "o"), _p(lse), _p(key_bias), B, H, Nq, Nk, 0 if kv_shared else Nk, d, scale, _s())
+    if timer is not None:
+        timer.stop(label, 4.0 * B * H * Nq * Nk * d, ev0)
     return o, lse
 
 
@@ -298,10 +326,17 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
     dk = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dk is None else dk
     dv = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dv is None else dv
     delta = torch.empty(B, H, Nq, dtype=F32, device=dev)
+    bias = "true" if key_bias is not None else "false"
+    label = (f"attention backward: ltx::attn_delta_kernel<{d}> + ltx::attn_dkdv_kernel<{d}, {bias}> + "
+             f"ltx::attn_q_kernel<{d}, 1, {bias}>")
+    timer = _timer if (_timer is not None and _timer.wants(label)) else None
+    ev0 = timer.start() if timer is not None else None
     call("ltx_attn_bwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
          _rows(o, "o"), _p(do), _rows(do, "do"), _p(lse), _p(key_bias), _p(delta), _p(dq),
          _rows(dq, "dq"), 1 if dq.dtype == F32 else 0, _p(dk), _rows(dk, "dk"), _p(dv),
          _rows(dv, "dv"), B, H, Nq, Nk, 0 if kv_shared else Nk, d, scale, _s())
+    if timer is not None:
+        timer.stop(label, 8.0 * B * H * Nq * Nk * d, ev0)
     return dq, dk, dv
 
 
@@ -318,17 +353,39 @@ def batch_sum(x, B, out=None):
 # GEMM + LoRA
 # ---------------------------------------------------------------------------------------------
 class LaunchTimer:
-    """Brackets every GEMM launch of one (M, N, K, epilogue) with HIP events on the stream the
-    kernel is launched on (bench.py's live per-launch duration for the roofline figure)."""
+    """bench.py's live per-kernel timing: HIP events recorded on the launch stream around every
+    GEMM and attention launch while installed (set_launch_timer), each tagged with the kernel
+    rocprofv3 names for it (GEMMs: ltx_gemm_describe, the dispatcher's own choice) and the
+    launch's ALGORITHMIC FLOPs (GEMM 2*M*N*K without the LoRA K-extension; attention forward
+    4*B*H*Nq*Nk*d, backward twice that -- SURVEY 8d, no recompute)."""
 
-    def __init__(self, key):
-        self.key = key
-        self.pairs = []
+    def __init__(self, only=None):
+        self.records = []  # (label, flops, ev0, ev1)
+        self.only = only   # time only the launches of this label (None: every launch)
 
-    def mean_ms(self):
+    def start(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def stop(self, label, flops, ev0):
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.records.append((label, float(flops), ev0, ev1))
+
+    def wants(self, label):
+        return self.only is None or self.only == label
+
+    def summary(self):
+        """[{kernel, launches, ms, flops}] per label, largest total time first."""
         torch.cuda.synchronize()
-        ts = [a.elapsed_time(b) for a, b in self.pairs]
-        return sum(ts) / len(ts) if ts else float("nan")
+        agg = {}
+        for label, flops, a, b in self.records:
+            e = agg.setdefault(label, {"kernel": label, "launches": 0, "ms": 0.0, "flops": 0.0})
+            e["launches"] += 1
+            e["ms"] += a.elapsed_time(b)
+            e["flops"] += flops
+        return sorted(agg.values(), key=lambda e: -e["ms"])
 
 
 _timer = None
@@ -337,6 +394,19 @@ _timer = None
 def set_launch_timer(timer):
     global _timer
     _timer = timer
+
+
+_GEMM_NAMES = {}
+
+
+def gemm_kernel_name(M, N, K, K2, epilogue, rank=0):
+    """The kernel ltx_gemm_bf16_nt_ext launches for this call on the current stream."""
+    key = (M, N, K, K2, epilogue, rank, _s().value)
+    if key not in _GEMM_NAMES:
+        buf = ctypes.create_string_buffer(256)
+        call("ltx_gemm_describe", M, N, K, K2, EPI[epilogue], rank, _s(), buf, 256)
+        _GEMM_NAMES[key] = buf.value.decode()
+    return _GEMM_NAMES[key]
 
 
 _GEMM_WS = {}
@@ -373,19 +443,19 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
     ld0 = _rows(aux0, "aux0") if aux0 is not None else 0
     ld1 = _rows(aux1, "aux1") if aux1 is not None else 0
     ld2 = _rows(aux2, "aux2") if aux2 is not None else 0
-    timed = _timer is not None and _timer.key == (M, N, K, epilogue)
-    if timed:
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
     a2, w2 = ext if ext is not None else (None, None)
     K2 = a2.shape[1] if a2 is not None else 0
+    timer = _timer
+    if timer is not None:
+        label = gemm_kernel_name(M, N, K, K2, epilogue, rank)
+        timer = timer if timer.wants(label) else None
+    ev0 = timer.start() if timer is not None else None
     call("ltx_gemm_bf16_nt_ext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
          _rows(a2, "a2") if a2 is not None else 0, _p(w2), _rows(w2, "w2") if w2 is not None else 0,
          K2, _p(out), _rows(out, "out"), M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1),
          ld1, _p(aux2), ld2, float(alpha), rank, rows_per_batch, _s())
-    if timed:
-        ev1.record()
-        _timer.pairs.append((ev0, ev1))
+    if timer is not None:
+        timer.stop(label, 2.0 * M * N * K, ev0)
     return out
 
 

@@ -21,70 +21,72 @@ import torch
 from . import ops
 
 
+def _tokens_per_sample(samples_shape):
+    """The token count m the resolution shifts key on (rf.py:50-57, 115-122): the sequence axis of
+    a (b, t, c) token tensor, or the product of the spatial axes of a (b, c, h, w) /
+    (b, c, f, h, w) latent."""
+    rank = len(samples_shape)
+    if rank == 3:
+        return samples_shape[1]
+    if rank in (4, 5):
+        return math.prod(samples_shape[2:])
+    raise ValueError("Samples must have shape (b, t, c), (b, c, h, w) or (b, c, f, h, w)")
+
+
 def linear_quadratic_schedule(num_steps, threshold_noise=0.025, linear_steps=None):
-    """rf.py:25-46."""
+    """rf.py:25-46. The noise level s(i) climbs linearly to `threshold_noise` over the first
+    `linear_steps` steps, then along the quadratic a*i^2 + b*i + c that continues it and reaches 1
+    at i = num_steps; the schedule is 1 - s(i) for i < num_steps (same double-precision
+    expressions as the reference, so the f32 tensor is identical)."""
     if num_steps == 1:
         return torch.tensor([1.0])
-    if linear_steps is None:
-        linear_steps = num_steps // 2
-    linear_sigma_schedule = [i * threshold_noise / linear_steps for i in range(linear_steps)]
-    threshold_noise_step_diff = linear_steps - threshold_noise * num_steps
-    quadratic_steps = num_steps - linear_steps
-    quadratic_coef = threshold_noise_step_diff / (linear_steps * quadratic_steps ** 2)
-    linear_coef = threshold_noise / linear_steps - 2 * threshold_noise_step_diff / (
-        quadratic_steps ** 2)
-    const = quadratic_coef * (linear_steps ** 2)
-    quadratic_sigma_schedule = [quadratic_coef * (i ** 2) + linear_coef * i + const
-                                for i in range(linear_steps, num_steps)]
-    sigma_schedule = linear_sigma_schedule + quadratic_sigma_schedule + [1.0]
-    sigma_schedule = [1.0 - x for x in sigma_schedule]
-    return torch.tensor(sigma_schedule[:-1])
+    lin = num_steps // 2 if linear_steps is None else linear_steps
+    quad = num_steps - lin
+    gap = lin - threshold_noise * num_steps
+    a = gap / (lin * quad ** 2)
+    b = threshold_noise / lin - 2 * gap / (quad ** 2)
+    c = a * (lin ** 2)
+    levels = [i * threshold_noise / lin for i in range(lin)]
+    levels += [a * (i ** 2) + b * i + c for i in range(lin, num_steps)]
+    return torch.tensor([1.0 - s for s in levels])
 
 
 def simple_diffusion_resolution_dependent_timestep_shift(samples_shape, timesteps, n=32 * 32):
-    if len(samples_shape) == 3:
-        _, m, _ = samples_shape
-    elif len(samples_shape) in (4, 5):
-        m = math.prod(samples_shape[2:])
-    else:
-        raise ValueError("Samples must have shape (b, t, c), (b, c, h, w) or (b, c, f, h, w)")
-    snr = (timesteps / (1 - timesteps)) ** 2
-    shift_snr = torch.log(snr) + 2 * math.log(m / n)
-    return torch.sigmoid(0.5 * shift_snr)
+    """rf.py:108-127: shift the log-SNR of t by 2 log(m / n), m = tokens per sample."""
+    m = _tokens_per_sample(samples_shape)
+    log_snr = torch.log((timesteps / (1 - timesteps)) ** 2)
+    return torch.sigmoid(0.5 * (log_snr + 2 * math.log(m / n)))
 
 
 def time_shift(mu: float, sigma: float, t):
-    return math.exp(mu) / (math.exp(mu) + (1 / t - 1) ** sigma)
+    """rf.py:49-50: e^mu / (e^mu + (1/t - 1)^sigma)."""
+    e = math.exp(mu)
+    return e / (e + (1 / t - 1) ** sigma)
 
 
 def get_normal_shift(n_tokens, min_tokens=1024, max_tokens=4096, min_shift=0.95, max_shift=2.05):
-    m = (max_shift - min_shift) / (max_tokens - min_tokens)
-    b = min_shift - m * min_tokens
-    return m * n_tokens + b
+    """rf.py:53-62: the shift interpolated linearly in the token count through
+    (min_tokens, min_shift) and (max_tokens, max_shift)."""
+    slope = (max_shift - min_shift) / (max_tokens - min_tokens)
+    return slope * n_tokens + (min_shift - slope * min_tokens)
 
 
 def strech_shifts_to_terminal(shifts, terminal=0.1):
+    """rf.py:65-92 (the reference's spelling): rescale 1 - shifts so that the last entry lands on
+    `terminal`."""
     if shifts.numel() == 0:
         raise ValueError("The 'shifts' tensor must not be empty.")
-    if terminal <= 0 or terminal >= 1:
+    if not 0 < terminal < 1:
         raise ValueError("The terminal value must be between 0 and 1 (exclusive).")
-    one_minus_z = 1 - shifts
-    scale_factor = one_minus_z[-1] / (1 - terminal)
-    return 1 - (one_minus_z / scale_factor)
+    rest = 1 - shifts
+    return 1 - rest / (rest[-1] / (1 - terminal))
 
 
 def sd3_resolution_dependent_timestep_shift(samples_shape, timesteps, target_shift_terminal=None):
-    if len(samples_shape) == 3:
-        _, m, _ = samples_shape
-    elif len(samples_shape) in (4, 5):
-        m = math.prod(samples_shape[2:])
-    else:
-        raise ValueError("Samples must have shape (b, t, c), (b, c, h, w) or (b, c, f, h, w)")
-    shift = get_normal_shift(m)
-    out = time_shift(shift, 1, timesteps)
-    if target_shift_terminal is not None:
-        out = strech_shifts_to_terminal(out, target_shift_terminal)
-    return out
+    """rf.py:95-105: time_shift by the token-count-dependent normal shift, optionally stretched
+    to a terminal value."""
+    out = time_shift(get_normal_shift(_tokens_per_sample(samples_shape)), 1, timesteps)
+    return out if target_shift_terminal is None else strech_shifts_to_terminal(out, target_shift_terminal)
 
 
 @dataclass
@@ -219,14 +221,18 @@ class RectifiedFlowScheduler:
         return timesteps
 
     def noise_and_velocity(self, tokens, noise, timesteps):
-        """Both RF quantities in one kernel pass: (x_t, v_target), bf16."""
+        """Both RF quantities in one kernel pass, rounded to bf16 (what train_step casts them to,
+        training.py:143,146): (x_t, v_target)."""
         return ops.rf_noise_velocity(tokens, noise, timesteps.float())
 
     def add_noise(self, original_samples, noise, timesteps):
-        return self.noise_and_velocity(original_samples, noise, timesteps)[0]
+        """rf.py:376-386: (1 - t) x0 + t eps with [B] timesteps, in the reference's result dtype
+        (f32 for f32 timesteps: the f32 kernel form, no bf16 rounding)."""
+        return ops.rf_noise_velocity_f32(original_samples, noise, timesteps, want_v=False)[0]
 
     def build_velocity_target(self, tokens, noise, t):
-        return self.noise_and_velocity(tokens, noise, t)[1]
+        """rf.py:400-426: alpha'(t) x0 + sigma'(t) eps = eps - x0, f32 like the reference."""
+        return ops.rf_noise_velocity_f32(tokens, noise, t, want_x=False)[1]
 
     def alpha(self, t):
         return 1 - t

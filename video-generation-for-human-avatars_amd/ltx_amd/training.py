@@ -8,8 +8,10 @@ Differences that are deliberate and documented:
   * the backward is seeded directly with d(loss)/d(out) from the fused MSE kernel
     (grad scale = transformer_loss_weight / gradient_accumulation_steps, the reference's
     `loss / accum` then `.backward()`), so no host sync happens inside the step;
-  * t is sampled on the host-side torch RNG exactly as the reference (so seeds reproduce it) but
-    without the `float(t_low)` device->host round trip when the tensors are already on the host.
+  * t is sampled on `device` exactly as the reference (training.py:124-132: LogNormal on the
+    device RNG, then randn_like for the noise, so a seeded run draws the same t and noise); the
+    quantile clamp takes the bounds as 0-dim device tensors instead of `float(t_low)`, which gives
+    the same f32 result without the device->host round trip in every micro-step.
 """
 import math
 
@@ -30,7 +32,9 @@ def sample_timesteps(batch, config, device):
     t_raw = raw / (1 + raw)
     t_low = torch.quantile(t_raw, config.rf_quantile_min)
     t_high = torch.quantile(t_raw, config.rf_quantile_max)
-    return t_raw.clamp(min=float(t_low), max=float(t_high))
+    # clamp against the 0-dim f32 bounds: the reference's float(t_low) is the same f32 value
+    # (exact in double, cast back to f32 by clamp), so only the host sync differs
+    return t_raw.clamp(min=t_low, max=t_high)
 
 
 def train_step(model, batch, scheduler, patchifier, config, prompt_embeds, prompt_attention_mask,
@@ -51,7 +55,7 @@ def train_step(model, batch, scheduler, patchifier, config, prompt_embeds, promp
     # one coordinate set broadcast over the batch (identical per sample): one shared RoPE table
     coords = patchifier.get_latent_coords(F, H, W, 1, device).expand(B, -1, -1)
     if t is None:
-        t = sample_timesteps(B, config, "cpu").to(device)
+        t = sample_timesteps(B, config, device)
         t = scheduler.shift_timesteps(torch.Size([B, N, C]), t)
     t = t.to(device=device, dtype=torch.float32)
     if noise is None:
@@ -134,47 +138,172 @@ class FusedAdamW(torch.optim.Optimizer):
 
 class GradAllReduce:
     """Data-parallel averaging of the trainable gradients (LoRA f32 + caption projection bf16)
-    over torch.distributed (RCCL on ROCm, gloo in the CPU tests). Gradients are packed into
-    ~bucket_mb f32 buckets in reverse registration order (last blocks first, the order the
-    backward produces them) and reduced with AVG; bf16 grads are reduced in f32."""
+    over torch.distributed (RCCL on ROCm, gloo in the CPU tests), overlapped with the backward.
 
-    def __init__(self, params, bucket_mb=25.0, group=None):
-        self.params = [p for p in params if p.requires_grad]
+    * The gradients ARE views of per-dtype flat bucket buffers (``zero_grad`` installs them), so
+      the backward's kernels accumulate straight into what gets reduced: no pack, no copy-back.
+      f32 buckets are reduced in place; bf16 buckets (caption projection) through an f32 staging
+      copy (one cast each way), so the sum is f32 and rounds to bf16 once.
+    * Buckets (~bucket_mb of f32 each) follow ``order``: the order the backward completes the
+      grads (``Transformer3DModel.grad_ready_order``: last block first).
+    * ``arm()`` before the LAST micro-step's backward of an accumulation cycle: from then on a
+      bucket's async all-reduce (SUM) is launched as soon as all of its grads are final -- the
+      blocks' LoRA grads via the block hook at the end of each ``_BlockFn.backward``, autograd-
+      accumulated grads via post-accumulate-grad hooks -- while the remaining blocks' backward
+      runs. Buckets always launch in index order on every rank (a ready bucket waits for its
+      predecessors), so the collectives match across ranks.
+    * ``__call__()`` (before the optimizer step) launches whatever has not been launched, waits
+      (a stream wait, no host sync) and divides by the world size. Unarmed, it is the plain
+      post-backward reduction of the same buckets: the two paths are bitwise equal.
+    """
+
+    def __init__(self, params, bucket_mb=25.0, group=None, order=None):
+        params = [p for p in params if p.requires_grad]
+        if order is not None:
+            ids = {id(p) for p in params}
+            ordered = [p for p in order if id(p) in ids]
+            rest = [p for p in reversed(params) if id(p) not in {id(q) for q in ordered}]
+            params = ordered + rest
+        else:
+            params = list(reversed(params))  # registration order reversed
+        self.params = params
         self.group = group
-        self.buckets = []
-        cur, size = [], 0
-        for p in reversed(self.params):
-            cur.append(p)
-            size += p.numel() * 4
-            if size >= bucket_mb * 1e6:
-                self.buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(cur)
+        self.buckets = []  # each: {"dtype", "params", "offsets", "n", "flat", "stage"}
+        open_b = {}
+        for p in params:
+            b = open_b.get(p.dtype)
+            if b is None:
+                b = {"dtype": p.dtype, "params": [], "offsets": [], "n": 0, "flat": None,
+                     "stage": None}
+                open_b[p.dtype] = b
+                self.buckets.append(b)
+            b["params"].append(p)
+            b["offsets"].append(b["n"])
+            b["n"] += p.numel()
+            if b["n"] * 4 >= bucket_mb * 1e6:
+                del open_b[p.dtype]
+        self._where = {id(p): (bi, j) for bi, b in enumerate(self.buckets)
+                       for j, p in enumerate(b["params"])}
+        self._armed = False
+        self._pending = None   # per bucket: grads not yet final
+        self._launched = 0     # buckets [0, _launched) have their all-reduce in flight
+        self._works = []
+        self._hooks = []
+
+    # ---- buffers -------------------------------------------------------------------------
+    def _world(self):
+        if not (dist.is_available() and dist.is_initialized()):
+            return 1
+        return dist.get_world_size(self.group)
+
+    def _alloc(self, b):
+        if b["flat"] is None:
+            dev = b["params"][0].device
+            b["flat"] = torch.zeros(b["n"], dtype=b["dtype"], device=dev)
+            if b["dtype"] != torch.float32:
+                b["stage"] = torch.empty(b["n"], dtype=torch.float32, device=dev)
+
+    def _view(self, b, j):
+        p, off = b["params"][j], b["offsets"][j]
+        return b["flat"][off:off + p.numel()].view_as(p)
+
+    @torch.no_grad()
+    def zero_grad(self):
+        """Zero every bucket (one fill each) and make each p.grad the view of its slice (in place
+        of optimizer.zero_grad(set_to_none=True), which would detach the grads from the buckets)."""
+        for b in self.buckets:
+            self._alloc(b)
+            b["flat"].zero_()
+            for j, p in enumerate(b["params"]):
+                p.grad = self._view(b, j)
+
+    @torch.no_grad()
+    def _adopt_grads(self, b):
+        """Make the bucket's grads views again if something replaced them (copy them in)."""
+        self._alloc(b)
+        for j, p in enumerate(b["params"]):
+            v = self._view(b, j)
+            g = p.grad
+            if g is not None and g.data_ptr() == v.data_ptr() and g.dtype == v.dtype:
+                continue
+            if g is None:
+                v.zero_()
+            else:
+                v.copy_(g)
+            p.grad = v
+
+    # ---- overlap with the backward -----------------------------------------------------------
+    def install(self, model):
+        """Hook the model: each block reports its finished grads (LoRA, written by the block's
+        kernels) at the end of its backward; autograd-accumulated params report through
+        post-accumulate-grad hooks."""
+        block_params = {}
+        for blk in getattr(model, "transformer_blocks", ()):
+            mine = [p for p in blk.parameters() if id(p) in self._where]
+            if mine:
+                block_params[id(blk)] = mine
+                hooks = blk.__dict__.setdefault("_grad_ready_hooks", [])
+                hooks.append(lambda b, ps=mine: self._ready(ps))
+        in_blocks = {id(p) for ps in block_params.values() for p in ps}
+        for p in self.params:
+            if id(p) not in in_blocks:
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda q: self._ready([q])))
+        return self
+
+    def arm(self):
+        """The next backward is the last of the accumulation cycle: reduce during it."""
+        if self._world() == 1:
+            return
+        for b in self.buckets:
+            self._adopt_grads(b)
+        self._armed = True
+        self._pending = [set(id(p) for p in b["params"]) for b in self.buckets]
+        self._launched = 0
+        self._works = []
+
+    def _ready(self, ps):
+        if not self._armed:
+            return
+        for p in ps:  # (each grad must be final after one report: one accumulation per backward)
+            bi, _ = self._where[id(p)]
+            self._pending[bi].discard(id(p))
+        while self._launched < len(self.buckets) and not self._pending[self._launched]:
+            self._launch(self._launched)
+
+    @torch.no_grad()
+    def _launch(self, bi):
+        b = self.buckets[bi]
+        buf = b["flat"]
+        if b["stage"] is not None:
+            b["stage"].copy_(buf)  # bf16 -> f32
+            buf = b["stage"]
+        self._works.append(dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group,
+                                           async_op=True))
+        self._launched = bi + 1
 
     @torch.no_grad()
     def __call__(self):
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
+        world = self._world()
+        if world == 1:
+            self._armed = False
             return
-        world = dist.get_world_size(self.group)
-        pending = []
-        for bucket in self.buckets:
-            grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in bucket]
-            flat = torch.cat([g.reshape(-1).float() for g in grads])
-            work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            pending.append((bucket, flat, work))
-        for bucket, flat, work in pending:
-            work.wait()
-            flat.div_(world)
-            off = 0
-            for p in bucket:
-                n = p.numel()
-                g = flat[off:off + n].view_as(p).to(p.dtype)
-                if p.grad is None:
-                    p.grad = g
-                else:
-                    p.grad.copy_(g)
-                off += n
+        if not self._armed:
+            for b in self.buckets:
+                self._adopt_grads(b)
+            self._launched = 0
+            self._works = []
+        while self._launched < len(self.buckets):
+            self._launch(self._launched)
+        for w in self._works:
+            w.wait()
+        for b in self.buckets:
+            if b["stage"] is not None:
+                b["stage"].div_(world)
+                b["flat"].copy_(b["stage"])  # f32 -> bf16, one rounding
+            else:
+                b["flat"].div_(world)
+        self._armed = False
+        self._works = []
 
 
 def train_one_epoch(model, dataloader, optimizer, scheduler, patchifier, device, config,
@@ -187,17 +316,26 @@ def train_one_epoch(model, dataloader, optimizer, scheduler, patchifier, device,
     an optimizer step logs them (one host sync per optimizer step, as the reference's .item())."""
     model.train()
     accum = max(1, int(config.gradient_accumulation_steps))
-    optimizer.zero_grad(set_to_none=True)
+
+    def zero():
+        if reducer is not None:
+            reducer.zero_grad()  # grads stay views of the reducer's buckets
+        else:
+            optimizer.zero_grad(set_to_none=True)
+    zero()
     losses = []
     for batch_idx, batch in enumerate(dataloader):
+        last = (batch_idx + 1) % accum == 0
+        if last and reducer is not None:
+            reducer.arm()  # the all-reduce overlaps this micro-step's backward
         loss, rel_mse, nrmse, loss_dict = train_step(model, batch, scheduler, patchifier, config,
                                                      prompt_embeds, prompt_attention_mask, device)
         losses.append(loss.detach().float())
-        if (batch_idx + 1) % accum == 0:
+        if last:
             if reducer is not None:
                 reducer()
             optimizer.step()
-            optimizer.zero_grad(set_to_none=True)
+            zero()
             global_step += 1
             if log_fn is not None:
                 payload = {"train/loss": float(loss), "train/rel_mse": float(rel_mse),
@@ -232,7 +370,10 @@ def train_loop(model, config, dataloader, prompt_embeds, prompt_attention_mask, 
                                 sampler=config.rf_sampler, shift=config.rf_shift)
     params = [p for p in model.parameters() if p.requires_grad]
     optimizer = FusedAdamW(params, lr=config.learning_rate)
-    reducer = GradAllReduce(params) if (dist.is_available() and dist.is_initialized()) else None
+    reducer = None
+    if dist.is_available() and dist.is_initialized():
+        order = model.grad_ready_order() if hasattr(model, "grad_ready_order") else None
+        reducer = GradAllReduce(params, order=order).install(model)
     best = float("inf")
     global_step = 0
     for epoch in range(config.num_epochs or 0):

@@ -626,6 +626,11 @@ class _BlockFn(torch.autograd.Function):
                 ops.colsum_into(dmods[:, 1], dx1, h, rstd1, mode=2, rows_per_group=rpm,
                                 sum_groups=False, accumulate=False)
         dm = dmods if full else None
+        # every grad this block's backward writes straight into .grad (the LoRA adapters) is
+        # enqueued now: tell the DP reducer (training.GradAllReduce), which can start their
+        # bucket's all-reduce beside the remaining blocks' backward
+        for cb in getattr(blk, "_grad_ready_hooks", ()):
+            cb(blk)
         return (None, None, None, None, dh, denc, dm, None, *grads_lora)
 
 
@@ -925,6 +930,24 @@ class Transformer3DModel(nn.Module):
         if patchifier is not None:
             model.patchifier = patchifier
         return model
+
+    def grad_ready_order(self):
+        """The trainable parameters in the order the backward finishes their gradients: the
+        blocks' own parameters from the last block to the first (their grads are complete when
+        that block's backward returns), then everything upstream of the blocks (caption
+        projection, AdaLN-single, patchify_proj) and the head. training.GradAllReduce buckets in
+        this order so the first buckets can be reduced while the backward still runs."""
+        seen, order = set(), []
+        for blk in reversed(self.transformer_blocks):
+            for p in blk.parameters():
+                if p.requires_grad and id(p) not in seen:
+                    seen.add(id(p))
+                    order.append(p)
+        for p in self.parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                order.append(p)
+        return order
 
     @property
     def dtype(self):
