@@ -265,7 +265,18 @@ static __device__ __forceinline__ uint64_t rt_stamp() { return __builtin_amdgcn_
 // less LDS fragment traffic per MFMA. Measured with this schedule (2 stages, one barrier per
 // K-tile): bit-identical results but 10-25 % slower than NW = 8 on every training shape -- at one
 // wave per SIMD nothing covers the mid-tile DMA wait. Not dispatched; kept for the next schedule.
-template <int EPI, int R, int BMT, int DMAW, int STAMP = 0, int SPLIT = 0, int NW = 8>
+// XR3: the X operand (activations, streamed from HBM / Infinity Cache) in a ring of THREE tiles
+// and W in a ring of two ([X0 X1 X2 | W0 W1]: 160 KiB at BMT 256, 148 KiB at 224). Tile t+2's X
+// pieces go out at the start of tile t (its buffer held tile t-1, free since tile t-1's mid-tile
+// barrier), its W pieces right after tile t's mid-tile barrier; that barrier then waits only for
+// tile t+1 and leaves tile t+2's X in flight: X gets 1.75 K-tiles to land, W a whole one (the
+// two-stage schedule gives them one and 0.75).
+template <int BMT, int XR3>
+constexpr int lds_t_bytes() {
+  return XR3 ? 3 * BMT * BK * 2 + 2 * WT2 : LDS2;
+}
+
+template <int EPI, int R, int BMT, int DMAW, int STAMP = 0, int SPLIT = 0, int NW = 8, int XR3 = 0>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams p) {
   static_assert(BMT == 256 || BMT == 224, "tile height");
   static_assert(NW == 8 || NW == 4, "waves");
@@ -346,10 +357,13 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
   };
+  // LDS byte offsets of X / W buffer `buf`
+  auto xaddr = [&](int buf) -> int { return XR3 ? buf * XT : buf * ST; };
+  auto waddr = [&](int buf) -> int { return XR3 ? 3 * XT + buf * WT2 : buf * ST + XT; };
   auto stage_x = [&](int st, int kt) {
     if (kt == nk_main && nk_main > 0) set_x(true);  // ext tiles come last, in issue order
     const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-    const uint32_t l = lds0 + st * ST + wv * (PPW * 1024);
+    const uint32_t l = lds0 + xaddr(st) + wv * (PPW * 1024);
 #pragma unroll
     for (int i = 0; i < PPW; ++i)
       if (i < xp) glds_s(xo[i], sb, l + i * 1024);
@@ -357,7 +371,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   auto stage_w = [&](int st, int kt) {
     if (kt == nk_main && nk_main > 0) set_w(true);
     const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
-    const uint32_t l = lds0 + st * ST + XT + wv * (PPW * 1024);
+    const uint32_t l = lds0 + waddr(st) + wv * (PPW * 1024);
 #pragma unroll
     for (int i = 0; i < PPW; ++i)
       if (i < wp) glds_s(wo[i], sb, l + i * 1024);
@@ -383,7 +397,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     for (int nh = 0; nh < 2; ++nh)
 #pragma unroll
       for (int i = 0; i < NFH; ++i)
-        aoff[2 * h + nh][i] = XT + swz(wn * WTN + nh * (WTN / 2) + i * 16 + frow, h * 4 + fchunk);
+        aoff[2 * h + nh][i] = swz(wn * WTN + nh * (WTN / 2) + i * 16 + frow, h * 4 + fchunk);
   }
   stage_x(0, 0);
   stage_w(0, 0);
@@ -403,9 +417,9 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   if constexpr (STAMP) st1 = rt_stamp();
   s16x8 aE[NFH], aO[NFH], b0[MF], b1[MF];  // A even/odd quarter sets, B per k-half
 #pragma unroll
-  for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(smem + aoff[0][i]);
+  for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(smem + waddr(0) + aoff[0][i]);
 #pragma unroll
-  for (int j = 0; j < MF; ++j) b0[j] = *(const s16x8*)(smem + boff[0][j]);
+  for (int j = 0; j < MF; ++j) b0[j] = *(const s16x8*)(smem + xaddr(0) + boff[0][j]);
 #define LTX_MFMA_T(AS, BS, NH)                                                                        \
   __builtin_amdgcn_sched_barrier(0);                                                                  \
   _Pragma("unroll") for (int i = 0; i < NFH; ++i)                                                     \
@@ -414,44 +428,61 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   __builtin_amdgcn_sched_barrier(0);
   if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 
-  int cur = 0;
-  bool pend_w = false;  // W half of tile kt+1's DMA still to issue in Q0
+  int cur = 0;           // two-stage schedule: tile kt's stage; XR3: tile kt's W buffer
+  int xcur = 0;          // XR3: tile kt's X buffer (kt % 3)
+  bool pend_w = false;   // two-stage: W half of tile kt+1's DMA still to issue in Q0
   for (int kt = 0; kt < nk; ++kt) {
-    const char* st = smem + cur * ST;
+    const char* xs = smem + (XR3 ? xaddr(xcur) : xaddr(cur));
+    const char* ws = smem + waddr(cur);
     // Q0 (h0, n0): prefetch A(Q1)
 #pragma unroll
-    for (int i = 0; i < NFH; ++i) aO[i] = *(const s16x8*)(st + aoff[1][i]);
-    if (pend_w) {
+    for (int i = 0; i < NFH; ++i) aO[i] = *(const s16x8*)(ws + aoff[1][i]);
+    if constexpr (XR3) {
+      if (kt + 2 < nk) stage_x(xcur == 0 ? 2 : xcur - 1, kt + 2);  // tile kt-1's X buffer
+    } else if (pend_w) {
       stage_w(cur ^ 1, kt + 1);
       pend_w = false;
     }
     LTX_MFMA_T(aE, b0, 0)
     // Q1 (h0, n1): prefetch A(Q2), B(h1)
 #pragma unroll
-    for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(st + aoff[2][i]);
+    for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(ws + aoff[2][i]);
 #pragma unroll
-    for (int j = 0; j < MF; ++j) b1[j] = *(const s16x8*)(st + boff[1][j]);
+    for (int j = 0; j < MF; ++j) b1[j] = *(const s16x8*)(xs + boff[1][j]);
     LTX_MFMA_T(aO, b0, 1)
     // Q2 (h1, n0): prefetch A(Q3)
 #pragma unroll
-    for (int i = 0; i < NFH; ++i) aO[i] = *(const s16x8*)(st + aoff[3][i]);
+    for (int i = 0; i < NFH; ++i) aO[i] = *(const s16x8*)(ws + aoff[3][i]);
     LTX_MFMA_T(aE, b1, 0)
     // all reads of tile t issued: wait tile t+1, free tile t's stage, DMA tile t+2's X into it
     if (kt + 1 < nk) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (kt + 2 < nk) {
-        stage_x(cur, kt + 2);
-        pend_w = true;
+      if constexpr (XR3) {
+        // tile t+1 landed; tile t+2's X (this wave's youngest xp pieces) may stay in flight
+        if (kt + 2 < nk && xp == 8)
+          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else if (kt + 2 < nk && xp == 4)
+          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (kt + 2 < nk) stage_w(cur, kt + 2);  // tile t's W buffer
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (kt + 2 < nk) {
+          stage_x(cur, kt + 2);
+          pend_w = true;
+        }
       }
-      const char* sn = smem + (cur ^ 1) * ST;
+      const char* xn = smem + (XR3 ? xaddr(xcur == 2 ? 0 : xcur + 1) : xaddr(cur ^ 1));
+      const char* wn_ = smem + waddr(cur ^ 1);
       // Q3 (h1, n1) of tile t: prefetch A(Q0), B(h0) of tile t+1
 #pragma unroll
-      for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(sn + aoff[0][i]);
+      for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(wn_ + aoff[0][i]);
 #pragma unroll
-      for (int j = 0; j < MF; ++j) b0[j] = *(const s16x8*)(sn + boff[0][j]);
+      for (int j = 0; j < MF; ++j) b0[j] = *(const s16x8*)(xn + boff[0][j]);
     }
     LTX_MFMA_T(aO, b1, 1)
     cur ^= 1;
+    xcur = xcur == 2 ? 0 : xcur + 1;
   }
 #undef LTX_MFMA_T
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -546,17 +577,23 @@ static SplitWs ws_for(hipStream_t s) {
   auto it = g_ws_stream.find(s);
   return it != g_ws_stream.end() ? it->second : g_ws_default;
 }
-static int g_variant = 0;  // tuning knob (ltx_gemm_set_variant): 0 default, 13 / 14 t-kernel with 256 / 224-row
-                           // tiles, 30 / 31 / 32 w4 kernel (auto / 256 / 224-row tiles)
+// tuning knob (ltx_gemm_set_variant, or LTX_GEMM_VARIANT at load for whole-step A/B runs): 0 default,
+// 13 / 14 t-kernel with 256 / 224-row tiles, 30-32 w4 kernel, 40-42 ns kernel, 50 XR3 schedule,
+// 60 / 61 / 62 tw kernel (auto / 256 / 224-row tiles)
+static int g_variant = [] {
+  const char* e = getenv("LTX_GEMM_VARIANT");
+  return e ? atoi(e) : 0;
+}();
 
 // The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can
 // attribute its per-launch timings to the kernel rocprof will name).
-enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_W4 = 2, PATH_SMALL = 3 };
+enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_W4 = 2, PATH_SMALL = 3, PATH_NS = 4, PATH_TW = 5 };
 struct GemmPlan {
   GemmPath path;
   int bmt;     // PATH_T / PATH_W4: tile height (256 or 224)
   int splitk;  // PATH_SPLIT_T / PATH_SMALL: K slices (1 = none)
   int nst;     // PATH_SMALL: LDS stages
+  int xr3 = 0; // PATH_T: three-tile X ring (gemm_nt_kernel_t XR3)
 };
 
 static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
@@ -589,13 +626,22 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
     // fraction of the last round of 256 CUs that has work, per tile height
     auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
     if (g_variant >= 33 && g_variant <= 36) return GemmPlan{PATH_W4, 32 - g_variant, 1, 2};  // measurement
+    if (g_variant >= 40 && g_variant <= 42) {  // 4-slot ring of 32-deep steps: 40 auto, 41 BMT 256, 42 BMT 224
+      const bool use224 = g_variant == 42 || (g_variant == 40 && fill(t224) > fill(t256) + 0.02);
+      return GemmPlan{PATH_NS, use224 ? 224 : 256, 1, 2};
+    }
     if (g_variant >= 30 && g_variant <= 32) {  // one-wave-per-SIMD kernel: 30 auto, 31 BMT 256, 32 BMT 224
       const bool use224 = g_variant == 32 || (g_variant == 30 && fill(t224) > fill(t256) + 0.02);
       return GemmPlan{PATH_W4, use224 ? 224 : 256, 1, 2};
     }
     // the tile height that fills the last round best; variant 13 forces BMT 256, 14 forces 224
     const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
-    return GemmPlan{PATH_T, use224 ? 224 : 256, 1, 2};
+    // four-wave kernel (gemm_tw.hip) on tile-aligned shapes: variant 60 (auto), 61 (256), 62 (224)
+    if (g_variant >= 60 && g_variant <= 62 && p.N % BN2 == 0 && R == 0 && tw_supports(epi)) {
+      const bool tw224 = g_variant == 62 || (g_variant == 60 && use224);
+      if (p.M % (tw224 ? 224 : 256) == 0) return GemmPlan{PATH_TW, tw224 ? 224 : 256, 1, 2};
+    }
+    return GemmPlan{PATH_T, use224 ? 224 : 256, 1, 2, g_variant == 50 ? 1 : 0};
   }
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int tiles = ntm * ntn;
@@ -622,11 +668,21 @@ static void describe_plan(const GemmPlan& pl, int epi, int R, char* buf, size_t 
       snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, 256, 8, 0, 1, 8>(ltx::GemmParams)", epi, R);
       break;
     case PATH_T:
-      snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0, 0, 8>(ltx::GemmParams)", epi, R, pl.bmt,
-               pl.bmt == 224 ? 4 : 8);
+      if (pl.xr3)
+        snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0, 0, 8, 1>(ltx::GemmParams)", epi, R, pl.bmt,
+                 pl.bmt == 224 ? 4 : 8);
+      else
+        snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0, 0, 8>(ltx::GemmParams)", epi, R, pl.bmt,
+                 pl.bmt == 224 ? 4 : 8);
       break;
     case PATH_W4:
       snprintf(buf, len, "ltx::gemm_w4 (BMT %d)", pl.bmt);
+      break;
+    case PATH_NS:
+      snprintf(buf, len, "ltx::gemm_ns_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt);
+      break;
+    case PATH_TW:
+      snprintf(buf, len, "ltx::gemm_tw_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt);
       break;
     default:
       snprintf(buf, len, "ltx::gemm_nt_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.nst);
@@ -657,20 +713,32 @@ static int launch(const GemmParams& p, hipStream_t s) {
     return LTX_OK;
   }
   if (pl.path == PATH_W4) return launch_w4(EPI, pl.bmt, p, s);
+  if (pl.path == PATH_NS) return launch_ns(EPI, pl.bmt, p, s);
+  if (pl.path == PATH_TW) return launch_tw(EPI, pl.bmt, p, s);
   if (pl.path == PATH_T) {
     static bool t_set = false;
     if (!t_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 0, 0, 8, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_t_bytes<256, 1>());
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4, 0, 0, 8, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_t_bytes<224, 1>());
       t_set = true;
     }
     const int64_t ntn = (p.N + BN2 - 1) / BN2;
-    if (pl.bmt == 224)  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
-      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), dim3((unsigned)(((p.M + 223) / 224) * ntn)), dim3(512),
-                         LDS2, s, p);
-    else
-      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), dim3((unsigned)(((p.M + 255) / 256) * ntn)), dim3(512),
-                         LDS2, s, p);
+    const dim3 g224((unsigned)(((p.M + 223) / 224) * ntn)), g256((unsigned)(((p.M + 255) / 256) * ntn));
+    constexpr int L224 = lds_t_bytes<224, 1>(), L256 = lds_t_bytes<256, 1>();
+    if (pl.xr3) {
+      if (pl.bmt == 224)
+        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4, 0, 0, 8, 1>), g224, dim3(512), L224, s, p);
+      else
+        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 0, 0, 8, 1>), g256, dim3(512), L256, s, p);
+    } else if (pl.bmt == 224) {  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
+      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), g224, dim3(512), LDS2, s, p);
+    } else {
+      hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), g256, dim3(512), LDS2, s, p);
+    }
     LTX_LAUNCH_CHECK();
     return LTX_OK;
   }

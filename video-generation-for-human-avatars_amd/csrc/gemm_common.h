@@ -173,5 +173,8 @@ constexpr int BM2 = 256, BN2 = 256;
 constexpr int C_STRIDE2 = BN2 * 2 + 8;  // bf16 C image row stride of the 256-wide tiles
 
 int launch_w4(int epi, int bmt, const GemmParams& p, hipStream_t s);  // gemm_w4.hip
+int launch_ns(int epi, int bmt, const GemmParams& p, hipStream_t s);  // gemm_ns.hip
+int launch_tw(int epi, int bmt, const GemmParams& p, hipStream_t s);  // gemm_tw.hip
+bool tw_supports(int epi);                                              // gemm_tw.hip
 
 }  // namespace ltx
