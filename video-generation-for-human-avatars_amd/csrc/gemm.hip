@@ -637,7 +637,8 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
     // the tile height that fills the last round best; variant 13 forces BMT 256, 14 forces 224
     const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
     // four-wave kernel (gemm_tw.hip) on tile-aligned shapes: variant 60 (auto), 61 (256), 62 (224)
-    if (g_variant >= 60 && g_variant <= 62 && p.N % BN2 == 0 && R == 0 && tw_supports(epi)) {
+    if (g_variant >= 60 && g_variant <= 62 && p.N % BN2 == 0 && R == 0 && tw_supports(epi) &&
+        (p.K / BK + p.K2 / BK) % 2 == 0) {
       const bool tw224 = g_variant == 62 || (g_variant == 60 && use224);
       if (p.M % (tw224 ? 224 : 256) == 0) return GemmPlan{PATH_TW, tw224 ? 224 : 256, 1, 2};
     }

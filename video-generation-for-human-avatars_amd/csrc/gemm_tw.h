@@ -224,8 +224,8 @@ __global__ __launch_bounds__(256, 1) void gemm_tw_kernel(const GemmParams p) {
   // done with step g's buffer and step g+2's DMA goes into it; at QW step g+1 has landed and its
   // k-half-0 fragments are read beside the last MFMAs. The MFMA stream is
   // generated with compile-time indices, so every accumulator / fragment index is a constant.
-  auto iter = [&](int g) {
-    const int c = g & 1;
+  auto iter = [&](auto c_tag) {
+    constexpr int c = decltype(c_tag)::value;  // buffer of this K-step (steps alternate)
     const char* bc = smem + c * SB;
     const char* bn = smem + (c ^ 1) * SB;
     auto step = [&](auto qc) {
@@ -347,10 +347,14 @@ __global__ __launch_bounds__(256, 1) void gemm_tw_kernel(const GemmParams p) {
   int c_kt = 0, c_tile = 0, c_m0 = 0, c_n0 = 0;
   coords(0, c_m0, c_n0);
   zero_acc();
-  for (int g = 0; g < total; ++g) {
-    iter(g);
+  // two K-steps per trip (buffers 0, 1 as constants); nk is even, so tiles end on odd steps
+  for (int g = 0; g < total; g += 2) {
+    iter(std::integral_constant<int, 0>{});
     dma_advance();
-    if (++c_kt == nk) {
+    iter(std::integral_constant<int, 1>{});
+    dma_advance();
+    c_kt += 2;
+    if (c_kt == nk) {
       epilogue(c_m0, c_n0);
       zero_acc();
       c_kt = 0;
