@@ -128,7 +128,8 @@ def _sdpa_ref(q, k, v, B, H, d, bias=None):
 
 @pytest.mark.parametrize("B,H,Nq,Nk,d,masked", [(2, 4, 128, 128, 64, False), (1, 3, 100, 77, 64, True),
                                                  (2, 4, 64, 4, 32, True), (2, 2, 256, 256, 32, False),
-                                                 (1, 32, 1792, 256, 64, True)])
+                                                 (1, 32, 1792, 256, 64, True), (2, 2, 640, 300, 64, False),
+                                                 (1, 2, 200, 520, 64, True)])
 def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
     from ltx_amd import ops
     scale = d ** -0.5
