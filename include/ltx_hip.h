@@ -199,6 +199,20 @@ int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, int64_t ldw,
                          int64_t ld1, const void* aux2, int64_t ld2, float alpha, int64_t rank,
                          int64_t rows_per_batch, void* stream);
 
+/* ltx_gemm_bf16_nt_ext with a GROUPED K extension: output columns [g*G, (g+1)*G) (G =
+ * ext_group_cols, a multiple of 256 dividing N) read their A2 rows at column offset
+ * g*ext_group_stride. One launch then computes several projections of one shared input that
+ * each carry their own fused LoRA operand: the attn2 text K/V of all 28 blocks
+ * (attention.py:1004-1014 per block, with the peft adapters of training.py:50-68).
+ * ext_group_cols = 0 is ltx_gemm_bf16_nt_ext. */
+int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, int64_t ldw, const void* A2,
+                          int64_t lda2, const void* W2, int64_t ldw2, int64_t K2,
+                          int64_t ext_group_cols, int64_t ext_group_stride, void* C, int64_t ldc,
+                          int64_t M, int64_t N, int64_t K, int epilogue, const void* bias,
+                          const void* aux0, int64_t ld0, const void* aux1, int64_t ld1,
+                          const void* aux2, int64_t ld2, float alpha, int64_t rank,
+                          int64_t rows_per_batch, void* stream);
+
 /* Tuning knob for A/B measurements of GEMM schedules (0: per-tile DMA split over two quarters,
  * the default; 1: one burst). Process-global. */
 int ltx_gemm_set_variant(int variant);
@@ -224,6 +238,13 @@ int ltx_gemm_set_stream_workspace(void* stream, void* ptr, int64_t bytes);
 int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk,
                   float* out, int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha,
                   void* split, int64_t ld_split, int64_t K2, void* stream);
+/* ltx_lora_down over `groups` adapters in one launch: group g reads x + g*gx, Wr + g*gw and
+ * writes out + g*go, split + g*gs (element offsets; 0 = shared operand). The text-side lora_A of
+ * all blocks' attn2 to_k / to_v (one shared input, 56 adapters) and their lora_B dgrads. */
+int ltx_lora_down_grouped(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk,
+                          float* out, int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha,
+                          void* split, int64_t ld_split, int64_t K2, int64_t groups, int64_t gx,
+                          int64_t gw, int64_t go, int64_t gs, void* stream);
 /* 3-term bf16 split of an f32 [R, r] matrix (element (i,j) at src[i*rs + j*cs], times scale) into
  * a K-extension operand out [R, K2] (K2 = round_up(3r, 64)): role 0 (activation) rows
  * [hi|hi|lo|0], role 1 (weight) rows [hi|lo|hi|0]; their dot product reproduces the f32 product
@@ -237,6 +258,12 @@ int ltx_lora_split_bf16(const float* src, int64_t rs, int64_t cs, float scale, i
 int ltx_lora_wgrad(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw,
                    int64_t on, int64_t oj, int64_t M, int64_t N, int64_t r, float alpha,
                    int accumulate, void* stream);
+/* ltx_lora_wgrad over `groups` adapters in one launch: group g reads y + g*gy, u + g*gu and
+ * writes dw + g*gd (element offsets; 0 = shared y or u; the outputs must not overlap). */
+int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw,
+                           int64_t on, int64_t oj, int64_t M, int64_t N, int64_t r, float alpha,
+                           int accumulate, int64_t groups, int64_t gy, int64_t gu, int64_t gd,
+                           void* stream);
 
 /* ---- small ops -------------------------------------------------------------------------------- */
 /* AdaLayerNormSingle sinusoid: out[b,:] = bf16([cos(s*t*f), sin(s*t*f)]) (256 ch), s = scale */

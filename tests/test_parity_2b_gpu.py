@@ -184,3 +184,33 @@ def test_ltx2b_loss_curve_shared_prompt():
             curves[dt].append(float(((r["sample"].float() - r["v_target"].float()) ** 2).mean()))
     for i in range(20):
         _loss_crit(f"step {i}", curves["build"][i], curves[torch.bfloat16][i], curves[torch.float32][i])
+
+
+def test_text_stack_matches_per_block():
+    """The batched text side (_TextStack: all blocks' text K/V as one grouped-extension GEMM, the
+    2n adapters' lora_down / lora_wgrad as grouped launches, one encoder-gradient GEMM over
+    K = n*2D) against the per-block path (LTX_TEXT_BATCH=0) on the config-A path at LTX-2B widths
+    (3 blocks, B = 8, shared prompt): the LoRA products are the same kernels on the same operands,
+    so to_k / to_v adapter grads of the LAST block (whose dK/dV do not depend on the encoder
+    gradient) agree to rounding; every other output within bf16 noise of each other."""
+    from ltx_amd import transformer3d as T
+    cfg = dict(T.OURS_TRANSFORMER_CONFIG, num_layers=3)
+    params = O.make_params(cfg, 41, lora_rank=16, requires_grad=False)
+    d = _inputs(8, 7, 16, 16, 256, 16, seed=13)
+    res = {}
+    saved = T._TEXT_BATCH
+    try:
+        for batched in (False, True):
+            T._TEXT_BATCH = batched
+            model = build_model(cfg, params, 16, device=DEV)
+            assert model._text_batchable() == batched
+            loss = _build_step(model, d)
+            res[batched] = (loss, grads_by_canonical(model))
+    finally:
+        T._TEXT_BATCH = saved
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert abs(l0 - l1) <= 1e-4 * abs(l0), (l0, l1)
+    assert set(g0) == set(g1)
+    for name in g0:
+        e = rel(g1[name].float(), g0[name].float())
+        assert e <= 1e-2, f"{name}: batched vs per-block {e:.3e}"

@@ -9,8 +9,8 @@
 //   * the bf16-packed accumulator is directly the B operand of the next product (sum over the
 //     register axis), and the matching A operand comes from a transposed LDS read
 //     (ds_read_b64_tr_b16) of a row-major tile -- no LDS round trip for P or dS.
-// LDS tiles are row-major [rows][HD] bf16 with a 16-B chunk XOR swizzle
-// (chunk ^ ((row >> 1) & (HD/8 - 1))): conflict-free for the 16-B row reads of a 32-row fragment.
+// LDS tiles are row-major [rows][HD] bf16 with a 16-B chunk XOR swizzle (swz below):
+// conflict-free for both the 16-B row reads and the transposed reads of a 32-row fragment.
 //
 // Forward: a workgroup = 4 waves x 32 queries; K/V tiles of 64 keys are register-prefetched
 // (global -> VGPR while the current tile computes) and written to LDS after a barrier.
@@ -33,33 +33,67 @@ namespace ltx {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int ATT_THREADS = 256;
 
+// Chunk swizzle of row `row`. HD = 64 (128-B rows, 8 chunks): x = (row >> 1) & 7 bit-reversed.
+//  * 16-B row reads (ds_read_b128, lane groups of 16 over rows {0-3,12-15,20-27} / {4-11,16-19,
+//    28-31}): the 8 rows of one parity in a group have distinct x, so distinct chunks.
+//  * transposed reads (ds_read_b64_tr_b16, 32-lane halves over rows R..R+3, R = 0 mod 4, one
+//    aligned group of 4 chunks): rows R and R+2 (same bank half) differ in x's bit 0, which the
+//    reversal moves to bit 2, so their chunk groups are disjoint. With the plain (row >> 1) & 7
+//    they coincide: a 2-way conflict on every transposed read (SQ_LDS_BANK_CONFLICT, r02_pmc_sq).
+// HD = 32 (64-B rows): four consecutive rows already cover the 64 banks.
+template <int HD>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (HD == 64) {
+    const int x = (row >> 1) & 7;
+    return ((x & 1) << 2) | (x & 2) | (x >> 2);
+  } else {
+    return (row >> 1) & (HD / 8 - 1);
+  }
+}
+
 template <int HD>
 __device__ __forceinline__ int toff(int row, int chunk) {
-  constexpr int CH = HD / 8;
-  return row * (HD * 2) + ((chunk ^ ((row >> 1) & (CH - 1))) << 4);
+  return row * (HD * 2) + ((chunk ^ swz<HD>(row)) << 4);
 }
+
+// Per-lane LDS byte offsets of the fragment reads, computed once per kernel. Both kinds of
+// read start at a row that is a multiple of 16 (rbase = 32u, + 16s), and swz depends on
+// (row >> 1) mod 8 only, so a read is this lane offset + a wave-uniform constant.
+template <int HD>
+struct LaneOfs {
+  static constexpr int KS = HD / 16, DS = HD / 32;
+  int row[KS];    // 16-B row fragment: row (lane & 31), dims ks*16 + 8*(lane >> 5) .. +7
+  int tr[DS][2];  // transposed fragment: rows 4h + q (+8), columns d*32 + (lane & 31)
+  __device__ __forceinline__ explicit LaneOfs(int lane) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) row[ks] = toff<HD>(lane & 31, ks * 2 + (lane >> 5));
+    const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+    for (int d = 0; d < DS; ++d) {
+      const int col = d * 32 + 16 * g + 4 * p;
+      tr[d][0] = toff<HD>(4 * h + q, col >> 3) + ((col & 7) << 1);
+      tr[d][1] = toff<HD>(4 * h + q + 8, col >> 3) + ((col & 7) << 1);
+    }
+  }
+};
 
 // 16-B row fragment: lane reads row (base + (l&31)), dims ks*16 + 8*(l>>5) .. +7
 template <int HD>
-__device__ __forceinline__ s16x8 row_frag(const char* tile, int base, int ks, int lane) {
-  return *(const s16x8*)(tile + toff<HD>(base + (lane & 31), ks * 2 + (lane >> 5)));
+__device__ __forceinline__ s16x8 row_frag(const char* tile, int base, int ks, const LaneOfs<HD>& lo) {
+  return *(const s16x8*)(tile + base * (HD * 2) + lo.row[ks]);
 }
 
 // Transposed fragment for an A operand that sums over the tile's ROW axis, matching an
 // accumulator-as-B operand (k-step s of a 32-row accumulator tile): element j of lane half h
-// is row 16s + 8(j>>2) + 4h + (j&3) (+ rbase), column c0 + (lane & 31).
+// is row 16s + 8(j>>2) + 4h + (j&3) (+ rbase), column 32d + (lane & 31).
 template <int HD>
-__device__ __forceinline__ s16x8 tr_frag(const char* tile, int rbase, int s, int c0, int lane) {
-  const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane & 15) >> 2, p = lane & 3;
-  const int col = c0 + 16 * g + 4 * p;
-  const int row = rbase + 16 * s + 4 * h + q;
-  const char* a0 = tile + toff<HD>(row, col >> 3) + ((col & 7) << 1);
-  const char* a1 = tile + toff<HD>(row + 8, col >> 3) + ((col & 7) << 1);
-  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
-  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+__device__ __forceinline__ s16x8 tr_frag(const char* tile, int rbase, int s, int d, const LaneOfs<HD>& lo) {
+  const char* t = tile + (rbase + 16 * s) * (HD * 2);
+  const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(t + lo.tr[d][0]));
+  const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(t + lo.tr[d][1]));
   s16x8 r;
-  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
-  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  r[0] = lo4[0]; r[1] = lo4[1]; r[2] = lo4[2]; r[3] = lo4[3];
+  r[4] = hi4[0]; r[5] = hi4[1]; r[6] = hi4[2]; r[7] = hi4[3];
   return r;
 }
 
@@ -179,7 +213,7 @@ __device__ __forceinline__ void xcd_block(int xcd_order, int& bx, int& by, int& 
 }
 
 template <int HD, int MODE, bool BIAS>
-__global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams p) {
+__global__ __launch_bounds__(ATT_THREADS, MODE == 1 ? 3 : 2) void attn_q_kernel(const AttnParams p) {
   constexpr int KT = 64;                 // keys per tile
   constexpr int KS = HD / 16;            // 16-deep k-steps over the head dim
   constexpr int DS = HD / 32;            // 32-wide d subtiles
@@ -190,6 +224,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
   char* vtile = smem + TILE;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const LaneOfs<HD> lofs(lane);
   int bx, hh, b;
   xcd_block(p.xcd_order, bx, hh, b);
   const int q0 = bx * 128 + wave * 32;
@@ -249,7 +284,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) kf[u][ks] = row_frag<HD>(ktile, u * 32, ks, lane);
+        for (int ks = 0; ks < KS; ++ks) kf[u][ks] = row_frag<HD>(ktile, u * 32, ks, lofs);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
 #pragma unroll
@@ -263,7 +298,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(ktile, u * 32, ks, lane), qf[ks], s[u]);
+        for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(ktile, u * 32, ks, lofs), qf[ks], s[u]);
       }
     }
     if constexpr (MODE == 0) {
@@ -317,7 +352,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
         for (int ss = 0; ss < 2; ++ss) {
           const s16x8 pb = acc_frag(s[u], ss);
 #pragma unroll
-          for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vtile, u * 32, ss, d * 32, lane), pb, acc[d]);
+          for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vtile, u * 32, ss, d, lofs), pb, acc[d]);
         }
     } else {
 #pragma unroll
@@ -325,7 +360,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
         f32x16 dp;
         s16x8 vfr[KS];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) vfr[ks] = row_frag<HD>(vtile, u * 32, ks, lane);
+        for (int ks = 0; ks < KS; ++ks) vfr[ks] = row_frag<HD>(vtile, u * 32, ks, lofs);
 #pragma unroll
         for (int r = 0; r < 16; ++r) dp[r] = 0.f;
 #pragma unroll
@@ -352,7 +387,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_q_kernel(const AttnParams
         for (int ss = 0; ss < 2; ++ss) {
           const s16x8 db = acc_frag(s[u], ss);
 #pragma unroll
-          for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(ktile, u * 32, ss, d * 32, lane), db, acc[d]);
+          for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(ktile, u * 32, ss, d, lofs), db, acc[d]);
         }
       }
     }
@@ -423,6 +458,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   char* otile = smem + TILE;  // dO
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const LaneOfs<HD> lofs(lane);
   int bx, hh, b;
   xcd_block(p.xcd_order, bx, hh, b);
   const int key = bx * 128 + wave * 32 + (lane & 31);
@@ -494,8 +530,8 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
       s16x8 qfr[KS], ofr[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        qfr[ks] = row_frag<HD>(qtile, u * 32, ks, lane);
-        ofr[ks] = row_frag<HD>(otile, u * 32, ks, lane);
+        qfr[ks] = row_frag<HD>(qtile, u * 32, ks, lofs);
+        ofr[ks] = row_frag<HD>(otile, u * 32, ks, lofs);
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
@@ -520,8 +556,8 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
         const s16x8 sb = acc_frag(dp, ss);
 #pragma unroll
         for (int d = 0; d < DS; ++d) {
-          dva[d] = mfma32(tr_frag<HD>(otile, u * 32, ss, d * 32, lane), pb, dva[d]);
-          dka[d] = mfma32(tr_frag<HD>(qtile, u * 32, ss, d * 32, lane), sb, dka[d]);
+          dva[d] = mfma32(tr_frag<HD>(otile, u * 32, ss, d, lofs), pb, dva[d]);
+          dka[d] = mfma32(tr_frag<HD>(qtile, u * 32, ss, d, lofs), sb, dka[d]);
         }
       }
     }

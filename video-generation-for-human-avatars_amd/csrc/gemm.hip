@@ -74,7 +74,8 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_nt_kernel(const GemmPara
       for (int i = 0; i < 4; ++i) {
         const int row = (wave * 4 + i) * 8 + lrow;
         const int lchunk = pchunk ^ (row & 7);
-        glds16(p.A2 + (int64_t)min(m0 + row, p.M - 1) * p.lda2 + koff + lchunk * 8, base + (wave * 4 + i) * 1024);
+        glds16(ext_a2(p, n0) + (int64_t)min(m0 + row, p.M - 1) * p.lda2 + koff + lchunk * 8,
+               base + (wave * 4 + i) * 1024);
         glds16(p.W2 + (int64_t)min(n0 + row, p.N - 1) * p.ldw2 + koff + lchunk * 8,
                base + TILE_BYTES + (wave * 4 + i) * 1024);
       }
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
       const int row = min(((wave % DMAW) * PPW + i) * 8 + lrow, BMT - 1);
       xo[i] = (uint32_t)(((int64_t)(min(m0 + row, p.M - 1) - m0) * ld + ((pchunk ^ (row & 7)) * 8)) * 2);
     }
-    xb = (const char*)(ext ? p.A2 : p.A) + (int64_t)m0 * ld * 2;
+    xb = (const char*)(ext ? ext_a2(p, n0) : p.A) + (int64_t)m0 * ld * 2;
   };
   auto set_w = [&](bool ext) {
     const int64_t ld = ext ? p.ldw2 : p.ldw;
@@ -597,6 +598,8 @@ struct GemmPlan {
 };
 
 static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
+  // the grouped K extension exists in the default kernels only (gemm_nt_kernel_t, gemm_nt_kernel)
+  const int g_variant = p.ext_gn > 0 ? 0 : ltx::g_variant;
   if (g_force_small < 0) {
     const char* e = getenv("LTX_GEMM_SMALL");
     g_force_small = (e && e[0] == '1') ? 1 : 0;
@@ -836,6 +839,14 @@ extern "C" int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, i
                                     const void* aux1, int64_t ld1, const void* aux2, int64_t ld2,
                                     float alpha, int64_t rank, int64_t rows_per_batch, void* stream);
 
+extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, int64_t ldw,
+                                     const void* A2, int64_t lda2, const void* W2, int64_t ldw2,
+                                     int64_t K2, int64_t ext_group_cols, int64_t ext_group_stride,
+                                     void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                     int epilogue, const void* bias, const void* aux0, int64_t ld0,
+                                     const void* aux1, int64_t ld1, const void* aux2, int64_t ld2,
+                                     float alpha, int64_t rank, int64_t rows_per_batch, void* stream);
+
 extern "C" int ltx_gemm_bf16_nt(const void* A, int64_t lda, const void* W, int64_t ldw, void* C,
                                 int64_t ldc, int64_t M, int64_t N, int64_t K, int epilogue,
                                 const void* bias, const void* aux0, int64_t ld0, const void* aux1,
@@ -851,6 +862,22 @@ extern "C" int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, i
                                     int epilogue, const void* bias, const void* aux0, int64_t ld0,
                                     const void* aux1, int64_t ld1, const void* aux2, int64_t ld2,
                                     float alpha, int64_t rank, int64_t rows_per_batch, void* stream) {
+  return ltx_gemm_bf16_nt_gext(A, lda, W, ldw, A2, lda2, W2, ldw2, K2, 0, 0, C, ldc, M, N, K, epilogue, bias,
+                               aux0, ld0, aux1, ld1, aux2, ld2, alpha, rank, rows_per_batch, stream);
+}
+
+extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, int64_t ldw,
+                                     const void* A2, int64_t lda2, const void* W2, int64_t ldw2,
+                                     int64_t K2, int64_t ext_group_cols, int64_t ext_group_stride,
+                                     void* C, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                                     int epilogue, const void* bias, const void* aux0, int64_t ld0,
+                                     const void* aux1, int64_t ld1, const void* aux2, int64_t ld2,
+                                     float alpha, int64_t rank, int64_t rows_per_batch, void* stream) {
+  LTX_CHECK_ARG(ext_group_cols == 0 ||
+                    (K2 > 0 && ext_group_cols % 256 == 0 && N % ext_group_cols == 0 && ext_group_stride >= 0 &&
+                     ext_group_stride % 8 == 0 && (N / ext_group_cols - 1) * ext_group_stride + K2 <= lda2),
+                "gemm: grouped K extension needs K2 > 0, groups of 256k columns dividing N, and every group's "
+                "A2 columns inside the A2 row");
   LTX_CHECK_ARG(K2 == 0 || (A2 && W2 && K2 % BK == 0 && lda2 >= K2 && ldw2 >= K2 && lda2 % 8 == 0 &&
                             ldw2 % 8 == 0 && ((uintptr_t)A2 | (uintptr_t)W2) % 16 == 0),
                 "gemm: K extension needs 16-B aligned A2/W2 with K2 % 64 == 0");
@@ -872,6 +899,7 @@ extern "C" int ltx_gemm_bf16_nt_ext(const void* A, int64_t lda, const void* W, i
   p.aux0 = aux0; p.ld0 = ld0; p.aux1 = aux1; p.ld1 = ld1; p.aux2 = aux2; p.ld2 = ld2;
   p.alpha = alpha; p.rank = (int)rank; p.rows_per_batch = (int)(rows_per_batch > 0 ? rows_per_batch : M);
   p.A2 = (const bf16_t*)A2; p.W2 = (const bf16_t*)W2; p.lda2 = lda2; p.ldw2 = ldw2; p.K2 = (int)K2;
+  p.ext_gn = (int)ext_group_cols; p.ext_gs = ext_group_stride;
   p.ws = nullptr; p.splitk = 1;
   hipStream_t s = (hipStream_t)stream;
   switch (epilogue) {

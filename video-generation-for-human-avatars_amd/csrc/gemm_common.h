@@ -35,11 +35,22 @@ struct GemmParams {
   const bf16_t* W2;
   int64_t lda2, ldw2;
   int K2;
+  // grouped K extension (ext_gn > 0): output columns [g*ext_gn, (g+1)*ext_gn) read their A2 rows
+  // at column offset g*ext_gs -- one launch for many projections that share A but each carry
+  // their own LoRA operand (the text K/V projections of all blocks). ext_gn % 256 == 0, so a
+  // tile never straddles two groups.
+  int ext_gn;
+  int64_t ext_gs;
   // split-K (small grids): S partial f32 tiles [S][M][N] in a caller-provided workspace, summed by
   // splitk_epilogue_kernel which then applies bias + the epilogue
   float* ws;
   int splitk;
 };
+
+// A2 of the output tile starting at column n0 (grouped K extension, see GemmParams)
+__device__ __forceinline__ const bf16_t* ext_a2(const GemmParams& p, int n0) {
+  return p.ext_gn > 0 ? p.A2 + (int64_t)(n0 / p.ext_gn) * p.ext_gs : p.A2;
+}
 
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(gsrc, LDS_PTR(lds_wave_base), 16, 0, 0);

@@ -31,7 +31,12 @@ __global__ __launch_bounds__(64 * KW) void lora_down_kernel(const bf16_t* __rest
                                                         const float* __restrict__ Wr, int64_t wj, int64_t wk,
                                                         float* __restrict__ out, int64_t ldo, int M, int K,
                                                         float alpha, bf16_t* __restrict__ split, int64_t lds,
-                                                        int K2) {
+                                                        int K2, int64_t gx, int64_t gw, int64_t go, int64_t gs) {
+  // group blockIdx.y: one launch for several adapters (element strides; 0 = shared operand)
+  x += blockIdx.y * gx;
+  Wr += blockIdx.y * gw;
+  out += blockIdx.y * go;
+  if (split) split += blockIdx.y * gs;
   constexpr int RP = R >= 16 ? R : 16;  // R = 8 runs as a padded 16-wide tile
   constexpr int JT = RP / 16;
   // RG = 16-row groups per block: 2 (one weight fetch serves 32 rows) when there are rows enough
@@ -140,7 +145,12 @@ template <int R>
 __global__ __launch_bounds__(512) void lora_wgrad_kernel(const bf16_t* __restrict__ y, int64_t ldy,
                                                          const float* __restrict__ u, int64_t ldu,
                                                          float* __restrict__ dw, int64_t on, int64_t oj, int M,
-                                                         int N, int rows_per_split, float alpha) {
+                                                         int N, int rows_per_split, float alpha, int64_t gy,
+                                                         int64_t gu, int64_t gd) {
+  // group blockIdx.z: one launch for several adapters (element strides; 0 = shared operand)
+  y += blockIdx.z * gy;
+  u += blockIdx.z * gu;
+  dw += blockIdx.z * gd;
   constexpr int RP = R >= 16 ? R : 16;
   constexpr int JT = RP / 16;
   constexpr int NW = 8;  // waves per block, interleaved over row quads
@@ -246,32 +256,35 @@ extern "C" int ltx_lora_split_bf16(const float* src, int64_t rs, int64_t cs, flo
   return LTX_OK;
 }
 
-extern "C" int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk, float* out,
-                             int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha, void* split,
-                             int64_t ld_split, int64_t K2, void* stream) {
+extern "C" int ltx_lora_down_grouped(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk,
+                                     float* out, int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha,
+                                     void* split, int64_t ld_split, int64_t K2, int64_t groups, int64_t gx,
+                                     int64_t gw, int64_t go, int64_t gs, void* stream) {
   LTX_CHECK_ARG(x && Wr && out && M > 0 && K > 0, "lora_down: bad args");
+  LTX_CHECK_ARG(groups >= 1 && groups <= 65535 && gx % 8 == 0 && (wk != 1 || gw % 4 == 0),
+                "lora_down: groups in [1, 65535], x / W group strides keep 16-B alignment");
   LTX_CHECK_ARG(!split || (K2 >= 3 * r && K2 % 64 == 0 && ld_split >= K2), "lora_down: split needs K2 >= 3r, %64");
   LTX_CHECK_ARG(K % 128 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0, "lora_down: K %128, 16-B rows");
   LTX_CHECK_ARG(wk != 1 || (wj % 4 == 0 && ((uintptr_t)Wr % 16) == 0), "lora_down: W rows must be 16-B aligned");
   // 32-row blocks for token-sized M (16-row blocks measured 26 vs 21 us at M = 14336); K split 8
   // ways (512 threads) there: 19.7 vs 20.7 us (forward A), 18.6 vs 19.6 us (split B^T dgrad)
   const bool big = M >= 8192;
-  const dim3 grid((unsigned)(big ? (M + 31) / 32 : (M + 15) / 16));
+  const dim3 grid((unsigned)(big ? (M + 31) / 32 : (M + 15) / 16), (unsigned)groups);
   hipStream_t s = (hipStream_t)stream;
   bf16_t* sp = (bf16_t*)split;
 #define LTX_LORA_DOWN(RR)                                                                                      \
   if (big && K % 256 == 0)                                                                                     \
     hipLaunchKernelGGL((lora_down_kernel<RR, 2, 8>), grid, dim3(512), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk,  \
-                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);                                \
+                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2, gx, gw, go, gs);                \
   else if (big)                                                                                                \
     hipLaunchKernelGGL((lora_down_kernel<RR, 2, 4>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk,  \
-                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);                                \
+                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2, gx, gw, go, gs);                \
   else if (K % 256 == 0)                                                                                       \
     hipLaunchKernelGGL((lora_down_kernel<RR, 1, 8>), grid, dim3(512), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk,  \
-                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);                                \
+                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2, gx, gw, go, gs);                \
   else                                                                                                         \
     hipLaunchKernelGGL((lora_down_kernel<RR, 1, 4>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx, Wr, wj, wk,  \
-                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);
+                       out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2, gx, gw, go, gs);
   switch (r) {
     case 8: LTX_LORA_DOWN(8) break;
     case 16: LTX_LORA_DOWN(16) break;
@@ -283,36 +296,55 @@ extern "C" int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_
   return LTX_OK;
 }
 
-extern "C" int ltx_lora_wgrad(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw, int64_t on,
-                              int64_t oj, int64_t M, int64_t N, int64_t r, float alpha, int accumulate,
-                              void* stream) {
+extern "C" int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_t wj, int64_t wk, float* out,
+                             int64_t ldo, int64_t M, int64_t K, int64_t r, float alpha, void* split,
+                             int64_t ld_split, int64_t K2, void* stream) {
+  return ltx_lora_down_grouped(x, ldx, Wr, wj, wk, out, ldo, M, K, r, alpha, split, ld_split, K2, 1, 0, 0, 0, 0,
+                               stream);
+}
+
+extern "C" int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw,
+                                      int64_t on, int64_t oj, int64_t M, int64_t N, int64_t r, float alpha,
+                                      int accumulate, int64_t groups, int64_t gy, int64_t gu, int64_t gd,
+                                      void* stream) {
   LTX_CHECK_ARG(y && u && dw && M > 0 && N > 0, "lora_wgrad: bad args");
   LTX_CHECK_ARG((on == r && oj == 1) || (on == 1 && oj == N), "lora_wgrad: output must be a dense [N,r] or [r,N]");
   LTX_CHECK_ARG(N % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)y % 16) == 0, "lora_wgrad: y rows must be 16-B aligned");
+  LTX_CHECK_ARG(groups >= 1 && groups <= 65535 && gy % 8 == 0 && (groups == 1 || gd >= N * r),
+                "lora_wgrad: groups in [1, 65535], 16-B aligned y groups, disjoint outputs");
   hipStream_t s = (hipStream_t)stream;
   if (!accumulate) {
-    hipError_t e = hipMemsetAsync(dw, 0, (size_t)N * r * sizeof(float), s);
-    if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+    const bool dense = groups == 1 || gd == N * r;  // one memset covers a dense stack
+    for (int64_t g = 0; g < (dense ? 1 : groups); ++g) {
+      hipError_t e = hipMemsetAsync(dw + g * gd, 0, (size_t)N * r * (dense ? groups : 1) * sizeof(float), s);
+      if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
+    }
   }
   // ~512 blocks of 128 columns x >= 512 rows (8 waves x 4-quad steps): enough waves to stream
   // y while keeping the f32 atomics (128 * r per block) small
   const int nb = (int)((N + 127) / 128);
   // ~512 blocks (two per CU): 17.9 us vs 20.0 us with 256 at M = 14336, N = 2048, r = 16
   const int target = 512;
-  int splits = (int)((target + nb - 1) / nb);
+  int splits = (int)((target + nb * groups - 1) / (nb * groups));
   const int max_splits = (int)((M + 511) / 512);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int rps = (int)((M + splits - 1) / splits);
   rps = (rps + 127) / 128 * 128;
   splits = (int)((M + rps - 1) / rps);
-  const dim3 grid((unsigned)nb, (unsigned)splits);
+  const dim3 grid((unsigned)nb, (unsigned)splits, (unsigned)groups);
   switch (r) {
-    case 8: hipLaunchKernelGGL(lora_wgrad_kernel<8>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
-    case 16: hipLaunchKernelGGL(lora_wgrad_kernel<16>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
-    case 32: hipLaunchKernelGGL(lora_wgrad_kernel<32>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha); break;
+    case 8: hipLaunchKernelGGL(lora_wgrad_kernel<8>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd); break;
+    case 16: hipLaunchKernelGGL(lora_wgrad_kernel<16>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd); break;
+    case 32: hipLaunchKernelGGL(lora_wgrad_kernel<32>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd); break;
     default: return fail(LTX_ERR_BAD_ARG, "lora_wgrad: rank must be 8, 16 or 32");
   }
   LTX_LAUNCH_CHECK();
   return LTX_OK;
+}
+
+extern "C" int ltx_lora_wgrad(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw, int64_t on,
+                              int64_t oj, int64_t M, int64_t N, int64_t r, float alpha, int accumulate,
+                              void* stream) {
+  return ltx_lora_wgrad_grouped(y, ldy, u, ldu, dw, on, oj, M, N, r, alpha, accumulate, 1, 0, 0, 0, stream);
 }

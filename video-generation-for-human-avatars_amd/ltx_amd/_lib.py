@@ -55,6 +55,13 @@ _SIGNATURES = {
     "ltx_gemm_set_stream_workspace": [_p, _p, _i64],
     "ltx_gemm_bf16_nt_ext": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64,
                              _i64, _i32, _p, _p, _i64, _p, _i64, _p, _i64, _f32, _i64, _i64, _p],
+    "ltx_gemm_bf16_nt_gext": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _p, _i64,
+                              _i64, _i64, _i64, _i32, _p, _p, _i64, _p, _i64, _p, _i64, _f32, _i64,
+                              _i64, _p],
+    "ltx_lora_down_grouped": [_p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _f32, _p, _i64,
+                              _i64, _i64, _i64, _i64, _i64, _i64, _p],
+    "ltx_lora_wgrad_grouped": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f32, _i32,
+                               _i64, _i64, _i64, _i64, _p],
     "ltx_lora_split_bf16": [_p, _i64, _i64, _f32, _i64, _i64, _i32, _p, _i64, _i64, _p],
     "ltx_lora_down": [_p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _f32, _p, _i64, _i64,
                       _p],

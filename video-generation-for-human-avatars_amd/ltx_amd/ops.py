@@ -429,9 +429,11 @@ def _gemm_workspace(device):
 
 
 def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2=None,
-         alpha=1.0, rank=0, rows_per_batch=0, ext=None):
+         alpha=1.0, rank=0, rows_per_batch=0, ext=None, ext_group=None):
     """out[M,N] = epilogue(a[M,K] . w[N,K]^T (+ bias) [+ a2 . w2^T]); see LTX_EPI_* in ltx_hip.h.
-    ext = (a2 [M,K2], w2 [N,K2]) appends K-extension tiles (the fused LoRA branch)."""
+    ext = (a2 [M,K2], w2 [N,K2]) appends K-extension tiles (the fused LoRA branch).
+    ext_group = (G, stride): output columns [g*G, (g+1)*G) read a2 from column g*stride on
+    (ltx_gemm_bf16_nt_gext: one launch for many LoRA-carrying projections of one input)."""
     _need(a, BF16, "gemm a")
     _need(w, BF16, "gemm w")
     _gemm_workspace(a.device)
@@ -444,26 +446,30 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
     ld1 = _rows(aux1, "aux1") if aux1 is not None else 0
     ld2 = _rows(aux2, "aux2") if aux2 is not None else 0
     a2, w2 = ext if ext is not None else (None, None)
-    K2 = a2.shape[1] if a2 is not None else 0
+    K2 = w2.shape[1] if w2 is not None else 0
+    gcols, gstride = ext_group if ext_group is not None else (0, 0)
     timer = _timer
     if timer is not None:
         label = gemm_kernel_name(M, N, K, K2, epilogue, rank)
         timer = timer if timer.wants(label) else None
     ev0 = timer.start() if timer is not None else None
-    call("ltx_gemm_bf16_nt_ext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
+    call("ltx_gemm_bf16_nt_gext", _p(a), _rows(a, "a"), _p(w), _rows(w, "w"), _p(a2),
          _rows(a2, "a2") if a2 is not None else 0, _p(w2), _rows(w2, "w2") if w2 is not None else 0,
-         K2, _p(out), _rows(out, "out"), M, N, K, EPI[epilogue], _p(bias), _p(aux0), ld0, _p(aux1),
-         ld1, _p(aux2), ld2, float(alpha), rank, rows_per_batch, _s())
+         K2, gcols, gstride, _p(out), _rows(out, "out"), M, N, K, EPI[epilogue], _p(bias),
+         _p(aux0), ld0, _p(aux1), ld1, _p(aux2), ld2, float(alpha), rank, rows_per_batch, _s())
     if timer is not None:
         timer.stop(label, 2.0 * M * N * K, ev0)
     return out
 
 
-def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_out=None):
+def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_out=None,
+              groups=1, group_strides=(0, 0, 0, 0)):
     """out[m,j] = alpha * x[m,:] . Wr[j,:]; Wr = lora_A [r,K]; transposed=True takes lora_B [K,r]
     (i.e. uses B^T) for the dgrad w = s * dY . B. split=True also returns the activation
     K-extension operand of the rows (what lora_split(out, "act") makes), written by the same
-    kernel."""
+    kernel. groups > 1 runs `groups` adapters in one launch (ltx_lora_down_grouped): wr is the
+    first adapter, group_strides = element offsets per group of (x, wr, out, split); the caller
+    passes out (and split_out) covering every group."""
     M, K = x.shape
     if transposed:
         r = wr.shape[1]
@@ -471,14 +477,17 @@ def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_o
     else:
         r = wr.shape[0]
         wj, wk = wr.stride(0), 1
+    if groups > 1 and (out is None or (split and split_out is None)):
+        raise ValueError("lora_down: grouped calls write into caller-provided out / split_out")
     out = torch.empty(M, r, dtype=F32, device=x.device) if out is None else out
     sp, K2, lds = None, 0, 0
     if split:  # split_out: a [M, K2] column block of a wider operand (the merged text K/V GEMMs)
         K2 = lora_k2(r)
         sp = torch.empty(M, K2, dtype=BF16, device=x.device) if split_out is None else split_out
         lds = _rows(sp, "split_out")
-    call("ltx_lora_down", _p(x), _rows(x, "x"), _p(wr), wj, wk, _p(out), _rows(out, "out"), M, K, r,
-         float(alpha), _p(sp), lds, K2, _s())
+    gx, gw, go, gs = group_strides
+    call("ltx_lora_down_grouped", _p(x), _rows(x, "x"), _p(wr), wj, wk, _p(out), _rows(out, "out"),
+         M, K, r, float(alpha), _p(sp), lds, K2, groups, gx, gw, go, gs, _s())
     return (out, sp) if split else out
 
 
@@ -516,19 +525,25 @@ def lora_split(src, role, scale=1.0, transposed=False, out=None):
     return out
 
 
-def lora_wgrad(y, u, alpha=1.0, transpose_out=False, out=None, accumulate=False):
+def lora_wgrad(y, u, alpha=1.0, transpose_out=False, out=None, accumulate=False, groups=1,
+               group_strides=(0, 0)):
     """dW[n,j] = alpha * sum_m y[m,n] u[m,j] -> [N,r] (or [r,N] when transpose_out). With
-    out/accumulate the product is added into an existing dense f32 buffer (e.g. p.grad)."""
+    out/accumulate the product is added into an existing dense f32 buffer (e.g. p.grad).
+    groups > 1 (ltx_lora_wgrad_grouped): out is a dense [groups, N, r] (or [groups, r, N]) stack,
+    y / u are the first group's operands, group_strides = element offsets per group of (y, u)."""
     M, N = y.shape
     r = u.shape[1]
     shape = (r, N) if transpose_out else (N, r)
+    if groups > 1:
+        shape = (groups,) + shape
     if out is None:
         out = torch.empty(shape, dtype=F32, device=y.device)
         accumulate = False
     assert tuple(out.shape) == shape and out.dtype == F32 and out.is_contiguous()
     on, oj = (1, N) if transpose_out else (r, 1)
-    call("ltx_lora_wgrad", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(out), on, oj, M, N, r,
-         float(alpha), 1 if accumulate else 0, _s())
+    gy, gu = group_strides
+    call("ltx_lora_wgrad_grouped", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(out), on, oj, M,
+         N, r, float(alpha), 1 if accumulate else 0, groups, gy, gu, N * r, _s())
     return out
 
 

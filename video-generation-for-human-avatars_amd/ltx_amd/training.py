@@ -90,7 +90,8 @@ class FusedAdamW(torch.optim.Optimizer):
                  multi_tensor=True):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.multi_tensor = multi_tensor
-        self._tables = []  # pinned host tables of the last steps (alive until their H2D lands)
+        self._tables = []  # pinned host tables of the last builds (alive until their H2D lands)
+        self._table_cache = {}  # dtype -> (buffer pointers, device table, rows)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -121,16 +122,27 @@ class FusedAdamW(torch.optim.Optimizer):
         ops.bump_weight_generation()  # in-place kernel updates: invalidate weight-derived caches
 
     def _multi(self, items, dtype, group, b1, b2, step):
-        """One ltx_adamw_multi launch for all tensors of a dtype (bitwise the per-tensor math)."""
-        rows = []
-        for p, g, st in items:
-            ptrs = (p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr())
-            n = p.numel()
-            for start in range(0, n, self.CHUNK):
-                rows.append(ptrs + (start, min(self.CHUNK, n - start)))
-        host = torch.tensor(rows, dtype=torch.int64).pin_memory()
-        dev = host.to(items[0][0].device, non_blocking=True)
-        self._tables = (self._tables + [(host, dev, [g for _, g, _ in items])])[-2:]
+        """One ltx_adamw_multi launch for all tensors of a dtype (bitwise the per-tensor math).
+        The chunk table (~10^4 rows at LTX-2B: milliseconds of host time) is built once per set
+        of buffers and reused while the parameter / grad / state storages stay the same."""
+        ptrs = [(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                 p.numel()) for p, g, st in items]
+        key = (dtype, tuple(ptrs))
+        hit = self._table_cache.get(dtype)
+        if hit is not None and hit[0] == key:
+            dev, nrows = hit[1], hit[2]
+        else:
+            rows = []
+            for pp, gp, ap, sp, n in ptrs:
+                for start in range(0, n, self.CHUNK):
+                    rows.append((pp, gp, ap, sp, start, min(self.CHUNK, n - start)))
+            host = torch.tensor(rows, dtype=torch.int64).pin_memory()
+            dev = host.to(items[0][0].device, non_blocking=True)
+            nrows = len(rows)
+            # the pinned host copy stays alive until its H2D has landed (two steps later)
+            self._tables = (self._tables + [(host, dev)])[-2:]
+            self._table_cache[dtype] = (key, dev, nrows)
+        rows = range(nrows)
         ops.call("ltx_adamw_multi", ops._p(dev), len(rows), 1 if dtype == torch.bfloat16 else 0,
                  float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                  float(group["weight_decay"]), int(step), ops._s())
@@ -243,7 +255,9 @@ class GradAllReduce:
             if mine:
                 block_params[id(blk)] = mine
                 hooks = blk.__dict__.setdefault("_grad_ready_hooks", [])
-                hooks.append(lambda b, ps=mine: self._ready(ps))
+                # the block reports the params it has finished (None: all of its own)
+                hooks.append(lambda b, done=None, ps=mine: self._ready(
+                    ps if done is None else [p for p in done if id(p) in self._where]))
         in_blocks = {id(p) for ps in block_params.values() for p in ps}
         for p in self.params:
             if id(p) not in in_blocks:

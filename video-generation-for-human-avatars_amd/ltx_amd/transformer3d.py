@@ -117,7 +117,7 @@ class LoraLinear(nn.Module):
         'B' -> s*B for the forward GEMM, 'A' -> A^T for the input-gradient GEMM. Rebuilt when
         the adapter changes: new storage, an in-place torch update (version counter) or a
         FusedAdamW step (ops.weight_generation())."""
-        p = self.lora_B["default"].weight if which == "B" else self.lora_A["default"].weight
+        p = _ab(self)[1 if which == "B" else 0]
         key = (p.data_ptr(), p._version, ops.weight_generation())
         hit = self._split_cache.get(which)
         if hit is None or hit[0] != key:
@@ -256,18 +256,24 @@ class BasicTransformerBlock(nn.Module):
 
     # ---- frozen-weight packing (fused QKV + W^T copies for the dgrad GEMMs) ----
     def _frozen(self):
-        a1, a2, ff = self.attn1, self.attn2, self.ff
-        return [a1.to_q.weight, a1.to_q.bias, a1.to_k.weight, a1.to_k.bias, a1.to_v.weight,
-                a1.to_v.bias, a1.to_out[0].weight, _lin(a2.to_q)[0], _lin(a2.to_k)[0],
-                _lin(a2.to_v)[0], _lin(a2.to_out[0])[0], ff.net[0].proj.weight, ff.net[2].weight]
+        # direct _modules / _parameters lookups: nn.Module.__getattr__ is ~60 us per block here,
+        # paid twice per step per block on the host critical path
+        a1, a2 = self._modules["attn1"]._modules, self._modules["attn2"]._modules
+        net = self._modules["ff"]._modules["net"]._modules
+        pw = lambda m, n="weight": _base(m)._parameters[n]
+        return [pw(a1["to_q"]), pw(a1["to_q"], "bias"), pw(a1["to_k"]), pw(a1["to_k"], "bias"),
+                pw(a1["to_v"]), pw(a1["to_v"], "bias"), pw(a1["to_out"]._modules["0"]),
+                pw(a2["to_q"]), pw(a2["to_k"]), pw(a2["to_v"]), pw(a2["to_out"]._modules["0"]),
+                pw(net["0"]._modules["proj"]), pw(net["2"])]
 
     @torch.no_grad()
     def packed(self):
         """Fused QKV weight/bias and W^T copies for the dgrad GEMMs, rebuilt whenever a weight
         changes (new storage, an in-place torch update, or a FusedAdamW step in
         train_mode='full' -- ops.weight_generation())."""
-        key = (tuple((t.data_ptr(), t._version) for t in self._frozen()), ops.weight_generation()
-               if any(t.requires_grad for t in self._frozen()) else 0)
+        fz = self._frozen()
+        key = (tuple((t.data_ptr(), t._version) for t in fz), ops.weight_generation()
+               if any(t.requires_grad for t in fz) else 0)
         if self._pack is not None and self._pack_key == key:
             return self._pack
         a1, a2, ff = self.attn1, self.attn2, self.ff
@@ -359,6 +365,8 @@ class _Shared:
         self.enc_bias = enc_bias
         # text K/V per block prefetched on the side stream (inference, _forward_tokens)
         self.text_pre = None
+        # all blocks' text K/V computed in one launch each way (LoRA training, _TextStack)
+        self.text_stack = None
         self.eps = eps
         self.full = False  # train_mode='full': attention / AdaLN weights take gradients
 
@@ -374,21 +382,33 @@ def _pgrad(p):
     return p.grad
 
 
+def _base(m):
+    """The nn.Linear under a LoraLinear (or the module itself)."""
+    return m._modules["base_layer"] if type(m) is LoraLinear else m
+
+
 def _lora_params(blk):
     """attn2 LoRA (A, B) per target in _LORA_KEYS order, or None (no adapters)."""
-    a2 = blk.attn2
-    lins = (a2.to_q, a2.to_k, a2.to_v, a2.to_out[0])
-    if not all(isinstance(m, LoraLinear) for m in lins):
-        if any(isinstance(m, LoraLinear) for m in lins):
+    a2 = blk._modules["attn2"]._modules
+    lins = (a2["to_q"], a2["to_k"], a2["to_v"], a2["to_out"]._modules["0"])
+    kinds = [type(m) is LoraLinear for m in lins]
+    if not all(kinds):
+        if any(kinds):
             raise NotImplementedError("LoRA must wrap all four attn2 projections (training.py:52-60)")
         return None
     return lins
 
 
+def _ab(m):
+    """(lora_A weight, lora_B weight) of a LoraLinear, by direct lookup."""
+    return (m._modules["lora_A"]._modules["default"]._parameters["weight"],
+            m._modules["lora_B"]._modules["default"]._parameters["weight"])
+
+
 def _grad_buf(lin, which):
     """The .grad of a LoraLinear adapter weight ('A' or 'B'), created zeroed on first use: the
     LoRA wgrad kernels add into it directly (no per-micro-step buffer, memset or add)."""
-    p = lin.lora_A["default"].weight if which == "A" else lin.lora_B["default"].weight
+    p = _ab(lin)[0 if which == "A" else 1]
     if p.grad is None:
         p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
     return p.grad
@@ -450,7 +470,9 @@ class _BlockFn(torch.autograd.Function):
             u_q = None
             q2raw = ops.gemm(h1, wq, bias=bq)
         q2, _, rq2, _ = ops.qk_norm_rope_fwd(q2raw, None, a2.q_norm.weight, None, None, B=B, N=N)
-        if pre is None:
+        if sh.text_stack is not None:  # computed for every block at once (_TextStack.forward)
+            k2raw, k2, rk2, v2, u_k, u_v = sh.text_stack.block_kv(blk, sh)
+        elif pre is None:
             k2raw, k2, rk2, v2, u_k, u_v = _text_kv(blk, sh, enc2, lora_ab)
         else:  # computed on the text side stream one block ahead (_forward_tokens)
             (k2raw, k2, rk2, v2, u_k, u_v), ev = pre
@@ -538,7 +560,12 @@ class _BlockFn(torch.autograd.Function):
             ops.wgrad_into(_pgrad(lin.weight), dh2, o2)
             ops.colsum_into(_pgrad(lin.bias), dh2)
         # [dK_raw | dV] of the text rows side by side: the merged encoder-gradient GEMM's operand
-        dkv = torch.empty(k2raw.shape[0], 2 * D, dtype=torch.bfloat16, device=h.device)
+        # (with the text stack: this block's slice of the all-blocks operand, reduced at the end)
+        tx = sh.text_stack
+        if tx is not None:
+            dkv = tx.block_dkv(blk)
+        else:
+            dkv = torch.empty(k2raw.shape[0], 2 * D, dtype=torch.bfloat16, device=h.device)
         if sh.text_shared:  # gradient of the shared text rows = sum over the query batches
             dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
                                          key_bias=sh.enc_bias, kv_shared=True)
@@ -561,31 +588,36 @@ class _BlockFn(torch.autograd.Function):
             ops.wgrad_into(_pgrad(a2.to_v.weight), dv2, enc2)
             ops.colsum_into(_pgrad(a2.to_v.bias), dv2)
         del dq2, dk2
+        denc = None
         if has_lora:
             ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
             w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True)
             ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
                            ext=(sw, lq.weight_split("A")))
-            K2 = ops.lora_k2(r)
-            swkv = torch.empty(dkv.shape[0], 2 * K2, dtype=torch.bfloat16, device=h.device)
-            ops.lora_wgrad(dk2raw, u_k, alpha=s, out=_grad_buf(lk, "B"), accumulate=True)
-            w_k, _ = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True, split=True,
-                                   split_out=swkv[:, :K2])
-            ops.lora_wgrad(enc2, w_k, transpose_out=True, out=_grad_buf(lk, "A"), accumulate=True)
-            ops.lora_wgrad(dv2, u_v, alpha=s, out=_grad_buf(lv, "B"), accumulate=True)
-            w_v, _ = ops.lora_down(dv2, Bv, alpha=s, transposed=True, split=True,
-                                   split_out=swkv[:, K2:])
-            ops.lora_wgrad(enc2, w_v, transpose_out=True, out=_grad_buf(lv, "A"), accumulate=True)
-            # denc = dK_raw.W_k + dV.W_v + both adapters' input-gradient terms, one GEMM
-            denc = ops.gemm(dkv, W["kv2_wT"], ext=(swkv, _kv_ext(blk, lk, lv)[1]))
-            del swkv
+            if tx is None:
+                K2 = ops.lora_k2(r)
+                swkv = torch.empty(dkv.shape[0], 2 * K2, dtype=torch.bfloat16, device=h.device)
+                ops.lora_wgrad(dk2raw, u_k, alpha=s, out=_grad_buf(lk, "B"), accumulate=True)
+                w_k, _ = ops.lora_down(dk2raw, Bk, alpha=s, transposed=True, split=True,
+                                       split_out=swkv[:, :K2])
+                ops.lora_wgrad(enc2, w_k, transpose_out=True, out=_grad_buf(lk, "A"),
+                               accumulate=True)
+                ops.lora_wgrad(dv2, u_v, alpha=s, out=_grad_buf(lv, "B"), accumulate=True)
+                w_v, _ = ops.lora_down(dv2, Bv, alpha=s, transposed=True, split=True,
+                                       split_out=swkv[:, K2:])
+                ops.lora_wgrad(enc2, w_v, transpose_out=True, out=_grad_buf(lv, "A"),
+                               accumulate=True)
+                # denc = dK_raw.W_k + dV.W_v + both adapters' input-gradient terms, one GEMM
+                denc = ops.gemm(dkv, W["kv2_wT"], ext=(swkv, _kv_ext(blk, lk, lv)[1]))
+                del swkv
             # the adapter gradients went straight into .grad (accumulated across micro-steps by
             # the kernels' atomics); autograd gets None for them
             grads_lora = [None] * 8
         else:
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2)
-            denc = ops.gemm(dkv, W["kv2_wT"])
+            if tx is None:
+                denc = ops.gemm(dkv, W["kv2_wT"])
         del dq2raw, dk2raw, dv2, dh2, dkv
         # ---- attn1: h1 = h + g_msa * to_out(sdpa(rope(qn(q)), rope(kn(k)), v))
         d_y1 = ops.gate_mul(dh1, mods[:, 2], rpm)
@@ -628,9 +660,11 @@ class _BlockFn(torch.autograd.Function):
         dm = dmods if full else None
         # every grad this block's backward writes straight into .grad (the LoRA adapters) is
         # enqueued now: tell the DP reducer (training.GradAllReduce), which can start their
-        # bucket's all-reduce beside the remaining blocks' backward
+        # bucket's all-reduce beside the remaining blocks' backward. With the text stack the
+        # to_k / to_v adapters are finished later, by _TextStackFn.backward.
+        done = None if tx is None else tx.token_params[tx.index[id(blk)]]
         for cb in getattr(blk, "_grad_ready_hooks", ()):
-            cb(blk)
+            cb(blk, done)
         return (None, None, None, None, dh, denc, dm, None, *grads_lora)
 
 
@@ -664,7 +698,7 @@ def _lora_ab(blk):
     ab = []
     if lora is not None:
         for m in lora:
-            ab += [m.lora_A["default"].weight, m.lora_B["default"].weight]
+            ab += _ab(m)
     return ab
 
 
@@ -689,6 +723,120 @@ def _text_kv(blk, sh, enc2, lora_ab):
     k2raw, v2 = kv[:, :D], kv[:, D:]
     k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, a2.k_norm.weight, None, None, B=sh.Bt, N=sh.L)
     return k2raw, k2, rk2, v2, u_k, u_v
+
+
+# training with LoRA: every block's attn2 text K/V (attention.py:1004-1014 + the to_k / to_v
+# adapters, training.py:50-68) depends only on enc2, so all 28 are one launch each way instead of
+# ~10 small M = L launches per block (LTX_TEXT_BATCH=0: per block, as before)
+_TEXT_BATCH = os.environ.get("LTX_TEXT_BATCH", "1") != "0"
+
+
+class _TextStack:
+    """The text side of every block's attn2 in one launch per kernel (LoRA training).
+
+    Forward: the K/V projections of all blocks are ONE GEMM over the blocks' stacked [2D, D]
+    weights, enc2 . [W_k1; W_v1; ...; W_kn; W_vn]^T + b, with each block's LoRA fused as its own
+    K-extension (ltx_gemm_bf16_nt_gext: output columns of block i read the adapter operand
+    columns of block i); the 2n lora_A products u = enc2 . A^T are one grouped lora_down.
+    Backward: the blocks write their [dK_raw | dV] into one [Lt, n*2D] operand; after the last
+    block (_TextStackFn.backward) the 2n lora_B grads, the 2n dgrads w = s*dY.B and the 2n lora_A
+    grads are one grouped launch each, and the encoder gradient of all blocks is one GEMM with
+    K = n*2D (plus every adapter's input-gradient term as K-extension): the f32 sum of the
+    reference's per-block dX terms, rounded once."""
+
+    def __init__(self, model, enc2):
+        # built lazily by the first block_kv call (block 0's attn2): the cache validation and the
+        # three launches then run on the host while block 0's attn1 keeps the device busy
+        self.model, self.enc2 = model, enc2
+        self.kv = None
+
+    def _build(self):
+        c = self.model._text_stack_cache()
+        self.blocks, self.index = c["blocks"], c["index"]
+        self.block_params, self.token_params = c["block_params"], c["token_params"]
+        self.r, self.s, self.D = c["r"], c["s"], c["D"]
+        self.w_all, self.b_all, self.wT_all = c["w"], c["b"], c["wT"]
+        self.ext_f, self.ext_b, self.A_all, self.B_all = c["ext_f"], c["ext_b"], c["A"], c["B"]
+        self.adapters = c["adapters"]
+        enc2 = self.enc2
+        n, D, r = len(self.blocks), self.D, self.r
+        K2 = ops.lora_k2(r)
+        self.K2 = K2
+        Lt = enc2.shape[0]
+        dev = enc2.device
+        # u = enc2 . A^T of the 2n adapters (k of block i = adapter 2i, v = 2i+1) + their splits
+        self.u = torch.empty(Lt, 2 * n * r, dtype=torch.float32, device=dev)
+        su = torch.empty(Lt, 2 * n * K2, dtype=torch.bfloat16, device=dev)
+        ops.lora_down(enc2, self.A_all[0], split=True, out=self.u[:, :r], split_out=su[:, :K2],
+                      groups=2 * n, group_strides=(0, r * D, r, K2))
+        self.kv = ops.gemm(enc2, self.w_all, bias=self.b_all, ext=(su, self.ext_f),
+                           ext_group=(2 * D, 2 * K2))
+        del su
+        self.dkv = torch.empty(Lt, 2 * n * D, dtype=torch.bfloat16, device=dev)
+
+    def block_kv(self, blk, sh):
+        """(k2raw, k2, rk2, v2, u_k, u_v) of one block: views of the stacked results + the k
+        RMSNorm (per block: its weight)."""
+        if self.kv is None:
+            self._build()
+        i, D, r = self.index[id(blk)], self.D, self.r
+        k2raw = self.kv[:, 2 * i * D:(2 * i + 1) * D]
+        v2 = self.kv[:, (2 * i + 1) * D:(2 * i + 2) * D]
+        k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, blk.attn2.k_norm.weight, None, None,
+                                             B=sh.Bt, N=sh.L)
+        return (k2raw, k2, rk2, v2, self.u[:, 2 * i * r:(2 * i + 1) * r],
+                self.u[:, (2 * i + 1) * r:(2 * i + 2) * r])
+
+    def block_dkv(self, blk):
+        i, D = self.index[id(blk)], self.D
+        return self.dkv[:, 2 * i * D:2 * (i + 1) * D]
+
+    def backward(self):
+        """Adapter grads of every block's to_k / to_v (into .grad) and the encoder gradient."""
+        n, D, r, K2, s = len(self.blocks), self.D, self.r, self.K2, self.s
+        enc2, dkv = self.enc2, self.dkv
+        Lt = enc2.shape[0]
+        dev = enc2.device
+        # lora_B grads: dB_j = s * dY_j^T . u_j  (dY of adapter j = columns j*D .. of dkv)
+        dB = ops.lora_wgrad(dkv[:, :D], self.u[:, :r], alpha=s, groups=2 * n,
+                            group_strides=(D, r))
+        # dgrads w_j = s * dY_j . B_j (+ their K-extension split)
+        w = torch.empty(Lt, 2 * n * r, dtype=torch.float32, device=dev)
+        sw = torch.empty(Lt, 2 * n * K2, dtype=torch.bfloat16, device=dev)
+        ops.lora_down(dkv[:, :D], self.B_all[0], alpha=s, transposed=True, split=True,
+                      out=w[:, :r], split_out=sw[:, :K2], groups=2 * n,
+                      group_strides=(D, D * r, r, K2))
+        # lora_A grads: dA_j = w_j^T . enc2
+        dA = ops.lora_wgrad(enc2, w[:, :r], transpose_out=True, groups=2 * n, group_strides=(0, r))
+        # into .grad (one multi-tensor add each; bitwise the per-block kernels' single-split adds)
+        gB, gA = [], []
+        for m in self.adapters:
+            gB.append(_grad_buf(m, "B"))
+            gA.append(_grad_buf(m, "A"))
+        torch._foreach_add_(gB, list(dB.unbind(0)))
+        torch._foreach_add_(gA, list(dA.unbind(0)))
+        # encoder gradient of all blocks: sum_i [dK_raw_i | dV_i] . [W_k_i ; W_v_i] + adapters
+        denc = ops.gemm(dkv, self.wT_all, ext=(sw, self.ext_b))
+        for blk, ps in zip(self.blocks, self.block_params):
+            for cb in getattr(blk, "_grad_ready_hooks", ()):
+                cb(blk, ps)
+        return denc
+
+
+class _TextStackFn(torch.autograd.Function):
+    """enc2 -> enc2 (an alias the blocks consume): autograd runs its backward once every block's
+    backward has written its [dK_raw | dV] slice, and it returns the encoder gradient."""
+
+    @staticmethod
+    def forward(ctx, enc2, tx):
+        ctx.tx = tx
+        return enc2.view_as(enc2)
+
+    @staticmethod
+    def backward(ctx, denc_blocks):
+        denc = ctx.tx.backward()
+        ctx.tx = None
+        return denc, None
 
 
 # inference forwards compute the text K/V one block ahead on a side stream (LTX_TEXT_STREAM=0:
@@ -931,6 +1079,79 @@ class Transformer3DModel(nn.Module):
             model.patchifier = patchifier
         return model
 
+    def _text_structure(self):
+        """Module-structure facts of the batched text side, cached on the identity of every
+        block's attn2 projections and the trainability of the K/V base weights (cheap to check;
+        the per-block lists below cost ~3 ms of host time to rebuild): None when the text side
+        cannot be batched, else the blocks, their (k, v) adapters and parameter lists."""
+        blocks = list(self.transformer_blocks)
+        if not (_TEXT_BATCH and blocks):
+            return None
+        lins = [_lora_params(b) for b in blocks]
+        if any(l is None for l in lins):
+            return None
+        key = tuple((id(l[1]), id(l[2]), _base(l[1])._parameters["weight"].requires_grad,
+                     _base(l[2])._parameters["weight"].requires_grad) for l in lins)
+        c = getattr(self, "_tx_struct", None)
+        if c is not None and c[0] == key:
+            return c[1]
+        r, sc = lins[0][1].r, lins[0][1].scaling
+        # grouped K-extension columns: one block's [k | v] outputs = 2D, a multiple of 256
+        ok = (2 * blocks[0].attn2.inner_dim) % 256 == 0 and all(
+            l[1].r == r and l[2].r == r and l[1].scaling == sc and l[2].scaling == sc
+            and not k[2] and not k[3] for l, k in zip(lins, key))
+        st = None
+        if ok:
+            # per block: the to_k / to_v adapter weights (finished by _TextStack.backward) and
+            # the rest of its trainable parameters (finished by its own backward)
+            block_params = [list(_ab(l[1]) + _ab(l[2])) for l in lins]
+            text_ids = {id(p) for ps in block_params for p in ps}
+            st = {"blocks": blocks, "lins": lins, "adapters": [m for l in lins for m in (l[1], l[2])],
+                  "index": {id(b): i for i, b in enumerate(blocks)}, "block_params": block_params,
+                  "token_params": [[p for p in b.parameters() if id(p) not in text_ids]
+                                   for b in blocks],
+                  "text_ids": text_ids, "r": r, "s": sc, "D": blocks[0].attn2.inner_dim}
+        self._tx_struct = (key, st)
+        return st
+
+    def _text_batchable(self):
+        """The batched text side (_TextStack) applies with LoRA on every block's attn2 and frozen
+        K/V base weights (lora_audio training)."""
+        return self._text_structure() is not None
+
+    @torch.no_grad()
+    def _text_stack_cache(self):
+        """Stacked operands of _TextStack, rebuilt when a block's packed weights or an adapter
+        change: [2nD, D] K/V weights, bias, their [D, 2nD] transpose, the forward K-extension
+        weights [2nD, 2 K2] (each block's block-diagonal split(s B_k) | split(s B_v)), the
+        backward ones [D, 2n K2], and the f32 adapters A [2n, r, D], B [2n, D, r]."""
+        st = self._text_structure()
+        blocks, lins, adapters = st["blocks"], st["lins"], st["adapters"]
+        packs = [b.packed() for b in blocks]
+        exts = [_kv_ext(b, l[1], l[2]) for b, l in zip(blocks, lins)]
+        abs_ = [t for m in adapters for t in _ab(m)]
+        key = (tuple(id(pk) for pk in packs), tuple(id(e[0]) for e in exts),
+               tuple((t.data_ptr(), t._version) for t in abs_), ops.weight_generation())
+        c = getattr(self, "_tx_cache", None)
+        if c is not None and c["key"] == key:
+            return c
+        base_key = tuple(id(pk) for pk in packs)
+        if c is not None and c["base_key"] == base_key:
+            w, b, wT = c["w"], c["b"], c["wT"]
+        else:
+            self._tx_cache = None  # drop the old stacks before building new ones
+            w = torch.cat([pk["kv2_w"] for pk in packs], 0)
+            b = torch.cat([pk["kv2_b"] for pk in packs], 0)
+            wT = torch.cat([pk["kv2_wT"] for pk in packs], 1)
+        c = dict(st)
+        c.update({"key": key, "base_key": base_key, "w": w, "b": b, "wT": wT,
+                  "ext_f": torch.cat([e[0] for e in exts], 0),
+                  "ext_b": torch.cat([e[1] for e in exts], 1),
+                  "A": torch.stack([_ab(m)[0] for m in adapters]),
+                  "B": torch.stack([_ab(m)[1] for m in adapters])})
+        self._tx_cache = c
+        return c
+
     def grad_ready_order(self):
         """The trainable parameters in the order the backward finishes their gradients: the
         blocks' own parameters from the last block to the first (their grads are complete when
@@ -938,6 +1159,14 @@ class Transformer3DModel(nn.Module):
         projection, AdaLN-single, patchify_proj) and the head. training.GradAllReduce buckets in
         this order so the first buckets can be reduced while the backward still runs."""
         seen, order = set(), []
+        # with the batched text side the to_k / to_v adapters finish after the last block
+        st = self._text_structure()
+        late = st["text_ids"] if st is not None else set()
+        for blk in reversed(self.transformer_blocks):
+            for p in blk.parameters():
+                if p.requires_grad and id(p) not in seen and id(p) not in late:
+                    seen.add(id(p))
+                    order.append(p)
         for blk in reversed(self.transformer_blocks):
             for p in blk.parameters():
                 if p.requires_grad and id(p) not in seen:
@@ -1062,6 +1291,10 @@ class Transformer3DModel(nn.Module):
         sh = _Shared(B, N, L, H, self.attention_head_dim, rope, enc_bias, eps, text_shared,
                      per_token)
         sh.full = full
+        ckpt = self.training and self.gradient_checkpointing and keep
+        if keep and not full and self._text_batchable():
+            sh.text_stack = _TextStack(self, enc2)
+            enc2 = _TextStackFn.apply(enc2, sh.text_stack)
         strat = None
         if skip_layer_mask is not None and skip_layer_strategy is not None:
             strat = SkipLayerStrategy[skip_layer_strategy.name] if isinstance(
@@ -1069,7 +1302,6 @@ class Transformer3DModel(nn.Module):
             if strat is SkipLayerStrategy.Residual:  # acts only with residual_connection (False)
                 strat = None
         blocks = list(self.transformer_blocks)
-        ckpt = self.training and self.gradient_checkpointing and keep
         if _TEXT_STREAM and not keep and h.is_cuda and len(blocks) > 1:
             # inference: text K/V of block i+1 on a side stream while block i runs (the small
             # M = L GEMM, LoRA and norm launches fill CUs the main stream leaves idle)
