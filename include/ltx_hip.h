@@ -46,6 +46,11 @@ enum {
   LTX_EPI_ACCUM = 6,            /* C = bf16(R + bf16(acc)); R = aux0 (may alias C) */
   LTX_EPI_LORA_DGRAD_ACCUM = 7, /* C = [R +] bf16(bf16(acc) + bf16(alpha * Wd[m,:].A[:,n]));
                                    Wd = aux1 f32 [M,rank], A = aux2 f32 [rank,N], R = aux0 opt. */
+  LTX_EPI_STORE_ROWDOT = 8,     /* C = y, and the attention backward's delta of the rows:
+                                   aux1 f32 [B, N/hd, rows_per_batch] gets, per hd-column head h
+                                   (hd = rank: 32 or 64), sum_c bf16(y)[m, hd*h+c] * O[m, hd*h+c]
+                                   (O = aux0, ld0): C is dO,
+                                   O the attention output (rowsum(dO*O) of ltx_attn_bwd) */
 };
 
 int ltx_abi_version(void);
@@ -228,6 +233,16 @@ int ltx_gemm_set_workspace(void* ptr, int64_t bytes);
 /* Split-K workspace for GEMMs launched on `stream` (overrides the default one for that stream):
  * GEMMs on concurrent streams each need their own partials buffer. */
 int ltx_gemm_set_stream_workspace(void* stream, void* ptr, int64_t bytes);
+
+/* ltx_attn_bwd with delta_ws already holding delta[b,h,q] = sum_d dO*O (f32 [B,H,Nq]), e.g.
+ * written by the dO-producing GEMM's LTX_EPI_STORE_ROWDOT epilogue: the delta pass is skipped.
+ * delta_ready = 0 is ltx_attn_bwd. */
+int ltx_attn_bwd_ex(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v,
+                    int64_t ldv, const void* o, int64_t ldo, const void* dout, int64_t lddo,
+                    const float* lse, const float* key_bias, float* delta_ws, int delta_ready,
+                    void* dq, int64_t lddq, int dq_is_f32, void* dk, int64_t lddk, void* dv,
+                    int64_t lddv, int64_t B, int64_t H, int64_t Nq, int64_t Nk,
+                    int64_t kv_batch_rows, int64_t d, float scale, void* stream);
 
 /* ---- LoRA skinny contractions in f32 (peft lora_A / lora_B, training.py:50-68) --------------- */
 /* out[m,j] = alpha * sum_k x[m,k] * Wr[j,k], Wr element (j,k) at Wr[j*wj + k*wk]; x bf16 [M,K]

@@ -115,6 +115,29 @@ def test_gemm_epilogues(M, N, K):
     assert rel(out, R.float() + acc + (Wd @ A).to(torch.bfloat16).float()) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K,hd,ext", [(14336, 2048, 2048, 64, False),  # large tile (224 rows)
+                                          (512, 256, 256, 64, False),     # 128x128, one pass
+                                          (256, 2048, 8192, 64, True),    # 128x128, split-K + LoRA ext
+                                          (600, 128, 128, 32, False)])    # head dim 32, ragged M
+def test_gemm_store_rowdot(M, N, K, hd, ext):
+    """LTX_EPI_STORE_ROWDOT: the dO GEMM also writes the attention backward's delta
+    rowsum(dO*O) per head (f32 [B, H, rows]); C is bitwise the plain store."""
+    from ltx_amd import ops
+    B = 2 if M % 2 == 0 else 1
+    a, w = g(M, K, seed=61), g(N, K, seed=62, scale=K ** -0.5)
+    o = g(M, N, seed=63)
+    kw = {}
+    if ext:
+        kw["ext"] = (g(M, 64, seed=64), g(N, 64, seed=65, scale=0.1))
+    ref = ops.gemm(a, w, **kw)
+    delta = torch.full((B, N // hd, M // B), float("nan"), device=DEV)
+    out = ops.gemm(a, w, epilogue="store_rowdot", aux0=o, aux1=delta, rank=hd, rows_per_batch=M // B, **kw)
+    assert torch.equal(out, ref)
+    want = (out.float() * o.float()).view(B, M // B, N // hd, hd).sum(-1).permute(0, 2, 1)
+    assert torch.isfinite(delta).all()
+    assert (delta - want).abs().max().item() <= 1e-4 * want.abs().max().item() + 1e-5
+
+
 # ------------------------------------------------------------------------------------- attention
 def _sdpa_ref(q, k, v, B, H, d, bias=None):
     Nq, Nk = q.shape[0] // B, k.shape[0] // B

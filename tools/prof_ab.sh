@@ -7,9 +7,9 @@ i=0
 for e in "$@"; do
   i=$((i+1))
   env $e timeout -k 10 300 rocprofv3 --kernel-trace --output-format rocpd -d $RAW/t$i -o run -- \
-      python3 $R/bench.py --steps 6 --warmup 2 --no-cpu-baseline > $OUT/bench_$i.jsonl 2> $RAW/t$i.err || exit $?
+      python3 $R/bench.py --steps ${STEPS:-8} --warmup 2 --no-cpu-baseline > $OUT/bench_$i.jsonl 2> $RAW/t$i.err || exit $?
   echo "== $e" > $OUT/summary_$i.txt
-  python3 $R/tools/step_gaps.py $RAW/t$i/run_results.db 800 20 >> $OUT/summary_$i.txt
+  python3 $R/tools/step_gaps.py $RAW/t$i/run_results.db 500 20 ${SKIP_MS:-1200} >> $OUT/summary_$i.txt
   python3 $R/tools/rocpd_summary.py $RAW/t$i/run_results.db 1 70 >> $OUT/summary_$i.txt
   head -30 $OUT/summary_$i.txt
 done

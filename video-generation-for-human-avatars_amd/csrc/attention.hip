@@ -636,10 +636,12 @@ static int launch_fwd(AttnParams p, hipStream_t s) {
 }
 
 template <int HD>
-static int launch_bwd(AttnParams p, float* delta, hipStream_t s) {
-  hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)(((int64_t)p.B * p.Nq + 3) / 4)), dim3(256), 0, s, p,
-                     delta);
-  LTX_LAUNCH_CHECK();
+static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s) {
+  if (!delta_ready) {
+    hipLaunchKernelGGL(attn_delta_kernel<HD>, dim3((unsigned)(((int64_t)p.B * p.Nq + 3) / 4)), dim3(256), 0, s,
+                       p, delta);
+    LTX_LAUNCH_CHECK();
+  }
   p.delta = delta;
   p.xcd_order = xcd_order_flag();
   dim3 gq((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
@@ -686,15 +688,16 @@ extern "C" int ltx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t l
   return d == 64 ? launch_fwd<64>(p, (hipStream_t)stream) : launch_fwd<32>(p, (hipStream_t)stream);
 }
 
-extern "C" int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
-                            const void* o, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
-                            const float* key_bias, float* delta_ws, void* dq, int64_t lddq, int dq_is_f32,
-                            void* dk, int64_t lddk, void* dv, int64_t lddv, int64_t B, int64_t H, int64_t Nq,
-                            int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale, void* stream) {
+extern "C" int ltx_attn_bwd_ex(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                               const void* o, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
+                               const float* key_bias, float* delta_ws, int delta_ready, void* dq, int64_t lddq,
+                               int dq_is_f32, void* dk, int64_t lddk, void* dv, int64_t lddv, int64_t B, int64_t H,
+                               int64_t Nq, int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale,
+                               void* stream) {
   int rc = check_common(q, ldq, k, ldk, v, ldv, B, H, Nq, Nk, d);
   if (rc) return rc;
   LTX_CHECK_ARG(kv_batch_rows == Nk || kv_batch_rows == 0, "attn_bwd: kv_batch_rows must be Nk or 0 (shared)");
-  LTX_CHECK_ARG(o && dout && lse && delta_ws && dq && dk && dv, "attn_bwd: null operand");
+  LTX_CHECK_ARG(dout && lse && delta_ws && dq && dk && dv && (o || delta_ready), "attn_bwd: null operand");
   LTX_CHECK_ARG((ldo | lddo | lddq | lddk | lddv) % 8 == 0, "attn_bwd: strides must be multiples of 8");
   AttnParams p = {};
   p.q = (const bf16_t*)q; p.ldq = ldq; p.k = (const bf16_t*)k; p.ldk = ldk; p.v = (const bf16_t*)v; p.ldv = ldv;
@@ -703,5 +706,15 @@ extern "C" int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t l
   p.dq = dq; p.lddq = lddq; p.dq_f32 = dq_is_f32;
   p.dk = (bf16_t*)dk; p.lddk = lddk; p.dv = (bf16_t*)dv; p.lddv = lddv;
   p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.kvb = (int)kv_batch_rows; p.scale = scale;
-  return d == 64 ? launch_bwd<64>(p, delta_ws, (hipStream_t)stream) : launch_bwd<32>(p, delta_ws, (hipStream_t)stream);
+  return d == 64 ? launch_bwd<64>(p, delta_ws, delta_ready, (hipStream_t)stream)
+                 : launch_bwd<32>(p, delta_ws, delta_ready, (hipStream_t)stream);
+}
+
+extern "C" int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const void* v, int64_t ldv,
+                            const void* o, int64_t ldo, const void* dout, int64_t lddo, const float* lse,
+                            const float* key_bias, float* delta_ws, void* dq, int64_t lddq, int dq_is_f32,
+                            void* dk, int64_t lddk, void* dv, int64_t lddv, int64_t B, int64_t H, int64_t Nq,
+                            int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale, void* stream) {
+  return ltx_attn_bwd_ex(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, key_bias, delta_ws, 0, dq, lddq, dq_is_f32,
+                         dk, lddk, dv, lddv, B, H, Nq, Nk, kv_batch_rows, d, scale, stream);
 }

@@ -923,6 +923,12 @@ extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, 
     case LTX_EPI_LORA_DGRAD_ACCUM:
       LTX_CHECK_ARG(aux1 && aux2, "gemm lora dgrad: needs Wd (aux1) and A (aux2)");
       return launch_lora<LTX_EPI_LORA_DGRAD_ACCUM>(p, s);
+    case LTX_EPI_STORE_ROWDOT:
+      LTX_CHECK_ARG(aux0 && aux1 && (rank == 32 || rank == 64) && N % rank == 0 && M % p.rows_per_batch == 0,
+                    "gemm store_rowdot: needs O (aux0), delta (aux1), head dim (rank) 32 or 64 dividing N, "
+                    "whole batches");
+      LTX_CHECK_ARG(((uintptr_t)aux1 % 4) == 0, "gemm store_rowdot: delta must be f32-aligned");
+      return launch<LTX_EPI_STORE_ROWDOT>(p, s);
     default:
       return fail(LTX_ERR_BAD_ARG, "gemm: unknown epilogue");
   }

@@ -83,6 +83,25 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
   if constexpr (EPI == LTX_EPI_STORE) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) out8[j] = v[j];
+  } else if constexpr (EPI == LTX_EPI_STORE_ROWDOT) {
+    // every epilogue site hands a row's 8-column chunks to consecutive lanes, so a head of
+    // hd = p.rank (32 / 64) columns is hd/8 lanes aligned at a multiple of hd/8 (N % hd == 0,
+    // checked at launch): reduce there
+    const u32x4 o4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      out8[j] = v[j];
+      s += v[j] * bf2f((bf16_t)(o4[j >> 1] >> ((j & 1) * 16)));
+    }
+    const int hd = p.rank, lanes = hd >> 3;
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (lanes == 8) s += __shfl_xor(s, 4, 64);
+    if (((n0 >> 3) & (lanes - 1)) == 0) {
+      const int rpb = p.rows_per_batch, H = p.N / hd;
+      ((float*)p.aux1)[((int64_t)(m / rpb) * H + n0 / hd) * rpb + m % rpb] = s;
+    }
   } else if constexpr (EPI == LTX_EPI_GELU) {
     // aux0: optional pre-activation store (bf16, ld0) for the backward
     if (p.aux0) {

@@ -45,6 +45,9 @@ _SIGNATURES = {
                      _i64, _f32, _p],
     "ltx_attn_bwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i32,
                      _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _p],
+    "ltx_attn_bwd_ex": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _i32, _p,
+                        _i64, _i32, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32,
+                        _p],
     "ltx_gemm_bf16_nt": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i32, _p, _p, _i64, _p,
                          _i64, _p, _i64, _f32, _i64, _i64, _p],
     "ltx_gemm_set_variant": [_i32],
@@ -91,7 +94,7 @@ _SIGNATURES = {
 }
 
 EPI = {"store": 0, "gelu": 1, "gated_residual": 2, "lora": 3, "lora_residual": 4,
-       "gelu_bwd": 5, "accum": 6, "lora_dgrad_accum": 7}
+       "gelu_bwd": 5, "accum": 6, "lora_dgrad_accum": 7, "store_rowdot": 8}
 
 _lib = None
 _lock = threading.Lock()

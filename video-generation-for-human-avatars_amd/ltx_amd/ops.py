@@ -316,25 +316,31 @@ def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
 
 
 def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, dq=None,
-             dk=None, dv=None, kv_shared=False):
+             dk=None, dv=None, kv_shared=False, delta=None):
     """Gradients (dq [B*Nq], dk/dv [B*Nk] per query batch -- with kv_shared their batch_sum is
-    the gradient of the shared rows)."""
+    the gradient of the shared rows). delta: the f32 [B, H, Nq] rowsum(dO*O), when the GEMM that
+    produced dO already wrote it (gemm epilogue 'store_rowdot'); else the delta pass runs here."""
     Nq = q.shape[0] // B
     Nk = k.shape[0] if kv_shared else k.shape[0] // B
     dev = q.device
     dq = torch.empty(B * Nq, H * d, dtype=F32 if dq_f32 else BF16, device=dev) if dq is None else dq
     dk = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dk is None else dk
     dv = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dv is None else dv
-    delta = torch.empty(B, H, Nq, dtype=F32, device=dev)
+    ready = delta is not None
+    if ready:
+        assert delta.dtype == F32 and delta.is_contiguous() and delta.numel() == B * H * Nq
+    else:
+        delta = torch.empty(B, H, Nq, dtype=F32, device=dev)
     bias = "true" if key_bias is not None else "false"
-    label = (f"attention backward: ltx::attn_delta_kernel<{d}> + ltx::attn_dkdv_kernel<{d}, {bias}> + "
-             f"ltx::attn_q_kernel<{d}, 1, {bias}>")
+    label = ("attention backward: " + ("" if ready else f"ltx::attn_delta_kernel<{d}> + ") +
+             f"ltx::attn_dkdv_kernel<{d}, {bias}> + ltx::attn_q_kernel<{d}, 1, {bias}>")
     timer = _timer if (_timer is not None and _timer.wants(label)) else None
     ev0 = timer.start() if timer is not None else None
-    call("ltx_attn_bwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
-         _rows(o, "o"), _p(do), _rows(do, "do"), _p(lse), _p(key_bias), _p(delta), _p(dq),
-         _rows(dq, "dq"), 1 if dq.dtype == F32 else 0, _p(dk), _rows(dk, "dk"), _p(dv),
-         _rows(dv, "dv"), B, H, Nq, Nk, 0 if kv_shared else Nk, d, scale, _s())
+    call("ltx_attn_bwd_ex", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"),
+         _p(o), _rows(o, "o") if o is not None else 0, _p(do), _rows(do, "do"), _p(lse),
+         _p(key_bias), _p(delta), 1 if ready else 0, _p(dq), _rows(dq, "dq"),
+         1 if dq.dtype == F32 else 0, _p(dk), _rows(dk, "dk"), _p(dv), _rows(dv, "dv"), B, H, Nq,
+         Nk, 0 if kv_shared else Nk, d, scale, _s())
     if timer is not None:
         timer.stop(label, 8.0 * B * H * Nq * Nk * d, ev0)
     return dq, dk, dv
@@ -443,7 +449,13 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
         raise ValueError(f"gemm: K mismatch {K} vs {K2}")
     out = torch.empty(M, N, dtype=BF16, device=a.device) if out is None else out
     ld0 = _rows(aux0, "aux0") if aux0 is not None else 0
-    ld1 = _rows(aux1, "aux1") if aux1 is not None else 0
+    if epilogue == "store_rowdot":  # aux1: the dense f32 [B, N / head_dim, rows_per_batch] delta
+        _need(aux1, F32, "gemm store_rowdot delta")
+        if not aux1.is_contiguous() or aux1.numel() != M * (N // max(rank, 1)):
+            raise ValueError("gemm store_rowdot: delta must be a dense [B, N/head_dim, rows] f32")
+        ld1 = 0
+    else:
+        ld1 = _rows(aux1, "aux1") if aux1 is not None else 0
     ld2 = _rows(aux2, "aux2") if aux2 is not None else 0
     a2, w2 = ext if ext is not None else (None, None)
     K2 = w2.shape[1] if w2 is not None else 0

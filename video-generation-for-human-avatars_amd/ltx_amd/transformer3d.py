@@ -547,14 +547,18 @@ class _BlockFn(torch.autograd.Function):
                             sum_groups=False, accumulate=False)
         del dx2
         # ---- attn2: h2 = h1 + to_out(o2)   (LoRA grads: peft f32 adapters)
+        # dO of the cross-attention + its delta rowsum(dO*O) in the GEMM epilogue
+        delta2 = torch.empty(B, H, N, dtype=torch.float32, device=h.device) if _DELTA_FUSED else None
+        rd = dict(epilogue="store_rowdot", aux0=o2, aux1=delta2, rank=d, rows_per_batch=N) \
+            if _DELTA_FUSED else {}
         if has_lora:
             lq, lk, lv, lo = lora
             ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
             w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True)
             ops.lora_wgrad(o2, w_o, transpose_out=True, out=_grad_buf(lo, "A"), accumulate=True)
-            do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")))
+            do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")), **rd)
         else:
-            do2 = ops.gemm(dh2, W["o2_wT"])
+            do2 = ops.gemm(dh2, W["o2_wT"], **rd)
         if full:  # attn2.to_out.0
             lin = a2.to_out[0]
             ops.wgrad_into(_pgrad(lin.weight), dh2, o2)
@@ -568,12 +572,12 @@ class _BlockFn(torch.autograd.Function):
             dkv = torch.empty(k2raw.shape[0], 2 * D, dtype=torch.bfloat16, device=h.device)
         if sh.text_shared:  # gradient of the shared text rows = sum over the query batches
             dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
-                                         key_bias=sh.enc_bias, kv_shared=True)
+                                         key_bias=sh.enc_bias, kv_shared=True, delta=delta2)
             dk2 = ops.batch_sum(dk2, B)
             dv2 = ops.batch_sum(dv2, B, out=dkv[:, D:])
         else:
             dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
-                                         key_bias=sh.enc_bias, dv=dkv[:, D:])
+                                         key_bias=sh.enc_bias, dv=dkv[:, D:], delta=delta2)
         del do2
         dq2raw, _ = ops.qk_norm_rope_bwd(dq2, q2raw, a2.q_norm.weight, rq2, B=B, N=N)
         dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=sh.Bt, N=L,
@@ -621,7 +625,10 @@ class _BlockFn(torch.autograd.Function):
         del dq2raw, dk2raw, dv2, dh2, dkv
         # ---- attn1: h1 = h + g_msa * to_out(sdpa(rope(qn(q)), rope(kn(k)), v))
         d_y1 = ops.gate_mul(dh1, mods[:, 2], rpm)
-        do1 = ops.gemm(d_y1, W["out1_wT"])
+        delta1 = torch.empty(B, H, N, dtype=torch.float32, device=h.device) if _DELTA_FUSED else None
+        rd = dict(epilogue="store_rowdot", aux0=o1, aux1=delta1, rank=d, rows_per_batch=N) \
+            if _DELTA_FUSED else {}
+        do1 = ops.gemm(d_y1, W["out1_wT"], **rd)
         if full:  # gate_msa, attn1.to_out.0
             ops.colsum_into(dmods[:, 2], dh1, y1, mode=1, rows_per_group=rpm, sum_groups=False,
                             accumulate=False)
@@ -632,7 +639,7 @@ class _BlockFn(torch.autograd.Function):
         M = B * N
         dqkv = torch.empty(M, 3 * D, dtype=torch.bfloat16, device=h.device)
         dq1, dk1, _ = ops.attn_bwd(qk[:, :D], qk[:, D:], qkv[:, 2 * D:], o1, do1, lse1, B, H, d,
-                                   a1.scale, dv=dqkv[:, 2 * D:])
+                                   a1.scale, dv=dqkv[:, 2 * D:], delta=delta1)
         del do1
         ops.qk_norm_rope_bwd(dq1, qkv[:, :D], a1.q_norm.weight, rq1, dk1, qkv[:, D:2 * D],
                              a1.k_norm.weight, rk1, sh.rope, dq_out=dqkv[:, :D],
@@ -729,6 +736,9 @@ def _text_kv(blk, sh, enc2, lora_ab):
 # adapters, training.py:50-68) depends only on enc2, so all 28 are one launch each way instead of
 # ~10 small M = L launches per block (LTX_TEXT_BATCH=0: per block, as before)
 _TEXT_BATCH = os.environ.get("LTX_TEXT_BATCH", "1") != "0"
+# the attention backward's delta = rowsum(dO*O) written by the dO GEMM's epilogue
+# (LTX_EPI_STORE_ROWDOT) instead of a separate pass over dO and O (LTX_DELTA_FUSED=0: separate)
+_DELTA_FUSED = os.environ.get("LTX_DELTA_FUSED", "1") != "0"
 
 
 class _TextStack:
