@@ -358,6 +358,36 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
   };
+  // a wave's whole set of PPW pieces (consecutive 1-KiB LDS slots) in one asm block: M0 saved /
+  // restored once and stepped by s_add instead of two moves per piece (g_dma_batch, A/B switch)
+  auto glds_batch = [&](const uint32_t* vo, const char* sbase, uint32_t lds) {
+    unsigned keep;
+    if constexpr (PPW == 4) {
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %5\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "s"(sbase), "s"(lds)
+          : "memory", "scc");
+    } else {
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %10\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %9\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %9\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %9\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %9\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %5, %9\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %6, %9\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %7, %9\n\t"
+          "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %8, %9\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(vo[0]), "v"(vo[1]), "v"(vo[2]), "v"(vo[3]), "v"(vo[4]), "v"(vo[5]), "v"(vo[6]), "v"(vo[7]),
+            "s"(sbase), "s"(lds)
+          : "memory", "scc");
+    }
+  };
+  const bool dma_batch = p.dma_batch != 0;
   // LDS byte offsets of X / W buffer `buf`
   auto xaddr = [&](int buf) -> int { return XR3 ? buf * XT : buf * ST; };
   auto waddr = [&](int buf) -> int { return XR3 ? 3 * XT + buf * WT2 : buf * ST + XT; };
@@ -365,6 +395,10 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     if (kt == nk_main && nk_main > 0) set_x(true);  // ext tiles come last, in issue order
     const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
     const uint32_t l = lds0 + xaddr(st) + wv * (PPW * 1024);
+    if (dma_batch && xp == PPW) {
+      glds_batch(xo, sb, l);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < PPW; ++i)
       if (i < xp) glds_s(xo[i], sb, l + i * 1024);
@@ -373,6 +407,10 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     if (kt == nk_main && nk_main > 0) set_w(true);
     const char* sb = wb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
     const uint32_t l = lds0 + waddr(st) + wv * (PPW * 1024);
+    if (dma_batch && wp == PPW) {
+      glds_batch(wo, sb, l);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < PPW; ++i)
       if (i < wp) glds_s(wo[i], sb, l + i * 1024);
@@ -584,6 +622,12 @@ static SplitWs ws_for(hipStream_t s) {
 static int g_variant = [] {
   const char* e = getenv("LTX_GEMM_VARIANT");
   return e ? atoi(e) : 0;
+}();
+// LTX_GEMM_DMA_BATCH=0: the large-tile kernel issues each LDS-DMA piece in its own asm block
+// (M0 saved / set / restored per piece) instead of one block per wave's piece set
+static int g_dma_batch = [] {
+  const char* e = getenv("LTX_GEMM_DMA_BATCH");
+  return (e && e[0] == '0') ? 0 : 1;
 }();
 
 // The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can
@@ -900,6 +944,7 @@ extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, 
   p.alpha = alpha; p.rank = (int)rank; p.rows_per_batch = (int)(rows_per_batch > 0 ? rows_per_batch : M);
   p.A2 = (const bf16_t*)A2; p.W2 = (const bf16_t*)W2; p.lda2 = lda2; p.ldw2 = ldw2; p.K2 = (int)K2;
   p.ext_gn = (int)ext_group_cols; p.ext_gs = ext_group_stride;
+  p.dma_batch = g_dma_batch;
   p.ws = nullptr; p.splitk = 1;
   hipStream_t s = (hipStream_t)stream;
   switch (epilogue) {

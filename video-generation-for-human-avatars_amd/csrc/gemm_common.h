@@ -41,6 +41,7 @@ struct GemmParams {
   // tile never straddles two groups.
   int ext_gn;
   int64_t ext_gs;
+  int dma_batch;  // large-tile kernel: issue a wave's DMA pieces in one asm block (1) or singly (0)
   // split-K (small grids): S partial f32 tiles [S][M][N] in a caller-provided workspace, summed by
   // splitk_epilogue_kernel which then applies bias + the epilogue
   float* ws;
