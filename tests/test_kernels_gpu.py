@@ -186,6 +186,52 @@ def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
     assert rel(dq32, qf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),  # no key bias
+                                                      (8, 4, 1792, 256, True, True),    # bench's attn2
+                                                      (1, 2, 300, 200, True, False),    # ragged both
+                                                      (2, 2, 64, 33, False, False)])    # < 2 waves
+def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
+    """Nk <= 256 runs the one-pass backward (attn_bwd1_kernel: S/dP once, dQ from the dS image);
+    LTX_ATTN_BWD1=0 forces the split dQ + dK/dV kernels. Both against fp32 autograd: rel-Frobenius
+    <= 2e-2, and the one-pass error within 1.25x the split path's (+1e-3)."""
+    from ltx_amd import ops
+    d = 64
+    scale = d ** -0.5
+    Bk = 1 if shared else B
+    q = g(B * Nq, H * d, seed=11)
+    k = g(Bk * Nk, H * d, seed=12)
+    v = g(Bk * Nk, H * d, seed=13)
+    do = g(B * Nq, H * d, seed=14)
+    bias = None
+    if masked:
+        keep = torch.arange(Nk, device=DEV)[None, :] < (Nk - 5 - 3 * torch.arange(Bk, device=DEV)[:, None])
+        bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
+    o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias, kv_shared=shared)
+    kx = k.repeat(B, 1) if shared else k
+    vx = v.repeat(B, 1) if shared else v
+    bx = (bias.repeat(B, 1) if shared else bias) if bias is not None else None
+    qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (q, kx, vx))
+    _sdpa_ref(qf, kf, vf, B, H, d, bx).backward(do.float())
+    errs = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("LTX_ATTN_BWD1", mode)
+        for f32 in (False, True):
+            dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, dq_f32=f32,
+                                      kv_shared=shared)
+            if shared:
+                dk = dk.float().view(B, Nk, H * d).sum(0).repeat(B, 1)
+                dv = dv.float().view(B, Nk, H * d).sum(0).repeat(B, 1)
+                kg = kf.grad.view(B, Nk, H * d).sum(0).repeat(B, 1)
+                vg = vf.grad.view(B, Nk, H * d).sum(0).repeat(B, 1)
+            else:
+                kg, vg = kf.grad, vf.grad
+            errs[mode, f32] = (rel(dq, qf.grad), rel(dk, kg), rel(dv, vg))
+    for f32 in (False, True):
+        for e1, e0 in zip(errs["1", f32], errs["0", f32]):
+            assert e1 < 2e-2 and e0 < 2e-2, errs
+            assert e1 <= 1.25 * e0 + 1e-3, errs
+
+
 def test_attention_strided_fused_qkv():
     """Q/K/V read in place from the fused [M, 3*H*d] projection buffer (attn1 layout)."""
     from ltx_amd import ops

@@ -116,12 +116,12 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 // chunk c = tid % CH of rows tid / CH + i * RSTEP: its byte offsets inside a tile are constant,
 // so a tile is one scalar base (row0 * ld) + a 24-bit-multiply lane offset per load (no per-tile
 // 64-bit address math, no lane predicates); rows past a ragged end re-read the last row.
-template <int HD, int ROWS>
+template <int HD, int ROWS, int NTH = ATT_THREADS>
 struct TileStage {
   static constexpr int CH = HD / 8;
-  static constexpr int PER = ROWS * CH / ATT_THREADS;
-  static constexpr int RSTEP = ATT_THREADS / CH;
-  static_assert(ROWS * CH % ATT_THREADS == 0, "a tile must split evenly over the workgroup");
+  static constexpr int PER = ROWS * CH / NTH;
+  static constexpr int RSTEP = NTH / CH;
+  static_assert(ROWS * CH % NTH == 0, "a tile must split evenly over the workgroup");
   u32x4 v[PER];
   __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int row0, int nrows, int tid) {
     const int r = tid / CH, c = tid % CH;
@@ -586,6 +586,257 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
     }
 }
 
+// =============================================================================================
+// One-pass backward for key ranges of at most 256 (the attn2 cross-attention over the caption
+// tokens): a workgroup = 8 waves x 32 keys holds EVERY key of one (batch, head), so dQ needs no
+// sum across workgroups and S / dP are computed once per tile instead of once in each of the
+// dK/dV and dQ kernels (5 MFMA products per tile instead of 7).
+// Per 64-query tile: the dK/dV kernel's S, dP, dV^T += dO^T.P, dK^T += Q^T.dS (keys on lanes);
+// dS (bf16, the same rounding the dK product uses) goes to an LDS image [key][query]; after a
+// barrier each wave computes dQ^T = K^T.dS^T for HD/32 16x16 output tiles over all 256 keys
+// (v_mfma_f32_16x16x32_bf16, both operands by transposed reads of the [key][.] images, so the
+// lane holds 4 consecutive head dims of one query: 8-byte stores).
+// k-slot order inside a 32-key step: slots 8g + j (g = lane >> 4) stand for keys 4g + j (j < 4)
+// and 16 + 4g + j - 4 (j >= 4), the same on both operands; each 32-lane half then reads 8
+// consecutive image rows, which the row swizzle keeps conflict-free.
+// =============================================================================================
+constexpr int BWD1_KEYS = 256;
+constexpr int BWD1_THREADS = 512;
+
+template <int HD, bool BIAS>
+__global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnParams p) {
+  constexpr int QT = 64;
+  constexpr int KS = HD / 16;
+  constexpr int DS = HD / 32;
+  constexpr int TILE = QT * HD * 2;
+  constexpr int KIMG = BWD1_KEYS * HD * 2;  // K image [key][HD]
+  constexpr int SIMG = BWD1_KEYS * QT * 2;  // dS image [key][64 queries], two of them
+  constexpr int NDB = HD / 16;              // 16-wide head-dim blocks of dQ
+  constexpr int QBW = HD / 32;              // 16-query blocks per wave (4 * NDB / 8 waves)
+  constexpr int KSTEPS = BWD1_KEYS / 32;    // 32-key steps of the dQ product
+  // Q / dO tiles and their row statistics double-buffered: one barrier per query tile
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + KIMG + 2 * SIMG];
+  __shared__ __attribute__((aligned(16))) float st_lse[2][QT];
+  __shared__ __attribute__((aligned(16))) float st_dl[2][QT];
+  char* kimg = smem + 4 * TILE;
+  char* simg0 = kimg + KIMG;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const LaneOfs<HD> lofs(lane);
+  const int hh = blockIdx.x, b = blockIdx.y;
+  const int kl = wave * 32 + (lane & 31);  // this lane's key
+  const int kc = min(kl, p.Nk - 1);
+  const float c2 = p.scale * LOG2E;
+  float kbias = 0.f;
+  if (BIAS) {
+    kbias = -INFINITY;
+    if (kl < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + kl] * LOG2E : 0.f;
+  }
+  const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  s16x8 kf[KS], vf[KS];
+  {
+    const bf16_t* kr = kbase + (int64_t)kc * p.ldk;
+    const bf16_t* vr = p.v + ((int64_t)b * p.kvb + kc) * p.ldv + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = *(const s16x8*)(kr + ks * 16 + 8 * h);
+      vf[ks] = *(const s16x8*)(vr + ks * 16 + 8 * h);
+    }
+  }
+  {  // K image of all 256 key rows (rows past Nk re-read the last: their dS is 0)
+    TileStage<HD, BWD1_KEYS, BWD1_THREADS> kst;
+    kst.load(kbase, p.ldk, 0, p.Nk, tid);
+    kst.store(kimg, tid);
+  }
+  f32x16 dka[DS], dva[DS];
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dka[d][r] = 0.f;
+      dva[d][r] = 0.f;
+    }
+
+  // dQ: this wave's head-dim block and query blocks; per-lane transposed-read offsets (the
+  // swizzle of rows 4g + q' (+16, +32 ks) depends on 4g + q' only)
+  const int db = wave % NDB, qb0 = (wave / NDB) * QBW;
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int offk = toff<HD>(4 * g4 + qq, 2 * db + (pp >> 1)) + 8 * (pp & 1);
+  int offs[QBW];
+#pragma unroll
+  for (int i = 0; i < QBW; ++i) offs[i] = toff<64>(4 * g4 + qq, 2 * (qb0 + i) + (pp >> 1)) + 8 * (pp & 1);
+  const int srow = kl * (QT * 2) + 8 * h;  // this lane's dS image row (+ chunk ^ swizzle)
+  const int sw4 = swz<64>(kl) << 4;
+  auto tr4 = [](const char* a) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
+  };
+  // dQ^T += K^T . dS^T over 32-key steps [k0, k1) of the dS image `sim`
+  f32x4 dqa[QBW];
+  auto dq_steps = [&](const char* sim, int k0, int k1) {
+#pragma unroll
+    for (int ks = k0; ks < k1; ++ks) {
+      const char* ka = kimg + ks * 32 * (HD * 2) + offk;
+      const s16x4 a0 = tr4(ka), a1 = tr4(ka + 16 * (HD * 2));
+      s16x8 av;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        av[j] = a0[j];
+        av[4 + j] = a1[j];
+      }
+#pragma unroll
+      for (int i = 0; i < QBW; ++i) {
+        const char* sa = sim + ks * 32 * (QT * 2) + offs[i];
+        const s16x4 b0 = tr4(sa), b1 = tr4(sa + 16 * (QT * 2));
+        s16x8 bv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bv[j] = b0[j];
+          bv[4 + j] = b1[j];
+        }
+        dqa[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, dqa[i], 0, 0, 0);
+      }
+    }
+  };
+  auto dq_store = [&](int q0) {
+#pragma unroll
+    for (int i = 0; i < QBW; ++i) {
+      // lane: query 16 (qb0 + i) + (lane & 15), head dims 16 db + 4 (lane >> 4) .. +3
+      const int q = q0 + 16 * (qb0 + i) + (lane & 15);
+      if (q < p.Nq) {
+        const int64_t col = (int64_t)hh * HD + 16 * db + 4 * g4;
+        if (p.dq_f32) {
+          const f32x4 w = {dqa[i][0] * p.scale, dqa[i][1] * p.scale, dqa[i][2] * p.scale, dqa[i][3] * p.scale};
+          *(f32x4*)((float*)p.dq + ((int64_t)b * p.Nq + q) * p.lddq + col) = w;
+        } else {
+          u32x2 w;
+          w[0] = pack2(dqa[i][0] * p.scale, dqa[i][1] * p.scale);
+          w[1] = pack2(dqa[i][2] * p.scale, dqa[i][3] * p.scale);
+          *(u32x2*)((bf16_t*)p.dq + ((int64_t)b * p.Nq + q) * p.lddq + col) = w;
+        }
+      }
+    }
+  };
+
+  const bf16_t* qbase = p.q + (int64_t)b * p.Nq * p.ldq + hh * HD;
+  const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
+  const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
+  const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
+  TileStage<HD, QT, BWD1_THREADS> qs_, os_;
+  const int ntiles = (p.Nq + QT - 1) / QT;
+  auto stage_stats = [&](int qb, int buf) {
+    if (tid < QT) {
+      const int q = qb + tid;
+      st_lse[buf][tid] = q < p.Nq ? -lbase[q] : -INFINITY;  // -lse2 (rows past Nq: P = 0)
+      st_dl[buf][tid] = q < p.Nq ? dbase[q] : 0.f;
+    }
+  };
+  qs_.load(qbase, p.ldq, 0, p.Nq, tid);
+  os_.load(obase, p.lddo, 0, p.Nq, tid);
+  qs_.store(smem, tid);
+  os_.store(smem + TILE, tid);
+  stage_stats(0, 0);
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);  // retire the pre-loop loads (see attn_dkdv_kernel)
+
+  // Tile t's dQ product runs during tile t+1's S / dP / dK / dV (its dS image is the other
+  // buffer): one barrier interval holds both, so the dQ MFMAs fill the softmax VALU gaps.
+  for (int t = 0; t < ntiles; ++t) {
+    const int q0 = t * QT;
+    char* simg = simg0 + (t & 1) * SIMG;
+    const char* qtile = smem + (t & 1) * 2 * TILE;
+    const char* otile = qtile + TILE;
+    const float* sl = st_lse[t & 1];
+    const float* sd = st_dl[t & 1];
+    const char* sprev = simg0 + ((t + 1) & 1) * SIMG;
+    if (t + 1 < ntiles) {
+      qs_.load(qbase, p.ldq, q0 + QT, p.Nq, tid);
+      os_.load(obase, p.lddo, q0 + QT, p.Nq, tid);
+    }
+#pragma unroll
+    for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] = 0.f;
+        dp[r] = 0.f;
+      }
+      s16x8 qfr[KS], ofr[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        qfr[ks] = row_frag<HD>(qtile, u * 32, ks, lofs);
+        ofr[ks] = row_frag<HD>(otile, u * 32, ks, lofs);
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s = mfma32(qfr[ks], kf[ks], s);
+        dp = mfma32(ofr[ks], vf[ks], dp);
+      }
+      if (t > 0) dq_steps(sprev, u * (KSTEPS / 2), (u + 1) * (KSTEPS / 2));
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 nl4 = *(const f32x4*)&sl[u * 32 + 8 * g + 4 * h];
+        const f32x4 dl4 = *(const f32x4*)&sd[u * 32 + 8 * g + 4 * h];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i;
+          const float pr = fast_exp2(fmaf(s[r], c2, BIAS ? kbias + nl4[i] : nl4[i]));
+          s[r] = pr;
+          dp[r] = pr * (dp[r] - dl4[i]);
+        }
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const s16x8 pb = acc_frag(s, ss);
+        const s16x8 sb = acc_frag(dp, ss);
+#pragma unroll
+        for (int d = 0; d < DS; ++d) {
+          dva[d] = mfma32(tr_frag<HD>(otile, u * 32, ss, d, lofs), pb, dva[d]);
+          dka[d] = mfma32(tr_frag<HD>(qtile, u * 32, ss, d, lofs), sb, dka[d]);
+        }
+        // dS rows of this lane's key: registers 8ss + 4gg + i are queries 32u + 16ss + 8gg + 4h + i
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          u32x2 w;
+          w[0] = (unsigned)(unsigned short)sb[4 * gg] | ((unsigned)(unsigned short)sb[4 * gg + 1] << 16);
+          w[1] = (unsigned)(unsigned short)sb[4 * gg + 2] | ((unsigned)(unsigned short)sb[4 * gg + 3] << 16);
+          int cx;
+          asm volatile("v_xor_b32 %0, %1, %2" : "=v"(cx) : "i"((4 * u + 2 * ss + gg) << 4), "v"(sw4));
+          *(u32x2*)(simg + srow + cx) = w;
+        }
+      }
+    }
+    if (t > 0) dq_store(q0 - QT);
+    if (t + 1 < ntiles) {  // tile t+1 into the other buffers (tile t-1's, free since the last barrier)
+      char* nt = smem + ((t + 1) & 1) * 2 * TILE;
+      qs_.store(nt, tid);
+      os_.store(nt + TILE, tid);
+      stage_stats(q0 + QT, (t + 1) & 1);
+    }
+    __syncthreads();  // dS image t and tile t+1 complete; tile t-1's buffers no longer read
+  }
+#pragma unroll
+  for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  dq_steps(simg0 + ((ntiles - 1) & 1) * SIMG, 0, KSTEPS);
+  dq_store((ntiles - 1) * QT);
+  if (kl >= p.Nk) return;
+  bf16_t* krow = p.dk + ((int64_t)b * p.Nk + kl) * p.lddk + hh * HD;
+  bf16_t* vrow = p.dv + ((int64_t)b * p.Nk + kl) * p.lddv + hh * HD;
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 wk, wv;
+      wk[0] = pack2(dka[d][4 * g] * p.scale, dka[d][4 * g + 1] * p.scale);
+      wk[1] = pack2(dka[d][4 * g + 2] * p.scale, dka[d][4 * g + 3] * p.scale);
+      wv[0] = pack2(dva[d][4 * g], dva[d][4 * g + 1]);
+      wv[1] = pack2(dva[d][4 * g + 2], dva[d][4 * g + 3]);
+      *(u32x2*)(krow + d * 32 + 8 * g + 4 * h) = wk;
+      *(u32x2*)(vrow + d * 32 + 8 * g + 4 * h) = wv;
+    }
+}
+
 // delta[b,h,q] = sum_d dO*O (f32), one wave per (b, q) row covering all heads
 template <int HD>
 __global__ __launch_bounds__(256) void attn_delta_kernel(const AttnParams p, float* __restrict__ delta) {
@@ -623,6 +874,13 @@ static int xcd_order_flag() {  // LTX_ATTN_XCD=0: hardware block order (A/B meas
   return v;
 }
 
+// LTX_ATTN_BWD1=0: the split dQ + dK/dV kernels for every key range (read per call, so a test
+// can compare both paths in one process)
+static int bwd1_flag() {
+  const char* e = getenv("LTX_ATTN_BWD1");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 template <int HD>
 static int launch_fwd(AttnParams p, hipStream_t s) {
   p.xcd_order = xcd_order_flag();
@@ -644,6 +902,17 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   }
   p.delta = delta;
   p.xcd_order = xcd_order_flag();
+  if constexpr (HD == 64) {  // (head dim 32, the tiny config, keeps the split kernels)
+    if (p.Nk <= BWD1_KEYS && bwd1_flag()) {  // every key in one workgroup: one-pass backward
+      const dim3 g1((unsigned)p.H, (unsigned)p.B);
+      if (p.key_bias != nullptr || p.Nk != BWD1_KEYS)
+        hipLaunchKernelGGL((attn_bwd1_kernel<HD, true>), g1, dim3(BWD1_THREADS), 0, s, p);
+      else
+        hipLaunchKernelGGL((attn_bwd1_kernel<HD, false>), g1, dim3(BWD1_THREADS), 0, s, p);
+      LTX_LAUNCH_CHECK();
+      return LTX_OK;
+    }
+  }
   dim3 gq((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   dim3 gk((unsigned)((p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   if (needs_bias(p)) {

@@ -332,8 +332,13 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
     else:
         delta = torch.empty(B, H, Nq, dtype=F32, device=dev)
     bias = "true" if key_bias is not None else "false"
-    label = ("attention backward: " + ("" if ready else f"ltx::attn_delta_kernel<{d}> + ") +
-             f"ltx::attn_dkdv_kernel<{d}, {bias}> + ltx::attn_q_kernel<{d}, 1, {bias}>")
+    if d == 64 and Nk <= 256 and os.environ.get("LTX_ATTN_BWD1", "1") != "0":
+        # every key in one workgroup: the one-pass kernel (attention.hip attn_bwd1_kernel)
+        b1 = "true" if (key_bias is not None or Nk != 256) else "false"
+        kern = f"ltx::attn_bwd1_kernel<{d}, {b1}>"
+    else:
+        kern = f"ltx::attn_dkdv_kernel<{d}, {bias}> + ltx::attn_q_kernel<{d}, 1, {bias}>"
+    label = ("attention backward: " + ("" if ready else f"ltx::attn_delta_kernel<{d}> + ") + kern)
     timer = _timer if (_timer is not None and _timer.wants(label)) else None
     ev0 = timer.start() if timer is not None else None
     call("ltx_attn_bwd_ex", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"),
