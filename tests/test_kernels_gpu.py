@@ -232,6 +232,35 @@ def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
             assert e1 <= 1.25 * e0 + 1e-3, errs
 
 
+@pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),
+                                                      (8, 4, 1792, 256, True, True),
+                                                      (1, 2, 300, 200, True, False),
+                                                      (2, 2, 40, 64, False, False)])
+def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
+    """Nk <= 256 runs attn_fwd1_kernel (K/V staged once per (batch, head)); its per-slice
+    arithmetic is the tiled kernel's, so O and lse are bitwise those of LTX_ATTN_FWD1=0."""
+    from ltx_amd import ops
+    d = 64
+    Bk = 1 if shared else B
+    q = g(B * Nq, H * d, seed=21)
+    k = g(Bk * Nk, H * d, seed=22)
+    v = g(Bk * Nk, H * d, seed=23)
+    bias = None
+    if masked:
+        keep = torch.arange(Nk, device=DEV)[None, :] < (Nk - 5 - 3 * torch.arange(Bk, device=DEV)[:, None])
+        bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
+    monkeypatch.setenv("LTX_ATTN_FWD1", "1")
+    o1, l1 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)
+    monkeypatch.setenv("LTX_ATTN_FWD1", "0")
+    o0, l0 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)
+    assert torch.equal(o1, o0)
+    assert torch.equal(l1, l0)
+    kx = k.repeat(B, 1) if shared else k
+    vx = v.repeat(B, 1) if shared else v
+    bx = (bias.repeat(B, 1) if shared else bias) if bias is not None else None
+    assert rel(o1, _sdpa_ref(q, kx, vx, B, H, d, bx)) < 1e-2
+
+
 def test_attention_strided_fused_qkv():
     """Q/K/V read in place from the fused [M, 3*H*d] projection buffer (attn1 layout)."""
     from ltx_amd import ops

@@ -212,8 +212,9 @@ __device__ __forceinline__ void xcd_block(int xcd_order, int& bx, int& by, int& 
   bz = wg / (gx * gy);
 }
 
-template <int HD, int MODE, bool BIAS>
-__global__ __launch_bounds__(ATT_THREADS, MODE == 1 ? 3 : 2) void attn_q_kernel(const AttnParams p) {
+// NW waves (NW x 32 queries) per workgroup: 4, or 8 to halve the K/V staging per query
+template <int HD, int MODE, bool BIAS, int NW = 4>
+__global__ __launch_bounds__(NW * 64, MODE == 1 ? 3 : 2) void attn_q_kernel(const AttnParams p) {
   constexpr int KT = 64;                 // keys per tile
   constexpr int KS = HD / 16;            // 16-deep k-steps over the head dim
   constexpr int DS = HD / 32;            // 32-wide d subtiles
@@ -227,7 +228,7 @@ __global__ __launch_bounds__(ATT_THREADS, MODE == 1 ? 3 : 2) void attn_q_kernel(
   const LaneOfs<HD> lofs(lane);
   int bx, hh, b;
   xcd_block(p.xcd_order, bx, hh, b);
-  const int q0 = bx * 128 + wave * 32;
+  const int q0 = bx * (NW * 32) + wave * 32;
   const int qi = q0 + (lane & 31);
   const int qc = min(qi, p.Nq - 1);
   const float c2 = p.scale * LOG2E;
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(ATT_THREADS, MODE == 1 ? 3 : 2) void attn_q_kernel(
     for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
   float m_run = -1e30f, l_run = 0.f;  // m_run in scaled log2 units
 
-  TileStage<HD, KT> ks_, vs_;
+  TileStage<HD, KT, NW * 64> ks_, vs_;
   const int ntiles = (p.Nk + KT - 1) / KT;
   ks_.load(kbase, p.ldk, 0, p.Nk, tid);
   vs_.load(vbase, p.ldv, 0, p.Nk, tid);
@@ -445,8 +446,9 @@ __global__ __launch_bounds__(ATT_THREADS, MODE == 1 ? 3 : 2) void attn_q_kernel(
 // dK / dV: keys on lanes, queries in registers; workgroup = 4 waves x 32 keys. Query tiles of 64
 // (two 32-row halves) between barrier pairs, so each wave runs 32 MFMAs per LDS refill.
 // =============================================================================================
-template <int HD, bool BIAS>
-__global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnParams p) {
+// NW waves (NW x 32 keys) per workgroup: 4, or 8 to halve the Q/dO staging per key
+template <int HD, bool BIAS, int NW = 4>
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_dkdv_kernel(const AttnParams p) {
   constexpr int QT = 64;
   constexpr int KS = HD / 16;
   constexpr int DS = HD / 32;
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   const LaneOfs<HD> lofs(lane);
   int bx, hh, b;
   xcd_block(p.xcd_order, bx, hh, b);
-  const int key = bx * 128 + wave * 32 + (lane & 31);
+  const int key = bx * (NW * 32) + wave * 32 + (lane & 31);
   const int kc = min(key, p.Nk - 1);
   const float c2 = p.scale * LOG2E;
   float kbias = 0.f;
@@ -493,7 +495,7 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
   const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
   const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
   const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
-  TileStage<HD, QT> qs_, os_;
+  TileStage<HD, QT, NW * 64> qs_, os_;
   const int ntiles = (p.Nq + QT - 1) / QT;
   auto stage_stats = [&](int qb) {
     if (tid < QT) {
@@ -586,6 +588,151 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
     }
 }
 
+// key ranges of at most this many run the one-pass kernels (one 8-wave workgroup holds them all)
+constexpr int BWD1_KEYS = 256;
+constexpr int BWD1_THREADS = 512;
+
+// =============================================================================================
+// Forward for key ranges of at most 256 (the attn2 cross-attention): a workgroup = 8 waves per
+// (batch, head) stages ALL K / V rows (and the key bias) into LDS once; each wave then sweeps
+// query slices w, w + 8, ... (32 queries each) with no barrier, the next slice's Q fragments
+// loaded while the current slice computes. The split kernel (attn_q_kernel) reloads K/V per
+// 128-query workgroup in 64-key tiles behind two barriers each, which at Nk = 256 is mostly
+// exposed load latency. Arithmetic per slice is attn_q_kernel's MODE 0 loop, bit for bit.
+// =============================================================================================
+template <int HD, bool BIAS>
+__global__ __launch_bounds__(BWD1_THREADS, 1) void attn_fwd1_kernel(const AttnParams p) {
+  constexpr int KT = 64;
+  constexpr int KS = HD / 16;
+  constexpr int DS = HD / 32;
+  constexpr int IMG = BWD1_KEYS * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
+  __shared__ __attribute__((aligned(16))) float kb[BWD1_KEYS];
+  char* kimg = smem;
+  char* vimg = smem + IMG;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const LaneOfs<HD> lofs(lane);
+  const int hh = blockIdx.x, b = blockIdx.y;
+  const float c2 = p.scale * LOG2E;
+  {
+    const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+    const bf16_t* vbase = p.v + (int64_t)b * p.kvb * p.ldv + hh * HD;
+    TileStage<HD, BWD1_KEYS, BWD1_THREADS> ks_, vs_;
+    ks_.load(kbase, p.ldk, 0, p.Nk, tid);
+    vs_.load(vbase, p.ldv, 0, p.Nk, tid);
+    ks_.store(kimg, tid);
+    vs_.store(vimg, tid);
+    if (BIAS && tid < BWD1_KEYS) {
+      float v = -INFINITY;
+      if (tid < p.Nk) v = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + tid] * LOG2E : 0.f;
+      kb[tid] = v;
+    }
+  }
+  __syncthreads();
+  const int ntiles = (p.Nk + KT - 1) / KT;
+  const int nslices = (p.Nq + 31) / 32;
+  const bf16_t* qb = p.q + (int64_t)b * p.Nq * p.ldq + hh * HD;
+  s16x8 qn[KS];
+  auto load_q = [&](int sl) {
+    const int qc = min(sl * 32 + (lane & 31), p.Nq - 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qn[ks] = *(const s16x8*)(qb + (int64_t)qc * p.ldq + ks * 16 + 8 * h);
+  };
+  if (wave < nslices) load_q(wave);
+  for (int sl = wave; sl < nslices; sl += BWD1_THREADS / 64) {
+    s16x8 qf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = qn[ks];
+    if (sl + BWD1_THREADS / 64 < nslices) load_q(sl + BWD1_THREADS / 64);
+    f32x16 acc[DS];
+#pragma unroll
+    for (int d = 0; d < DS; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+    for (int t = 0; t < ntiles; ++t) {
+      const int k0 = t * KT;
+      f32x16 s[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(kimg, k0 + u * 32, ks, lofs), qf[ks], s[u]);
+      }
+      float mt = -1e30f;
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const f32x4 kb4 = *(const f32x4*)&kb[k0 + u * 32 + 8 * g + 4 * h];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float x = fmaf(s[u][4 * g + i], c2, kb4[i]);
+              s[u][4 * g + i] = x;
+              mt = fmaxf(mt, x);
+            }
+          }
+      } else {
+        float mr[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mr[r & 3] = fmaxf(mr[r & 3], s[u][r]);
+        mt = fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3])) * c2;
+      }
+      mt = xor32_max(mt);
+      const float m_new = fmaxf(m_run, mt);
+      if (__any(m_new > m_run)) {
+        const float alpha = fast_exp2(m_run - m_new);
+        l_run *= alpha;
+#pragma unroll
+        for (int d = 0; d < DS; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[d][r] *= alpha;
+        m_run = m_new;
+      }
+      const float nm = -m_run;
+      float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = BIAS ? fast_exp2(s[u][r] + nm) : fast_exp2(fmaf(s[u][r], c2, nm));
+          s[u][r] = e;
+          ls[r & 3] += e;
+        }
+      l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const s16x8 pb = acc_frag(s[u], ss);
+#pragma unroll
+          for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vimg, k0 + u * 32, ss, d, lofs), pb, acc[d]);
+        }
+    }
+    const int qi = sl * 32 + (lane & 31);
+    const float l_tot = xor32_sum(l_run);
+    if (qi < p.Nq) {
+      const float inv = 1.0f / l_tot;
+      bf16_t* orow = p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD;
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u32x2 w;
+          w[0] = pack2(acc[d][4 * g] * inv, acc[d][4 * g + 1] * inv);
+          w[1] = pack2(acc[d][4 * g + 2] * inv, acc[d][4 * g + 3] * inv);
+          *(u32x2*)(orow + d * 32 + 8 * g + 4 * h) = w;
+        }
+      if (h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
+    }
+  }
+}
+
 // =============================================================================================
 // One-pass backward for key ranges of at most 256 (the attn2 cross-attention over the caption
 // tokens): a workgroup = 8 waves x 32 keys holds EVERY key of one (batch, head), so dQ needs no
@@ -600,8 +747,6 @@ __global__ __launch_bounds__(ATT_THREADS, 2) void attn_dkdv_kernel(const AttnPar
 // and 16 + 4g + j - 4 (j >= 4), the same on both operands; each 32-lane half then reads 8
 // consecutive image rows, which the row swizzle keeps conflict-free.
 // =============================================================================================
-constexpr int BWD1_KEYS = 256;
-constexpr int BWD1_THREADS = 512;
 
 template <int HD, bool BIAS>
 __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnParams p) {
@@ -881,9 +1026,49 @@ static int bwd1_flag() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
+// LTX_ATTN_W8 (A/B switch, read per call): bit 0 = 8-wave (256-query) tiled forward, bit 1 =
+// 8-wave (256-key) dK/dV kernel; the default is LTX_ATTN_W8_DEFAULT (forward only: self-attention
+// forward 297-305 vs 310-316 us, dK/dV 881-889 vs 857-862 us with 8 waves, tools/attn_bench.py)
+#ifndef LTX_ATTN_W8_DEFAULT
+#define LTX_ATTN_W8_DEFAULT 1
+#endif
+static int waves8_flag(int bit) {
+  const char* e = getenv("LTX_ATTN_W8");
+  const int v = e ? atoi(e) : LTX_ATTN_W8_DEFAULT;
+  return (v >> bit) & 1;
+}
+
+// LTX_ATTN_FWD1=0: the tiled forward (attn_q_kernel) for every key range
+static int fwd1_flag() {
+  const char* e = getenv("LTX_ATTN_FWD1");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 template <int HD>
 static int launch_fwd(AttnParams p, hipStream_t s) {
   p.xcd_order = xcd_order_flag();
+  if constexpr (HD == 64) {
+    if (p.Nk <= BWD1_KEYS && fwd1_flag()) {  // every key staged once per (batch, head)
+      const dim3 g1((unsigned)p.H, (unsigned)p.B);
+      if (needs_bias(p))
+        hipLaunchKernelGGL((attn_fwd1_kernel<HD, true>), g1, dim3(BWD1_THREADS), 0, s, p);
+      else
+        hipLaunchKernelGGL((attn_fwd1_kernel<HD, false>), g1, dim3(BWD1_THREADS), 0, s, p);
+      LTX_LAUNCH_CHECK();
+      return LTX_OK;
+    }
+  }
+  if constexpr (HD == 64) {
+    if (waves8_flag(0)) {
+      dim3 grid((unsigned)((p.Nq + 255) / 256), (unsigned)p.H, (unsigned)p.B);
+      if (needs_bias(p))
+        hipLaunchKernelGGL((attn_q_kernel<HD, 0, true, 8>), grid, dim3(512), 0, s, p);
+      else
+        hipLaunchKernelGGL((attn_q_kernel<HD, 0, false, 8>), grid, dim3(512), 0, s, p);
+      LTX_LAUNCH_CHECK();
+      return LTX_OK;
+    }
+  }
   dim3 grid((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   if (needs_bias(p))
     hipLaunchKernelGGL((attn_q_kernel<HD, 0, true>), grid, dim3(ATT_THREADS), 0, s, p);
@@ -914,15 +1099,23 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
     }
   }
   dim3 gq((unsigned)((p.Nq + 127) / 128), (unsigned)p.H, (unsigned)p.B);
-  dim3 gk((unsigned)((p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
+  bool k8 = false;
+  if constexpr (HD == 64) k8 = waves8_flag(1);
+  dim3 gk((unsigned)(k8 ? (p.Nk + 255) / 256 : (p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   if (needs_bias(p)) {
     hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
     LTX_LAUNCH_CHECK();
-    hipLaunchKernelGGL((attn_dkdv_kernel<HD, true>), gk, dim3(ATT_THREADS), 0, s, p);
+    if (k8)
+      hipLaunchKernelGGL((attn_dkdv_kernel<HD, true, HD == 64 ? 8 : 4>), gk, dim3(512), 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_dkdv_kernel<HD, true>), gk, dim3(ATT_THREADS), 0, s, p);
   } else {
     hipLaunchKernelGGL((attn_q_kernel<HD, 1, false>), gq, dim3(ATT_THREADS), 0, s, p);
     LTX_LAUNCH_CHECK();
-    hipLaunchKernelGGL((attn_dkdv_kernel<HD, false>), gk, dim3(ATT_THREADS), 0, s, p);
+    if (k8)
+      hipLaunchKernelGGL((attn_dkdv_kernel<HD, false, HD == 64 ? 8 : 4>), gk, dim3(512), 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_dkdv_kernel<HD, false>), gk, dim3(ATT_THREADS), 0, s, p);
   }
   LTX_LAUNCH_CHECK();
   return LTX_OK;

@@ -304,8 +304,13 @@ def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
     Nk = k.shape[0] if kv_shared else k.shape[0] // B
     o = torch.empty(B * Nq, H * d, dtype=BF16, device=q.device) if out is None else out
     lse = torch.empty(B, H, Nq, dtype=F32, device=q.device)
-    bias = "true" if key_bias is not None else "false"
-    label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}>"
+    bias = "true" if (key_bias is not None or Nk % 64) else "false"
+    if d == 64 and Nk <= 256 and os.environ.get("LTX_ATTN_FWD1", "1") != "0":
+        label = f"attention forward: ltx::attn_fwd1_kernel<{d}, {bias}>"  # K/V staged once
+    elif d == 64 and int(os.environ.get("LTX_ATTN_W8", "1")) & 1:  # 8 waves x 32 queries
+        label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}, 8>"
+    else:
+        label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}>"
     timer = _timer if (_timer is not None and _timer.wants(label)) else None
     ev0 = timer.start() if timer is not None else None
     call("ltx_attn_fwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
