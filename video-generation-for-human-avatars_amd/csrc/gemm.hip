@@ -566,22 +566,40 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   __syncthreads();
   if constexpr (STAMP) st3 = rt_stamp();
   const int cgrp = tid & 31;
-  for (int rr = tid >> 5; rr < BMT; rr += NT / 32) {
+  // row pass: this thread's rows (tid >> 5) + RPP i. Epilogues that read aux rows issue the loads
+  // of U rows before the first row's arithmetic (one load in flight per row instead of a
+  // vmcnt(0) wait per row; LTX_GEMM_EPI_BATCH=0 restores the one-row loop for A/B runs)
+  constexpr int RPP = NT / 32, NPASS = BMT / RPP;
+  constexpr int U = epi_has_aux<EPI>() ? (NPASS % 7 == 0 ? 7 : 8) : 1;
+  static_assert(NPASS % U == 0, "row passes split evenly");
+  auto row_out = [&](int rr, const EpiAux* pre) {
     const int m = m0 + rr;
     const int n = n0 + cgrp * 8;
-    if (m >= p.M || n >= p.N) continue;
+    if (m >= p.M || n >= p.N) return;
     const u32x2 lo = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16);
     const u32x2 hi = *(const u32x2*)(cimg + rr * C_STRIDE2 + cgrp * 16 + 8);
     bf16_t cv[8] = {(bf16_t)lo[0], (bf16_t)(lo[0] >> 16), (bf16_t)lo[1], (bf16_t)(lo[1] >> 16),
                     (bf16_t)hi[0], (bf16_t)(hi[0] >> 16), (bf16_t)hi[1], (bf16_t)(hi[1] >> 16)};
     float o[8];
-    epilogue_row8<EPI, R>(p, m, n, cv, o);
+    epilogue_row8<EPI, R>(p, m, n, cv, o, pre);
     u32x4 pk;
     pk[0] = pack2(o[0], o[1]);
     pk[1] = pack2(o[2], o[3]);
     pk[2] = pack2(o[4], o[5]);
     pk[3] = pack2(o[6], o[7]);
     *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
+  };
+  if (U > 1 && p.epi_batch) {
+    for (int i0 = 0; i0 < NPASS; i0 += U) {
+      EpiAux ax[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)  // clamped: every load is in bounds, rows past M are not stored
+        epi_load<EPI>(p, min(m0 + (tid >> 5) + (i0 + u) * RPP, p.M - 1), min(n0 + cgrp * 8, p.N - 8), ax[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) row_out((tid >> 5) + (i0 + u) * RPP, &ax[u]);
+    }
+  } else {
+    for (int rr = tid >> 5; rr < BMT; rr += RPP) row_out(rr, nullptr);
   }
   if constexpr (STAMP) {
     if (tid == 0) {
@@ -627,6 +645,11 @@ static int g_variant = [] {
 // (M0 saved / set / restored per piece) instead of one block per wave's piece set
 static int g_dma_batch = [] {
   const char* e = getenv("LTX_GEMM_DMA_BATCH");
+  return (e && e[0] == '0') ? 0 : 1;
+}();
+// LTX_GEMM_EPI_BATCH=0: the large-tile epilogue row pass loads one row's aux operands at a time
+static int g_epi_batch = [] {
+  const char* e = getenv("LTX_GEMM_EPI_BATCH");
   return (e && e[0] == '0') ? 0 : 1;
 }();
 
@@ -945,6 +968,7 @@ extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, 
   p.A2 = (const bf16_t*)A2; p.W2 = (const bf16_t*)W2; p.lda2 = lda2; p.ldw2 = ldw2; p.K2 = (int)K2;
   p.ext_gn = (int)ext_group_cols; p.ext_gs = ext_group_stride;
   p.dma_batch = g_dma_batch;
+  p.epi_batch = g_epi_batch;
   p.ws = nullptr; p.splitk = 1;
   hipStream_t s = (hipStream_t)stream;
   switch (epilogue) {

@@ -42,6 +42,7 @@ struct GemmParams {
   int ext_gn;
   int64_t ext_gs;
   int dma_batch;  // large-tile kernel: issue a wave's DMA pieces in one asm block (1) or singly (0)
+  int epi_batch;  // large-tile kernel: epilogue aux loads of several rows in flight (1) or one (0)
   // split-K (small grids): S partial f32 tiles [S][M][N] in a caller-provided workspace, summed by
   // splitk_epilogue_kernel which then applies bias + the epilogue
   float* ws;
@@ -74,9 +75,27 @@ __device__ __forceinline__ void block_to_tile(int bid, int ntm, int ntn, int& tm
   tn = (wg % (GROUP * ntn)) / gsize;
 }
 
+// The aux operands one epilogue row chunk reads (aux0 row m, and the gate row of m's batch for the
+// gated residual), loaded ahead of the arithmetic by epi_load so a row pass keeps many loads in
+// flight instead of waiting on one per row.
+struct EpiAux {
+  u32x4 a, g;
+};
+template <int EPI>
+constexpr bool epi_has_aux() {
+  return EPI == LTX_EPI_STORE_ROWDOT || EPI == LTX_EPI_GATED_RESIDUAL || EPI == LTX_EPI_GELU_BWD ||
+         EPI == LTX_EPI_ACCUM;
+}
+template <int EPI>
+__device__ __forceinline__ void epi_load(const GemmParams& p, int m, int n0, EpiAux& x) {
+  if constexpr (epi_has_aux<EPI>()) x.a = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+  if constexpr (EPI == LTX_EPI_GATED_RESIDUAL)
+    x.g = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)(m / p.rows_per_batch) * p.ld1 + n0);
+}
+
 template <int EPI, int R>
 __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0, const bf16_t* cvals,
-                                              float* out8) {
+                                              float* out8, const EpiAux* pre = nullptr) {
   // cvals: 8 bf16 of bf16(acc [+ bias]) for columns n0..n0+7 of row m
   float v[8];
 #pragma unroll
@@ -88,7 +107,7 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
     // every epilogue site hands a row's 8-column chunks to consecutive lanes, so a head of
     // hd = p.rank (32 / 64) columns is hd/8 lanes aligned at a multiple of hd/8 (N % hd == 0,
     // checked at launch): reduce there
-    const u32x4 o4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    const u32x4 o4 = pre ? pre->a : *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -131,8 +150,8 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       *(u32x4*)((bf16_t*)p.aux2 + (int64_t)m * p.ld2 + n0) = pk;
     }
     const int b = m / p.rows_per_batch;
-    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
-    const u32x4 g4 = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)b * p.ld1 + n0);
+    const u32x4 r4 = pre ? pre->a : *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    const u32x4 g4 = pre ? pre->g : *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)b * p.ld1 + n0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float r = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16)));
@@ -161,7 +180,7 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
     }
   } else if constexpr (EPI == LTX_EPI_GELU_BWD) {
     // dF = bf16(bf16(acc) * gelu'(F)), F = aux0 pre-activation bf16 (ld0)
-    const u32x4 f4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    const u32x4 f4 = pre ? pre->a : *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       const f32x2 f = {bf2f((bf16_t)f4[j >> 1]), bf2f((bf16_t)(f4[j >> 1] >> 16))};
@@ -171,7 +190,7 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
     }
   } else if constexpr (EPI == LTX_EPI_ACCUM) {
     // out = R + bf16(acc): R = aux0 (ld0); C may alias R
-    const u32x4 r4 = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    const u32x4 r4 = pre ? pre->a : *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + v[j];
   } else if constexpr (EPI == LTX_EPI_LORA_DGRAD_ACCUM) {
