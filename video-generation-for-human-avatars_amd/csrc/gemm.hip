@@ -540,20 +540,22 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     return;
   }
 
-  // epilogue stage 1: bf16(acc + bias) -> LDS image [BMT m][256 n]
+  // epilogue stage 1: bf16(acc + bias) -> LDS image [BMT m][256 n]; the NF bias chunks are all
+  // loaded before the first use (one wait, not one per fragment column)
   char* cimg = smem;
+  u32x2 bias2[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    bias2[i] = (u32x2){0u, 0u};
+    const int gn = n0 + wn * WTN + i * 16 + (lane >> 4) * 4;
+    if (p.bias && gn + 3 < p.N) bias2[i] = *(const u32x2*)(p.bias + gn);
+  }
 #pragma unroll
   for (int i = 0; i < NF; ++i) {
     const int nl = wn * WTN + i * 16 + (lane >> 4) * 4;
-    float b4[4] = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias) {
-      const int gn = n0 + nl;
-      if (gn + 3 < p.N) {
-        const u32x2 bb = *(const u32x2*)(p.bias + gn);
-        b4[0] = bf2f((bf16_t)bb[0]); b4[1] = bf2f((bf16_t)(bb[0] >> 16));
-        b4[2] = bf2f((bf16_t)bb[1]); b4[3] = bf2f((bf16_t)(bb[1] >> 16));
-      }
-    }
+    const u32x2 bb = bias2[i];
+    const float b4[4] = {bf2f((bf16_t)bb[0]), bf2f((bf16_t)(bb[0] >> 16)), bf2f((bf16_t)bb[1]),
+                         bf2f((bf16_t)(bb[1] >> 16))};
 #pragma unroll
     for (int j = 0; j < MF; ++j) {
       const int ml = wm * WTM + j * 16 + (lane & 15);
