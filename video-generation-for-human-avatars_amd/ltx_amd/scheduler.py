@@ -1,9 +1,10 @@
 """RectifiedFlowScheduler (ltx_video/schedulers/rf.py:179-426): training side and the
 inference step.
 
-add_noise / build_velocity_target keep the reference signatures; on ROCm tensors both run in the
-fused kernel ltx_rf_noise_velocity (f32 arithmetic, bf16 result -- the reference computes the
-same f32 values and train_step casts them to the model dtype at training.py:143,146).
+add_noise / build_velocity_target keep the reference signatures and its f32 results (kernel
+ltx_rf_noise_velocity_f32); train_step's fused prologue (ltx_rf_prepare_tokens) computes the same
+f32 values and rounds them to the model dtype once, where the reference casts at
+training.py:143,146.
 shift_timesteps implements the SD3 and SimpleDiffusion resolution shifts (rf.py:49-149);
 anything else is the reference's silent no-op. The timestep shift math acts on [B] scalars and
 stays in torch (host-side plumbing), as does the 20-entry schedule of set_timesteps.
