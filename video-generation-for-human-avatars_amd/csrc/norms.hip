@@ -21,6 +21,17 @@ __device__ __forceinline__ void load8f(const float* p, float* v) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
 }
+// the MAXP 16-B chunks of a row (chunk p at p*512 + 8*lane) issued together: addresses clamped
+// into the row so no per-chunk branch separates the loads (hipcc otherwise waits vmcnt(0) on
+// each chunk before issuing the next one); chunks past D are ignored by the caller
+__device__ __forceinline__ void load_row_raw(const bf16_t* row, int D, int lane, u32x4 (&raw)[MAXP]) {
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) raw[p] = *(const u32x4*)(row + min(p * 512 + lane * 8, D - 8));
+}
+__device__ __forceinline__ void unpack8(const u32x4 w, float* v) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f((bf16_t)(w[j >> 1] >> ((j & 1) * 16)));
+}
 __device__ __forceinline__ void store8(bf16_t* p, const float* v) {
   u32x4 w;
 #pragma unroll
@@ -43,13 +54,16 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_fwd_kernel(
   const bf16_t* xr = x + (int64_t)m * D;
   float v[MAXP][8];
   float ss = 0.f;
+  {
+    u32x4 raw[MAXP];
+    load_row_raw(xr, D, lane, raw);
 #pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    const int e = p * 512 + lane * 8;
-    if (e < D) {
-      load8(xr + e, v[p]);
+    for (int p = 0; p < MAXP; ++p) {
+      unpack8(raw[p], v[p]);
+      if (p * 512 + lane * 8 < D) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
+        for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
+      }
     }
   }
   ss = wave_sum(ss);
@@ -92,14 +106,17 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_bwd_kernel(
   const bf16_t* op = onep + (int64_t)b * ld_mod;
   u32x4 gpk[MAXP], xpk[MAXP];
   float dr = 0.f;
+  u32x4 dyr[MAXP], opr[MAXP];
+  load_row_raw(dy + (int64_t)m * D, D, lane, dyr);
+  load_row_raw(x + (int64_t)m * D, D, lane, xpk);
+  load_row_raw(op, D, lane, opr);
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
     if (e < D) {
       float d8[8], o8[8], g8[8];
-      load8(dy + (int64_t)m * D + e, d8);
-      load8(op + e, o8);
-      xpk[p] = *(const u32x4*)(x + (int64_t)m * D + e);
+      unpack8(dyr[p], d8);
+      unpack8(opr[p], o8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         g8[j] = rbf(d8[j] * o8[j]);
@@ -324,13 +341,16 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
   const bf16_t* w = which ? kw : qw;
   float v[MAXP][8];
   float ss = 0.f;
+  {
+    u32x4 raw[MAXP];
+    load_row_raw(in, D, lane, raw);
 #pragma unroll
-  for (int p = 0; p < MAXP; ++p) {
-    const int e = p * 512 + lane * 8;
-    if (e < D) {
-      load8(in + e, v[p]);
+    for (int p = 0; p < MAXP; ++p) {
+      unpack8(raw[p], v[p]);
+      if (p * 512 + lane * 8 < D) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
+        for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
+      }
     }
   }
   ss = wave_sum(ss);
@@ -389,6 +409,10 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
   const int64_t csrow = ((int64_t)(m / N) * cs_batch_rows + (m % N)) * (D / 2);
   float gx[MAXP][8], xv[MAXP][8];
   float dr = 0.f;
+  // the bf16 gradient row and the input row: all chunks in flight together
+  u32x4 graw[MAXP], xraw[MAXP];
+  if (!gf32) load_row_raw((const bf16_t*)gin + (int64_t)m * ldg, D, lane, graw);
+  load_row_raw(xin, D, lane, xraw);
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
@@ -399,7 +423,7 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) g8[j] = rbf(g8[j]);
       } else {
-        load8((const bf16_t*)gin + (int64_t)m * ldg + e, g8);
+        unpack8(graw[p], g8);
       }
       if (rope) {
         float c4[4], s4[4];
@@ -418,7 +442,7 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
         for (int j = 0; j < 8; ++j) dn[j] = g8[j];
       }
       load8(w + e, w8);
-      load8(xin + e, xv[p]);
+      unpack8(xraw[p], xv[p]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         gx[p][j] = rbf(dn[j] * w8[j]);
