@@ -565,15 +565,13 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
       *(u32x2*)(cimg + ml * C_STRIDE2 + nl * 2) = pk;
     }
   }
-  __syncthreads();
-  if constexpr (STAMP) st3 = rt_stamp();
   const int cgrp = tid & 31;
-  // row pass: this thread's rows (tid >> 5) + RPP i. Epilogues that read aux rows issue the loads
-  // of U rows before the first row's arithmetic (one load in flight per row instead of a
-  // vmcnt(0) wait per row; LTX_GEMM_EPI_BATCH=0 restores the one-row loop for A/B runs)
+  // row pass: this thread's rows (tid >> 5) + RPP i. Epilogues that read aux rows issue every
+  // row's aux loads right after stage 1 and cross the image barrier with an LDS-only wait, so the
+  // loads overlap the barrier and no row waits on its own load (hipcc had emitted one load +
+  // vmcnt(0) per row; LTX_GEMM_EPI_BATCH=0 restores that one-row loop for A/B runs)
   constexpr int RPP = NT / 32, NPASS = BMT / RPP;
-  constexpr int U = epi_has_aux<EPI>() ? (NPASS % 7 == 0 ? 7 : 8) : 1;
-  static_assert(NPASS % U == 0, "row passes split evenly");
+  constexpr bool BATCH = epi_has_aux<EPI>();
   auto row_out = [&](int rr, const EpiAux* pre) {
     const int m = m0 + rr;
     const int n = n0 + cgrp * 8;
@@ -591,16 +589,18 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     pk[3] = pack2(o[6], o[7]);
     *(u32x4*)(p.C + (int64_t)m * p.ldc + n) = pk;
   };
-  if (U > 1 && p.epi_batch) {
-    for (int i0 = 0; i0 < NPASS; i0 += U) {
-      EpiAux ax[U];
+  if (BATCH && p.epi_batch) {
+    EpiAux ax[BATCH ? NPASS : 1];
 #pragma unroll
-      for (int u = 0; u < U; ++u)  // clamped: every load is in bounds, rows past M are not stored
-        epi_load<EPI>(p, min(m0 + (tid >> 5) + (i0 + u) * RPP, p.M - 1), min(n0 + cgrp * 8, p.N - 8), ax[u]);
+    for (int u = 0; u < NPASS; ++u)  // clamped: every load is in bounds, rows past M are not stored
+      epi_load<EPI>(p, min(m0 + (tid >> 5) + u * RPP, p.M - 1), min(n0 + cgrp * 8, p.N - 8), ax[u]);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // C image complete
+    if constexpr (STAMP) st3 = rt_stamp();
 #pragma unroll
-      for (int u = 0; u < U; ++u) row_out((tid >> 5) + (i0 + u) * RPP, &ax[u]);
-    }
+    for (int u = 0; u < NPASS; ++u) row_out((tid >> 5) + u * RPP, &ax[u]);
   } else {
+    __syncthreads();
+    if constexpr (STAMP) st3 = rt_stamp();
     for (int rr = tid >> 5; rr < BMT; rr += RPP) row_out(rr, nullptr);
   }
   if constexpr (STAMP) {
