@@ -175,9 +175,19 @@ __device__ __forceinline__ void key_bias_tile(float* kb, const AttnParams& p, in
 // (self-attention, Nk % 64 == 0) the per-key LDS reads and adds disappear.
 // VALU diet (the forward is VALU-bound at head dim 64): the running max is taken on the raw
 // scores (scale > 0), each probability is one v_fma + one v_exp_f32, and the O rescale is skipped
-// whenever no lane's max grew (exact: alpha would be 1).
+// unless some lane's max grew by more than RESCALE_TAU (deferred max, above).
 // =============================================================================================
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Deferred max (forward kernels): the running max m_run (log2 units) and with it O and l are
+// rescaled only when some lane's tile max exceeds it by more than RESCALE_TAU; below that the
+// probabilities 2^(s - m_run) stay <= 2^TAU (exact in f32, bf16 keeps its relative precision for
+// the P.V MFMA) and lse = m_run + log2(l) is unchanged in meaning. Most 64-key tiles then skip the
+// O rescale pass.
+#ifndef LTX_RESCALE_TAU
+#define LTX_RESCALE_TAU 8.0f
+#endif
+constexpr float RESCALE_TAU = LTX_RESCALE_TAU;
 
 // lane l and lane l ^ 32 combined without an LDS round trip (v_permlane32_swap): both halves
 // get the bit-identical result (same operand order in every lane)
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(NW * 64, MODE == 1 ? 3 : 2) void attn_q_kernel(cons
       }
       mt = xor32_max(mt);
       const float m_new = fmaxf(m_run, mt);
-      if (__any(m_new > m_run)) {
+      if (__any(m_new > m_run + RESCALE_TAU)) {
         const float alpha = fast_exp2(m_run - m_new);
         l_run *= alpha;
 #pragma unroll
@@ -685,7 +695,7 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_fwd1_kernel(const AttnPa
       }
       mt = xor32_max(mt);
       const float m_new = fmaxf(m_run, mt);
-      if (__any(m_new > m_run)) {
+      if (__any(m_new > m_run + RESCALE_TAU)) {
         const float alpha = fast_exp2(m_run - m_new);
         l_run *= alpha;
 #pragma unroll
