@@ -611,7 +611,7 @@ constexpr int BWD1_THREADS = 512;
 // exposed load latency. Arithmetic per slice is attn_q_kernel's MODE 0 loop, bit for bit.
 // =============================================================================================
 template <int HD, bool BIAS>
-__global__ __launch_bounds__(BWD1_THREADS, 1) void attn_fwd1_kernel(const AttnParams p) {
+__global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BIAS ? 4 : 2, 4))) void attn_fwd1_kernel(const AttnParams p) {
   constexpr int KT = 64;
   constexpr int KS = HD / 16;
   constexpr int DS = HD / 32;
@@ -649,12 +649,16 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_fwd1_kernel(const AttnPa
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qn[ks] = *(const s16x8*)(qb + (int64_t)qc * p.ldq + ks * 16 + 8 * h);
   };
-  if (wave < nslices) load_q(wave);
-  for (int sl = wave; sl < nslices; sl += BWD1_THREADS / 64) {
+  // blockIdx.z of gridDim.z workgroups per (batch, head) takes every gridDim.z-th 8-slice group
+  const int sstep = (BWD1_THREADS / 64) * gridDim.z;
+  const int s0 = wave + (BWD1_THREADS / 64) * blockIdx.z;
+  for (int sl = s0; sl < nslices; sl += sstep) {
+    // (no cross-slice Q prefetch: at two workgroups per CU the other one covers the load, and
+    // its 16 registers would push the kernel past the 128 that 4 waves per SIMD allow)
+    load_q(sl);
     s16x8 qf[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[ks] = qn[ks];
-    if (sl + BWD1_THREADS / 64 < nslices) load_q(sl + BWD1_THREADS / 64);
     f32x16 acc[DS];
 #pragma unroll
     for (int d = 0; d < DS; ++d)
@@ -1059,7 +1063,9 @@ static int launch_fwd(AttnParams p, hipStream_t s) {
   p.xcd_order = xcd_order_flag();
   if constexpr (HD == 64) {
     if (p.Nk <= BWD1_KEYS && fwd1_flag()) {  // every key staged once per (batch, head)
-      const dim3 g1((unsigned)p.H, (unsigned)p.B);
+      // two workgroups per (batch, head) when that still leaves >= 8 slices each: 2 per CU
+      const int nsl = (p.Nq + 31) / 32;
+      const dim3 g1((unsigned)p.H, (unsigned)p.B, nsl >= 16 ? 2u : 1u);
       if (needs_bias(p))
         hipLaunchKernelGGL((attn_fwd1_kernel<HD, true>), g1, dim3(BWD1_THREADS), 0, s, p);
       else
