@@ -29,5 +29,5 @@ python3 $R/tools/pmc_table.py $RAW/pmc_sq/run_counter_collection.csv > $OUT/pmc_
 python3 $R/tools/kernel_traffic.py $RAW/pmc_f/run_counter_collection.csv $RAW/pmc_w/run_counter_collection.csv \
     $OUT/traffic.json > /dev/null
 python3 $R/tools/hbm_table.py $RAW/pmc_f/run_counter_collection.csv $RAW/pmc_w/run_counter_collection.csv \
-    $RAW/short/run_results.db 4 $OUT/hbm_per_kernel.md > /dev/null
+    $RAW/short/run_results.db 8 $OUT/hbm_per_kernel.md > /dev/null
 ls -la $OUT
