@@ -17,7 +17,7 @@ timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format cs
     python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $RAW/pmc_w.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format rocpd -d $RAW/short -o run -- \
     python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $RAW/short.log 2>&1
-python3 $R/tools/rocpd_summary.py $RAW/trace/run_results.db 18 60 > $OUT/trace_summary.txt
+python3 $R/tools/rocpd_summary.py $RAW/trace/run_results.db 23 60 > $OUT/trace_summary.txt  # 2 warm-up + 16 timed + 1 + 4 timer steps
 python3 $R/tools/pmc_summary.py stats $RAW/trace/run_kernel_stats.csv $OUT/kernel_stats.md > /dev/null
 cp $RAW/trace/run_kernel_stats.csv $OUT/kernel_stats.csv
 python3 $R/tools/pmc_summary.py traffic $RAW/pmc_f/run_counter_collection.csv $RAW/pmc_w/run_counter_collection.csv \
