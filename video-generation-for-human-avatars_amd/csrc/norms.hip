@@ -315,13 +315,21 @@ __global__ __launch_bounds__(256) void rope_pack_kernel(const bf16_t* __restrict
   cs[idx] = (uint32_t)cosv[e] | ((uint32_t)sinv[e] << 16);
 }
 
-__device__ __forceinline__ void cs4(const uint32_t* __restrict__ cs, int64_t rowbase, int e, float* c, float* s) {
-  const u32x4 v = *(const u32x4*)(cs + rowbase + (e >> 1));
+__device__ __forceinline__ void cs_unpack(const u32x4 v, float* c, float* s) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     c[t] = bf2f((bf16_t)(v[t] & 0xffff));
     s[t] = bf2f((bf16_t)(v[t] >> 16));
   }
+}
+__device__ __forceinline__ void cs4(const uint32_t* __restrict__ cs, int64_t rowbase, int e, float* c, float* s) {
+  cs_unpack(*(const u32x4*)(cs + rowbase + (e >> 1)), c, s);
+}
+// the packed (cos, sin) words of a row's MAXP chunks (D / 2 words per row), clamped like
+// load_row_raw so all chunks go out with the row loads
+__device__ __forceinline__ void load_cs_raw(const uint32_t* __restrict__ csr, int D, int lane, u32x4 (&raw)[MAXP]) {
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) raw[p] = *(const u32x4*)(csr + (min(p * 512 + lane * 8, D - 8) >> 1));
 }
 
 // one wave = one (row, q|k) item
@@ -341,9 +349,14 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
   const bf16_t* w = which ? kw : qw;
   float v[MAXP][8];
   float ss = 0.f;
+  // the row, the weight and the RoPE words: one round trip
+  const int64_t csrow = ((int64_t)(m / N) * cs_batch_rows + (m % N)) * (D / 2);
+  u32x4 wraw[MAXP], csraw[MAXP];
   {
     u32x4 raw[MAXP];
     load_row_raw(in, D, lane, raw);
+    load_row_raw(w, D, lane, wraw);
+    if (rope) load_cs_raw(cs + csrow, D, lane, csraw);
 #pragma unroll
     for (int p = 0; p < MAXP; ++p) {
       unpack8(raw[p], v[p]);
@@ -356,18 +369,17 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)D + eps);
   if (lane == 0) (which ? rstd_k : rstd_q)[m] = r;
-  const int64_t csrow = ((int64_t)(m / N) * cs_batch_rows + (m % N)) * (D / 2);
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
     if (e < D) {
       float w8[8], nv[8], o[8];
-      load8(w + e, w8);
+      unpack8(wraw[p], w8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) nv[j] = rbf(rbf(v[p][j] * r) * w8[j]);
       if (rope) {
         float c4[4], s4[4];
-        cs4(cs, csrow, e, c4, s4);
+        cs_unpack(csraw[p], c4, s4);
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
           const float c = c4[j >> 1], s = s4[j >> 1];
@@ -410,9 +422,11 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
   float gx[MAXP][8], xv[MAXP][8];
   float dr = 0.f;
   // the bf16 gradient row and the input row: all chunks in flight together
-  u32x4 graw[MAXP], xraw[MAXP];
+  u32x4 graw[MAXP], xraw[MAXP], wraw[MAXP], csraw[MAXP];
   if (!gf32) load_row_raw((const bf16_t*)gin + (int64_t)m * ldg, D, lane, graw);
   load_row_raw(xin, D, lane, xraw);
+  load_row_raw(w, D, lane, wraw);
+  if (rope) load_cs_raw(cs + csrow, D, lane, csraw);
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
@@ -427,7 +441,7 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
       }
       if (rope) {
         float c4[4], s4[4];
-        cs4(cs, csrow, e, c4, s4);
+        cs_unpack(csraw[p], c4, s4);
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
           const float c = c4[j >> 1], s = s4[j >> 1];
@@ -441,7 +455,7 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) dn[j] = g8[j];
       }
-      load8(w + e, w8);
+      unpack8(wraw[p], w8);
       unpack8(xraw[p], xv[p]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
