@@ -59,6 +59,34 @@ __global__ __launch_bounds__(256) void stream_kernel(const u32x4* __restrict__ x
   out[blockIdx.x * 256 + threadIdx.x] = (float)acc;
 }
 
+// P4: P0 plus lora_down's adapter loads (f32 W[16][K]: per 32-deep k step a lane reads the 8
+// weights of its j = lane & 15 at k = kb + 8 * (lane >> 4), served from L2 / L1)
+__global__ __launch_bounds__(512) void ldw_kernel(const uint16_t* __restrict__ x, int ldx, const float* __restrict__ W, float* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int m0 = blockIdx.x * 32, k0 = wave * 256;
+  float facc = 0.f;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int grp = 0; grp < 2; ++grp) {
+    u32x4 v[8];
+    float4 w[4][2];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int k = k0 + 32 * (grp * 4 + st) + 8 * (lane >> 4);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) v[st * 2 + q] = *(const u32x4*)(x + (int64_t)(m0 + 16 * q + (lane & 15)) * ldx + k);
+      const float* wp = W + (int64_t)(lane & 15) * ldx + k;
+      w[st][0] = *(const float4*)wp;
+      w[st][1] = *(const float4*)(wp + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc ^= v[i][0] + v[i][1] + v[i][2] + v[i][3];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) facc += w[st][0].x + w[st][1].w;
+  }
+  out[blockIdx.x * 512 + threadIdx.x] = (float)acc + facc;
+}
+
 // P3: lora_down geometry with all 16 loads of a wave in flight at once
 __global__ __launch_bounds__(512) void ld16_kernel(const uint16_t* __restrict__ x, int ldx, float* out) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -107,6 +135,24 @@ int main() {
       const double us = tot / reps * 1e3;
       printf("%s %s: %.2f us  %.0f GB/s\n", hot ? "hot " : "cold", names[p], us, (double)M * K * 2 / us / 1e3);
     }
+  }
+  {
+    float* W;
+    hipMalloc(&W, (size_t)16 * K * 4);
+    hipMemset(W, 0, (size_t)16 * K * 4);
+    float tot = 0.f;
+    const int reps = 50;
+    for (int r = 0; r < reps + 5; ++r) {
+      hipEventRecord(a, 0);
+      hipLaunchKernelGGL(ldw_kernel, dim3(M / 32), dim3(512), 0, 0, x, K, W, out);
+      hipEventRecord(b, 0);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      if (r >= 5) tot += ms;
+    }
+    const double us = tot / reps * 1e3;
+    printf("hot  P4 P0 + adapter loads : %.2f us  %.0f GB/s (x only)\n", us, (double)M * K * 2 / us / 1e3);
   }
   // hot only: ceilings
   const int64_t n16 = (int64_t)M * K / 8;
