@@ -185,20 +185,36 @@ def cpu_baseline(budget_layers=28, warmup=2, timed=5):
                        f"(os.cpu_count()={os.cpu_count()} is the whole shared host)")}
 
 
+def _kernel_key(name):
+    """rocprofv3 / bench kernel name -> comparison key: no argument list, no 'void ', no spaces,
+    and trailing template arguments that are 0 (defaulted parameters print as ', 0') dropped."""
+    k = name.split("(")[0].replace("void ", "").replace(" ", "")
+    while k.endswith(",0>"):
+        k = k[:-3] + ">"
+    return k
+
+
 def load_traffic(label):
-    """Measured HBM bytes per launch of the kernel(s) behind `label` from the committed PMC
-    summary (tools/kernel_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or None."""
-    path = os.path.join(REPO, "profiles", "r02_traffic.json")
+    """Measured HBM bytes per launch of the kernel(s) behind `label`, from the NEWEST committed
+    PMC summary profiles/r*_traffic.json (tools/kernel_traffic.py: FETCH_SIZE x2 + WRITE_SIZE,
+    separate passes, means over every dispatch of the name). Returns (bytes, file name) or
+    (None, reason)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_traffic.json")))
+    if not files:
+        return None, "no profiles/r*_traffic.json"
+    path = files[-1]
     try:
         with open(path) as f:
             table = json.load(f)["bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        return None
-    names = [n.split("(")[0].strip() for n in label.split(": ", 1)[-1].split(" + ")]
-    vals = [table.get(n) for n in names]
+    except (OSError, ValueError, KeyError) as exc:
+        return None, f"{os.path.basename(path)}: {exc!r}"[:160]
+    keyed = {_kernel_key(k): v for k, v in table.items()}
+    names = [_kernel_key(n) for n in label.split(": ", 1)[-1].split(" + ")]
+    vals = [keyed.get(n) for n in names]
     if any(v is None for v in vals):
-        return None
-    return float(sum(vals))
+        return None, f"{os.path.basename(path)} has no entry for {label}"
+    return float(sum(vals)), os.path.basename(path)
 
 
 def infer_main(args):
@@ -407,6 +423,10 @@ def main():
     for k in kernels + [dom]:
         k["tflops"] = k["flops"] / (k["ms"] * 1e-3) / 1e12
     achieved = dom["tflops"]
+    if args.config == "a" and not full:
+        traffic, traffic_src = load_traffic(dom["kernel"])
+    else:
+        traffic, traffic_src = None, "measured for config A LoRA only"
     line = {
         "metric": f"LTX-2B {'full (ZeRO-2)' if full else 'LoRA'} train-step samples/sec (latent-tokens/sec = samples/sec x {N})",
         "value": round(value, 4),
@@ -438,7 +458,11 @@ def main():
         "roofline": {"bound": "mfma", "kernel": dom["kernel"],
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),
-                     "traffic": (load_traffic(dom["kernel"]) if args.config == "a" and not full else None),
+                     "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "algorithmic_bytes": dom["bytes"] / dom["launches"],
+                     "traffic_over_algorithmic": (round(traffic / (dom["bytes"] / dom["launches"]), 3)
+                                                  if traffic and dom["bytes"] else None),
                      "launch_ms": round(dom["ms"] / dom["launches"], 4), "launches": dom["launches"],
                      "share_of_step": round(dom["ms"] / prof_steps / (elapsed * 1e3 / args.steps), 4),
                      "timing": f"HIP events around each of its launches in {prof_steps} steps after the timed region",

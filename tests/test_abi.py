@@ -52,7 +52,43 @@ def test_gemm_describe_names_the_dispatched_kernel():
         return buf.value.decode()
     M = 8 * 1792
     # N = 2048 tiles: 64 x 8 = 512 of 224 rows fill two rounds exactly
-    assert name(M, 2048, 8192) == "ltx::gemm_nt_kernel_t<0, 0, 224, 4, 0, 0, 8>(ltx::GemmParams)"
-    assert name(M, 8192, 2048, epi="gelu") == "ltx::gemm_nt_kernel_t<1, 0, 256, 8, 0, 0, 8>(ltx::GemmParams)"
+    assert name(M, 2048, 8192) == "ltx::gemm_nt_kernel_t<0, 0, 224, 4, 0>(ltx::GemmParams)"
+    assert name(M, 8192, 2048, epi="gelu") == "ltx::gemm_nt_kernel_t<1, 0, 256, 8, 0>(ltx::GemmParams)"
     # the text side (M = 256 rows) runs the 128x128 kernel with three LDS stages
     assert name(256, 4096, 2048, K2=128).startswith("ltx::gemm_nt_kernel<0, 0, 3>")
+
+
+def test_gemm_set_variant_rejects_removed_schedules():
+    """Only the tile-height knobs remain (0 / 13 / 14); the not-adopted schedules are no longer
+    in the library (tools/experiments/)."""
+    from ltx_amd import _lib
+    lib = _lib.load()
+    assert lib.ltx_gemm_set_variant(13) == 0
+    assert lib.ltx_gemm_set_variant(0) == 0
+    for v in (30, 40, 50, 60):
+        assert lib.ltx_gemm_set_variant(v) != 0
+    assert lib.ltx_gemm_set_variant(0) == 0
+
+
+def test_bench_traffic_lookup_reads_newest_profile():
+    """bench.py's roofline.traffic comes from the newest committed profiles/r*_traffic.json, with
+    kernel names compared after dropping the argument list and trailing default (0) template
+    arguments, and names the file it used."""
+    import glob
+    import importlib.util
+    import json
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench._kernel_key("void ltx::gemm_nt_kernel_t<0, 0, 224, 4, 0>(ltx::GemmParams)") == \
+        "ltx::gemm_nt_kernel_t<0,0,224,4>"
+    newest = sorted(glob.glob(os.path.join(repo, "profiles", "r*_traffic.json")))[-1]
+    table = json.load(open(newest))["bytes_per_launch"]
+    name, val = max(((k, v) for k, v in table.items() if k.startswith("ltx::gemm_nt_kernel_t")),
+                    key=lambda kv: kv[1])
+    got, src = bench.load_traffic(name + "(ltx::GemmParams)")
+    assert src == os.path.basename(newest) and got == val
+    got, why = bench.load_traffic("ltx::no_such_kernel<1>")
+    assert got is None and "no entry" in why

@@ -23,7 +23,40 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _ltx28(dev, seed=1234):
+    """The full 28-layer LTX-2B model with LoRA r=16 (7.34 M f32 adapter params) + trainable
+    caption_projection (12.59 M bf16), random init drawn on the device (the bench's init)."""
+    import math
+    from ltx_amd.config import TrainConfig
+    from ltx_amd.lora import apply_training_strategy
+    from ltx_amd.patchifier import SymmetricPatchifier
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG, Transformer3DModel
+    with torch.device("meta"):
+        model = Transformer3DModel.from_config(OURS_TRANSFORMER_CONFIG)
+        apply_training_strategy(model, TrainConfig(checkpoint_path="-", lora_rank=16, lora_alpha=16),
+                                "lora_audio")
+    g = torch.Generator(device=dev).manual_seed(seed)
+    sd = {}
+    for name, p in model.named_parameters():
+        t = torch.empty(p.shape, dtype=torch.float32, device=dev)
+        if p.dim() == 2:
+            t.normal_(0, 1.0 / math.sqrt(p.shape[1]), generator=g)
+        elif "norm" in name:
+            t.fill_(1.0)
+        else:
+            t.normal_(0, 0.02, generator=g)
+        if "lora_B" in name:
+            t.normal_(0, 0.01, generator=g)
+        sd[name] = t.to(torch.float32 if "lora_" in name else torch.bfloat16)
+    model.load_state_dict(sd, assign=True, strict=True)
+    for n, p in model.named_parameters():
+        p.requires_grad_(("lora_" in n) or ("caption_projection" in n))
+    model.patchifier = SymmetricPatchifier(1)
+    model.train()
+    return model
+
+
+def _worker(rank, world, port, out_dir, kind):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (os.path.join(os.path.dirname(here), "video-generation-for-human-avatars_amd"),
@@ -34,57 +67,74 @@ def _worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from safetensors.torch import load_file
-        from model_utils import build_model
+        from model_utils import build_full_model, build_model
         from ltx_amd.config import TrainConfig
         from ltx_amd.scheduler import RectifiedFlowScheduler
         from ltx_amd.training import GradAllReduce, train_step
-        d = load_file(os.path.join(GOLD, "tiny_train_step.safetensors"))
-        with open(os.path.join(GOLD, "tiny_train_step.json")) as f:
-            meta = json.load(f)
-        params = {k[2:]: v for k, v in d.items() if k.startswith("w.")}
+        import ltx_oracle as O
         dev = "cuda:0"
+        golden = "tiny_full_step" if kind == "full" else "tiny_train_step"
+        d = load_file(os.path.join(GOLD, golden + ".safetensors"))
+        with open(os.path.join(GOLD, golden + ".json")) as f:
+            meta = json.load(f)
         tc = TrainConfig(checkpoint_path="-", gradient_accumulation_steps=2)
+        bucket_mb = 25.0 if kind == "ltx28" else 0.05
         res = {}
         for mode in ("overlap", "posthoc", "local"):
-            model = build_model(meta["config"], params, meta["lora_rank"], device=dev)
+            if kind == "ltx28":
+                model = _ltx28(dev)
+                shapes = {"latents": (1, 128, 2, 8, 8), "ref_image_latents": (1, 128, 1, 8, 8),
+                          "pose_latents": (1, 128, 2, 8, 8)}
+                prompt = torch.randn(1, 256, 4096, generator=torch.Generator().manual_seed(9)).to(dev, torch.bfloat16)
+                pmask = (torch.arange(256) < 16).long().view(1, 256).to(dev)
+            else:
+                if kind == "full":
+                    params = O.make_params(meta["config"], meta["param_seed"], lora_rank=0, requires_grad=False)
+                    model = build_full_model(meta["config"], params, device=dev)
+                else:
+                    params = {k[2:]: v for k, v in d.items() if k.startswith("w.")}
+                    model = build_model(meta["config"], params, meta["lora_rank"], device=dev)
+                shapes = {k: d["in." + k].shape for k in ("latents", "ref_image_latents", "pose_latents")}
+                prompt, pmask = d["in.prompt_embeds"].to(dev), d["in.prompt_attention_mask"].to(dev)
             trainable = [p for p in model.parameters() if p.requires_grad]
             red = None
             if mode != "local":
-                red = GradAllReduce(trainable, bucket_mb=0.05, order=model.grad_ready_order()).install(model)
+                red = GradAllReduce(trainable, bucket_mb=bucket_mb, order=model.grad_ready_order()).install(model)
                 red.zero_grad()
             g = torch.Generator().manual_seed(500 + rank)
             for step in range(2):
                 if mode == "overlap" and step == 1:
                     red.arm()
-                batch = {k: torch.randn(d["in." + k].shape, generator=g).to(dev, torch.bfloat16)
-                         for k in ("latents", "ref_image_latents", "pose_latents")}
-                B = batch["latents"].shape[0]
+                batch = {k: torch.randn(shapes[k], generator=g).to(dev, torch.bfloat16) for k in shapes}
+                B, C, F_, H_, W_ = batch["latents"].shape
                 t = torch.rand(B, generator=g).to(dev)
-                noise = torch.randn((B, d["out.noise"].shape[1], d["out.noise"].shape[2]),
-                                    generator=g).to(dev, torch.bfloat16)
-                train_step(model, batch, RectifiedFlowScheduler(), model.patchifier, tc,
-                           d["in.prompt_embeds"].to(dev), d["in.prompt_attention_mask"].to(dev),
+                noise = torch.randn((B, F_ * H_ * W_, C), generator=g).to(dev, torch.bfloat16)
+                train_step(model, batch, RectifiedFlowScheduler(), model.patchifier, tc, prompt, pmask,
                            t=t, noise=noise)
             if red is not None:
-                n_launched = red._launched
+                if mode == "overlap":
+                    res["launched_in_backward"] = red._launched
                 red()
+                res[mode + "_buckets"] = [(str(b["dtype"]), b["n"]) for b in red.buckets]
+                red.uninstall()
             torch.cuda.synchronize()
             res[mode] = {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()
                          if p.requires_grad}
-            if red is not None:
-                res[mode + "_buckets"] = len(red.buckets)
+            del model, red, trainable
+            torch.cuda.empty_cache()
         torch.save(res, os.path.join(out_dir, f"g{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
 
-def test_dp_overlapped_allreduce_on_the_tiny_model_two_ranks():
+def _check(kind):
     world = 2
     with tempfile.TemporaryDirectory() as td:
-        mp.start_processes(_worker, args=(world, _port(), td), nprocs=world, start_method="spawn",
+        mp.start_processes(_worker, args=(world, _port(), td, kind), nprocs=world, start_method="spawn",
                            join=True)
         res = [torch.load(os.path.join(td, f"g{r}.pt"), weights_only=True) for r in range(world)]
-    assert res[0]["overlap_buckets"] > 2
+    assert len(res[0]["overlap_buckets"]) > 2
+    assert res[0]["launched_in_backward"] >= 1, "buckets launch while the backward still runs"
     for r in range(world):
         for n, g in res[r]["overlap"].items():
             assert torch.equal(g, res[r]["posthoc"][n]), n
@@ -92,3 +142,29 @@ def test_dp_overlapped_allreduce_on_the_tiny_model_two_ranks():
         exp = ((res[0]["local"][n].float() + res[1]["local"][n].float()) / world).to(res[0]["local"][n].dtype)
         assert torch.equal(res[0]["overlap"][n], exp), n
         assert torch.equal(res[1]["overlap"][n], exp), n
+    return res
+
+
+def test_dp_overlapped_allreduce_on_the_tiny_model_two_ranks():
+    _check("lora")
+
+
+def test_dp_overlapped_allreduce_full_mode_two_ranks():
+    """train_mode='full' (tiny golden config): every block's scale_shift_table gets its gradient
+    from autograd after the block's backward hook; the armed reduction must still equal the
+    post-hoc one bitwise (its bucket launches from its post-accumulate-grad hook)."""
+    res = _check("full")
+    assert any("scale_shift_table" in n for n in res[0]["overlap"])
+
+
+def test_dp_overlapped_allreduce_ltx2b_28_layers_real_buckets():
+    """Config A8's reduction at its real gradient sizes: the 28-layer LTX-2B LoRA model (7.34 M f32
+    adapter params = 29.4 MB, 12.59 M bf16 caption params reduced through f32 staging = 50.3 MB) in
+    ~25 MB buckets, the block buckets launched from the backward hooks; bitwise the post-hoc
+    reduction and the f32 mean of the two ranks' grads."""
+    res = _check("ltx28")
+    bks = res[0]["overlap_buckets"]
+    n32 = sum(n for dt, n in bks if dt == "torch.float32")
+    n16 = sum(n for dt, n in bks if dt == "torch.bfloat16")
+    assert n32 == 7_340_032 and n16 == 12_587_008, (n32, n16)
+    assert len(bks) >= 4 and all(n * 4 <= 26e6 + 4 * 2048 * 4096 for _, n in bks), bks

@@ -11,7 +11,7 @@ import torch
 from safetensors.torch import load_file
 
 import ltx_oracle as O
-from model_utils import grads_by_canonical, rel
+from model_utils import grads_by_canonical, loss_crit, rel
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -61,8 +61,7 @@ def test_full_mode_grads_match_reference():
     params = O.make_params(cfg, meta["param_seed"], lora_rank=0, requires_grad=False)
     model = _build_full(cfg, params)
     assert sorted(grads_by_canonical(model)) == meta["trainable"]
-    loss, _, _, _ = _run(model, d)
-    assert abs(float(loss) - float(d["out.loss"])) <= 1e-2 * abs(float(d["out.loss"]))
+    loss, _, _, ld = _run(model, d)
     g = grads_by_canonical(model)
     # fp32 oracle on the device: the yardstick of the reference's own bf16 noise
     q = {k: v.to(DEV).float().requires_grad_(any(s in k for s in FULL_KEYS))
@@ -73,6 +72,12 @@ def test_full_mode_grads_match_reference():
                      c(d["in.prompt_attention_mask"]), t=c(d["out.t"]),
                      noise=c(d["out.noise"]).float())
     r["loss"].backward()
+    # loss: the f32 mse vs the fp32 oracle, the reference's bf16 output as the noise yardstick
+    # (the golden holds no v_target: v = noise - x0 in f32, rounded to bf16 as training.py:146 does)
+    l16 = float(((d["out.sample"].to(DEV).float() - r["v_target"].detach().bfloat16().float()) ** 2).mean())
+    l32 = float(((r["sample"].float() - r["v_target"].float()) ** 2).mean())
+    loss_crit("tiny full loss", ld["_mse_f32"], l16, l32)
+    assert abs(float(loss) - float(d["out.loss"])) <= 2 ** -7 * abs(float(d["out.loss"]))
     worst = []
     for k, v in d.items():
         if not k.startswith("grad."):
@@ -133,44 +138,50 @@ def test_zero2_kernels_match_torch_math():
 
 def test_full_mode_zero2_loss_curve():
     """5 optimizer steps of the full-mode tiny model with Zero2AdamW (world 1) vs the oracle +
-    clip_grad_norm_(1.0) + torch AdamW on the same t / noise streams."""
+    clip_grad_norm_(1.0) + torch AdamW on the same t / noise streams (bf16 weights on an f32
+    master and an all-fp32 trajectory; SURVEY 8c-4 loss criterion per step)."""
     from ltx_amd.zero import Zero2AdamW
     d, meta = _load()
     cfg = meta["config"]
     params = O.make_params(cfg, meta["param_seed"], lora_rank=0, requires_grad=False)
     model = _build_full(cfg, params)
-    opt = Zero2AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3)
-    q = {k: v.to(DEV).requires_grad_(any(s in k for s in FULL_KEYS)) for k, v in params.items()}
-    qt = [v for v in q.values() if v.requires_grad]
-    qm = [v.detach().float().clone().requires_grad_(True) for v in qt]  # f32 master (bf16 config)
-    ref = torch.optim.AdamW(qm, lr=1e-3, foreach=False)
+    # lr 1e-4: train-avatars.yaml's learning_rate (the trajectories stay within the per-step noise
+    # criterion; at 10x the configured lr a bf16 trajectory drifts past 1e-3 by step 2 by itself)
+    opt = Zero2AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    refs = {}  # bf16 weights + f32 master (the bf16 config), and an all-fp32 trajectory
+    for dt in (torch.bfloat16, torch.float32):
+        q = {k: v.to(DEV).to(dt).requires_grad_(any(s in k for s in FULL_KEYS)) for k, v in params.items()}
+        qt = [v for v in q.values() if v.requires_grad]
+        qm = [v.detach().float().clone().requires_grad_(True) for v in qt]
+        refs[dt] = (q, qt, qm, torch.optim.AdamW(qm, lr=1e-4, foreach=False))
     g = torch.Generator(device=DEV).manual_seed(11)
     lat = d["in.latents"]
     B, C = lat.shape[:2]
     N = lat[0, 0].numel()
-    ours, refs = [], []
+    ours, curves = [], {torch.bfloat16: [], torch.float32: []}
     c = lambda x: x.to(DEV)  # noqa: E731
     for _ in range(5):
         t = torch.rand(B, generator=g, device=DEV) * 0.9 + 0.05
         noise = torch.randn(B, N, C, generator=g, device=DEV).bfloat16()
         dd = dict(d)
         dd["out.t"], dd["out.noise"] = t, noise
-        loss, _, _, _ = _run(model, dd)
+        _, _, _, ld = _run(model, dd)
         opt.step()
         opt.zero_grad()
-        r = O.train_step(q, cfg, c(d["in.latents"]), c(d["in.ref_image_latents"]),
-                         c(d["in.pose_latents"]), c(d["in.prompt_embeds"]),
-                         c(d["in.prompt_attention_mask"]), t=t, noise=noise)
-        r["loss"].backward()
-        for v, m in zip(qt, qm):
-            m.grad = v.grad.float()
-            v.grad = None
-        torch.nn.utils.clip_grad_norm_(qm, 1.0)
-        ref.step()
-        with torch.no_grad():
+        for dt, (q, qt, qm, ref) in refs.items():
+            r = O.train_step(q, cfg, c(d["in.latents"]), c(d["in.ref_image_latents"]),
+                             c(d["in.pose_latents"]), c(d["in.prompt_embeds"]),
+                             c(d["in.prompt_attention_mask"]), t=t, noise=noise.to(dt))
+            r["loss"].backward()
             for v, m in zip(qt, qm):
-                v.copy_(m)
-        ours.append(float(loss))
-        refs.append(float(r["loss"]))
-    for i, (a, b) in enumerate(zip(ours, refs)):
-        assert abs(a - b) <= 3e-2 * abs(b), (i, ours, refs)
+                m.grad = v.grad.float()
+                v.grad = None
+            torch.nn.utils.clip_grad_norm_(qm, 1.0)
+            ref.step()
+            with torch.no_grad():
+                for v, m in zip(qt, qm):
+                    v.copy_(m.to(dt))
+            curves[dt].append(float(((r["sample"].float() - r["v_target"].float()) ** 2).mean()))
+        ours.append(float(ld["_mse_f32"]))
+    for i, a in enumerate(ours):
+        loss_crit(f"full curve step {i}", a, curves[torch.bfloat16][i], curves[torch.float32][i])

@@ -280,66 +280,89 @@ def test_grad_allreduce_gloo_world2():
 
 
 class _FakeBlockFn(torch.autograd.Function):
-    """y = x . W with W's grad written straight into .grad and the block's ready hooks called at
-    the end of backward: the contract of transformer3d._BlockFn for the LoRA adapters."""
+    """y = (x + mods) . W with W (under blk.attn2, as the LoRA adapters / attention weights sit in
+    the real block) written straight into .grad and the block's ready hooks called at the end of
+    backward: the contract of transformer3d._BlockFn. mods stands for the AdaLN modulation rows
+    (scale_shift_table + tmod through _AdaModFn): its gradient is RETURNED, so the table's .grad
+    is accumulated by autograd after the hooks have fired."""
 
     @staticmethod
-    def forward(ctx, blk, x):
+    def forward(ctx, blk, x, mods):
         ctx.blk = blk
-        ctx.save_for_backward(x)
-        return x @ blk.w
+        xm = x + mods
+        ctx.save_for_backward(xm)
+        return xm @ blk.attn2.w
 
     @staticmethod
     def backward(ctx, dy):
-        (x,) = ctx.saved_tensors
+        (xm,) = ctx.saved_tensors
         blk = ctx.blk
+        w = blk.attn2.w
         with torch.no_grad():
-            if blk.w.grad is None:
-                blk.w.grad = torch.zeros_like(blk.w)
-            blk.w.grad.add_(x.t() @ dy)
+            if w.grad is None:
+                w.grad = torch.zeros_like(w)
+            w.grad.add_(xm.t() @ dy)
         for cb in getattr(blk, "_grad_ready_hooks", ()):
             cb(blk)
-        return None, dy @ blk.w.t()
+        dx = dy @ w.t()
+        return None, dx, dx.sum(0, keepdim=True)
 
 
 class _FakeModel(torch.nn.Module):
-    """caption (bf16, autograd-accumulated) -> 3 blocks (f32 grads written by the 'kernel')."""
+    """caption (bf16, autograd-accumulated) -> 3 blocks (f32 grads written by the 'kernel');
+    full=True also trains each block's scale_shift_table (autograd-accumulated, like
+    train_mode='full')."""
 
-    def __init__(self):
+    def __init__(self, full=False):
         super().__init__()
         g = torch.Generator().manual_seed(3)
         self.cap = torch.nn.Parameter(torch.randn(8, 8, generator=g).to(torch.bfloat16))
         self.transformer_blocks = torch.nn.ModuleList()
         for _ in range(3):
             b = torch.nn.Module()
-            b.w = torch.nn.Parameter(torch.randn(8, 8, generator=g) * 0.3)
+            b.attn2 = torch.nn.Module()
+            b.attn2.w = torch.nn.Parameter(torch.randn(8, 8, generator=g) * 0.3)
+            b.scale_shift_table = torch.nn.Parameter(torch.randn(1, 8, generator=g) * 0.1,
+                                                     requires_grad=full)
             self.transformer_blocks.append(b)
 
     def forward(self, x):
         h = (x.to(torch.bfloat16) @ self.cap).float()
         for b in self.transformer_blocks:
-            h = _FakeBlockFn.apply(b, h)
+            h = _FakeBlockFn.apply(b, h, b.scale_shift_table * 1.0)
         return h
 
     def grad_ready_order(self):
-        return [b.w for b in reversed(self.transformer_blocks)] + [self.cap]
+        order = []
+        for b in reversed(self.transformer_blocks):
+            order += [p for p in b.parameters() if p.requires_grad]
+        return order + [self.cap]
 
 
-def _dp_overlap_worker(rank, world, port, out_dir):
+def _dp_overlap_worker(rank, world, port, out_dir, full):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from ltx_amd.training import GradAllReduce
         res = {}
         for mode in ("overlap", "posthoc"):
-            m = _FakeModel()
-            params = [p for p in m.parameters()]
+            m = _FakeModel(full)
+            params = [p for p in m.parameters() if p.requires_grad]
             launched_at_cap, box = [], []
             # registered first: runs before the reducer's own hook on the caption grad
             m.cap.register_post_accumulate_grad_hook(lambda p: launched_at_cap.append(box[0]._launched))
-            red = GradAllReduce(params, bucket_mb=1e-4, order=m.grad_ready_order()).install(m)
+            # a stale reducer installed and removed first: its hooks must be gone
+            GradAllReduce(params, bucket_mb=1e-5, order=m.grad_ready_order()).install(m).uninstall()
+            snaps = {}
+
+            class Rec(GradAllReduce):  # the bucket contents at the moment its all-reduce launches
+                def _launch(self, bi):
+                    snaps[bi] = self.buckets[bi]["flat"].clone()
+                    super()._launch(bi)
+            red = Rec(params, bucket_mb=1e-5, order=m.grad_ready_order()).install(m)
             box.append(red)
-            assert len(red.buckets) == 4  # one param each: blocks 2, 1, 0, caption
+            assert all(len(b.__dict__.get("_grad_ready_hooks", [])) == 1 for b in m.transformer_blocks)
+            assert len(red.buckets) == len(params)  # one param each
             red.zero_grad()
             g = torch.Generator().manual_seed(100 + rank)
             for step in range(3):  # three micro-steps, the last one armed
@@ -354,29 +377,42 @@ def _dp_overlap_worker(rank, world, port, out_dir):
                                       for p in params),
                          "launched_at_cap": launched_at_cap[-1]}
             # local (unreduced) grads of this rank for the expected average
-            m2 = _FakeModel()
+            m2 = _FakeModel(full)
             g = torch.Generator().manual_seed(100 + rank)
             for step in range(3):
                 m2(torch.randn(4, 8, generator=g)).square().sum().backward()
-            res[mode]["local"] = [p.grad.clone() for p in m2.parameters()]
+            res[mode]["local"] = [p.grad.clone() for p in m2.parameters() if p.requires_grad]
+            # every bucket launched holding this rank's complete local gradient
+            local = {id(q): g2 for q, g2 in zip(params, res[mode]["local"])}
+            res[mode]["complete_at_launch"] = all(
+                torch.equal(snaps[bi], torch.cat([local[id(q)].reshape(-1) for q in b["params"]]))
+                for bi, b in enumerate(red.buckets))
         torch.save(res, os.path.join(out_dir, f"o{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
 
-def test_grad_allreduce_overlapped_with_backward_gloo_world2():
+@pytest.mark.parametrize("full", [False, True], ids=["lora", "full"])
+def test_grad_allreduce_overlapped_with_backward_gloo_world2(full):
     """GradAllReduce armed for the last micro-step launches the block buckets from the blocks'
     backward hooks (before the caption grad exists) and ends bitwise equal to the post-backward
-    reduction, equal to the f32 mean of the ranks' grads, with .grad kept as bucket views."""
+    reduction, equal to the f32 mean of the ranks' grads, with .grad kept as bucket views.
+    full: each block's scale_shift_table gets its gradient from autograd AFTER the block's hook
+    has fired; it must report through its post-accumulate-grad hook, not the block hook, or its
+    bucket reduces without the last micro-step's term."""
     world = 2
     with tempfile.TemporaryDirectory() as td:
-        mp.start_processes(_dp_overlap_worker, args=(world, _free_port(), td), nprocs=world,
+        mp.start_processes(_dp_overlap_worker, args=(world, _free_port(), td, full), nprocs=world,
                            start_method="spawn", join=True)
         res = [torch.load(os.path.join(td, f"o{r}.pt"), weights_only=True) for r in range(world)]
     for r in range(world):
         ov, ph = res[r]["overlap"], res[r]["posthoc"]
-        assert ov["launched_at_cap"] == 3, "the three block buckets launch during the backward"
+        if not full:
+            assert ov["launched_at_cap"] == 3, "the three block buckets launch during the backward"
+        else:
+            assert ov["launched_at_cap"] >= 1, "block buckets launch during the backward"
         assert ph["launched_at_cap"] == 0
+        assert ov["complete_at_launch"] and ph["complete_at_launch"]
         assert ov["views"] and ph["views"]
         for a, b in zip(ov["grads"], ph["grads"]):
             assert torch.equal(a, b)

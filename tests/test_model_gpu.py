@@ -3,7 +3,8 @@
   (2) the pinned oracle (oracle/ltx_oracle.py) run on the GPU in bf16 and fp32.
 Criterion (the reference's own bf16 noise as the yardstick):
   err(build_bf16, ref_fp32) <= 1.25 * err(ref_bf16, ref_fp32) + slack, rel-Frobenius,
-for out.sample and for every trainable gradient; loss scalar within 1e-2 relative (bf16 scalar).
+for out.sample and for every trainable gradient; the loss (the f32 mean before the bf16 scalar
+rounding) within max(1e-3, 1.25 x the reference's own bf16 distance) of the fp32 oracle.
 """
 import json
 import os
@@ -13,7 +14,7 @@ import torch
 from safetensors.torch import load_file
 
 import ltx_oracle as O
-from model_utils import build_model, grads_by_canonical, rel
+from model_utils import build_model, grads_by_canonical, loss_crit, rel
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -46,13 +47,18 @@ def _build_run(model, d, cfg):
     from ltx_amd.training import train_step
     tc = TrainConfig(checkpoint_path="-", gradient_accumulation_steps=1)
     cast = lambda x: x.to(DEV)
-    loss, rel_mse, nrmse, _ = train_step(
+    loss, rel_mse, nrmse, ld = train_step(
         model, {"latents": cast(d["in.latents"]), "ref_image_latents": cast(d["in.ref_image_latents"]),
                 "pose_latents": cast(d["in.pose_latents"])},
         RectifiedFlowScheduler(), model.patchifier, tc, cast(d["in.prompt_embeds"]),
         cast(d["in.prompt_attention_mask"]), t=d["out.t"].to(DEV),
         noise=d["out.noise"].to(DEV).to(torch.bfloat16))
-    return loss, rel_mse, nrmse
+    return loss, rel_mse, nrmse, float(ld["_mse_f32"])
+
+
+def _mse32(r):
+    """f32 mean of (sample - v_target)^2 of an oracle / reference run (training.py:159)."""
+    return float(((r["sample"].float() - r["v_target"].float()) ** 2).mean())
 
 
 def _forward_sample(model, d):
@@ -71,6 +77,7 @@ def _check_noise_criterion(name, build, ref16, ref32, factor=1.25, slack=2e-3):
     e_b = rel(build, ref32)
     e_r = rel(ref16, ref32)
     assert e_b <= factor * e_r + slack, f"{name}: build err {e_b:.3e} vs reference bf16 noise {e_r:.3e}"
+    return e_b, e_r
 
 
 def test_tiny_model_matches_reference_goldens():
@@ -83,12 +90,15 @@ def test_tiny_model_matches_reference_goldens():
     s16, s32 = d["out.sample"].to(DEV), d["out.sample_fp32"].to(DEV)
     _check_noise_criterion("tiny sample", out, s16, s32)
     # full train step (loss + backward) vs the reference's loss and grads
-    loss, rel_mse, nrmse = _build_run(model, d, cfg)
-    assert abs(float(loss) - float(d["out.loss"])) <= 1e-2 * abs(float(d["out.loss"]))
-    assert abs(float(rel_mse) - float(d["out.rel_mse"])) <= 2e-2 * abs(float(d["out.rel_mse"]))
+    loss, rel_mse, nrmse, lb = _build_run(model, d, cfg)
     g = grads_by_canonical(model)
     p32 = {k: v for k, v in params.items()}
-    _, gref32 = _oracle_run(p32, cfg, d, torch.float32)
+    r32, gref32 = _oracle_run(p32, cfg, d, torch.float32)
+    # the reference's own bf16 step: its loss as the f32 mean of its bf16 output
+    l16 = float(((d["out.sample"].float() - d["out.v_target"].float()) ** 2).mean())
+    loss_crit("tiny loss", lb, l16, _mse32(r32))
+    assert abs(float(loss) - float(d["out.loss"])) <= 2 ** -7 * abs(float(d["out.loss"]))  # bf16 scalar
+    assert abs(float(rel_mse) - float(d["out.rel_mse"])) <= 2e-2 * abs(float(d["out.rel_mse"]))
     for k, v in d.items():
         if k.startswith("grad."):
             name = k[5:]
@@ -160,8 +170,9 @@ def test_block2b_matches_reference_goldens():
     out = _forward_sample(model, d)
     r32, g32 = _oracle_run(params, cfg, d, torch.float32)
     _check_noise_criterion("2b sample", out, d["out.sample"].to(DEV), r32["sample"])
-    loss, _, _ = _build_run(model, d, cfg)
-    assert abs(float(loss) - float(d["out.loss"])) <= 1e-2 * abs(float(d["out.loss"]))
+    loss, _, _, lb = _build_run(model, d, cfg)
+    l16 = float(((d["out.sample"].float() - d["out.v_target"].float()) ** 2).mean())
+    loss_crit("2b block loss", lb, l16, _mse32(r32))
     g = grads_by_canonical(model)
     for k, v in d.items():
         if k.startswith("grad."):
@@ -197,14 +208,16 @@ def test_ltx2b_full_depth_vs_oracle():
     r32, g32 = _oracle_run(params, cfg, d, torch.float32)
     r16, g16 = _oracle_run(params, cfg, d, torch.bfloat16)
     _check_noise_criterion("2b28 sample", out, r16["sample"], r32["sample"])
-    loss, _, _ = _build_run(model, d, cfg)
-    assert abs(float(loss) - float(r16["loss"])) <= 1e-2 * abs(float(r16["loss"]))
+    loss, _, _, lb = _build_run(model, d, cfg)
+    loss_crit("2b28 loss", lb, _mse32(r16), _mse32(r32))
     g = grads_by_canonical(model)
-    for name in ("transformer_blocks.27.attn2.to_out.0.lora_B.default.weight",
-                 "transformer_blocks.0.attn2.to_q.lora_A.default.weight",
-                 "transformer_blocks.13.attn2.to_v.lora_B.default.weight",
-                 "caption_projection.linear_1.weight", "caption_projection.linear_2.bias"):
-        _check_noise_criterion(name, g[name], g16[name], g32[name], slack=5e-3)
+    # every trainable tensor: 28 blocks x 4 attn2 targets x (lora_A, lora_B) + caption_projection (4)
+    assert len(g) == len(g32) == 28 * 4 * 2 + 4, (len(g), len(g32))
+    worst = []
+    for name in sorted(g32):
+        e_b, e_r = _check_noise_criterion(name, g[name], g16[name], g32[name], slack=5e-3)
+        worst.append((e_b - 1.25 * e_r, name))
+    print("worst margins:", sorted(worst, reverse=True)[:4])
 
 
 from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG as O_CFG  # noqa: E402

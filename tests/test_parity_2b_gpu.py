@@ -214,3 +214,43 @@ def test_text_stack_matches_per_block():
     for name in g0:
         e = rel(g1[name].float(), g0[name].float())
         assert e <= 1e-2, f"{name}: batched vs per-block {e:.3e}"
+
+
+def test_frozen_caption_projection_keeps_text_adapter_grads():
+    """LoRA on attn2 with caption_projection FROZEN: enc2 then carries no grad, so the
+    batched text side -- whose backward runs as enc2's -- must not be used; the per-block path
+    computes every to_k / to_v adapter gradient. They must equal (to rounding) the grads of the
+    same step with a trainable caption projection (batched text side), and match the oracle."""
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    from model_utils import oracle_step
+    cfg = dict(OURS_TRANSFORMER_CONFIG, num_layers=2)
+    params = O.make_params(cfg, 53, lora_rank=16, requires_grad=False)
+    d = _inputs(8, 7, 16, 16, 256, 16, seed=19)
+    res = {}
+    for frozen in (False, True):
+        model = build_model(cfg, params, 16, device=DEV)
+        if frozen:
+            for p in model.caption_projection.parameters():
+                p.requires_grad_(False)
+        _build_step(model, d)
+        res[frozen] = grads_by_canonical(model)
+    g_tr, g_fr = res[False], res[True]
+    lora_names = [n for n in g_tr if "lora_" in n]
+    assert sorted(n for n in g_fr) == sorted(lora_names)
+    for n in lora_names:
+        assert g_fr[n] is not None and float(g_fr[n].abs().max()) > 0, n
+        assert rel(g_fr[n].float(), g_tr[n].float()) <= 1e-2, n
+    _, g32, _ = oracle_step(params, cfg, d, torch.float32, lambda k: "lora_" in k)
+    _, g16, _ = oracle_step(params, cfg, d, torch.bfloat16, lambda k: "lora_" in k)
+    for n in lora_names:
+        _crit(f"frozen-caption {n}", g_fr[n], g16[n], g32[n], slack=5e-3)
+
+
+def test_four_blocks_config_x_grads():
+    """Config X gradients over depth: 4 LTX-2B blocks at latent 13x24x24 (N = 7488), B = 1,
+    256 text tokens (16 valid): out.sample, loss and every LoRA / caption-projection gradient."""
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    cfg = dict(OURS_TRANSFORMER_CONFIG, num_layers=4)
+    params = O.make_params(cfg, 59, lora_rank=16, requires_grad=False)
+    d = _inputs(1, 13, 24, 24, 256, 16, seed=23)
+    _compare_model("X 4-block", cfg, params, d)

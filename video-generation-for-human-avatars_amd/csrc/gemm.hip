@@ -255,42 +255,17 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const GemmParams p
 // (k-half, n-half) with the next quarter's fragments prefetched, one barrier per K-tile.
 // X pieces (8 rows x 128 B) go to waves 4w..4w+3 (for BMT = 224 wave 7 moves only W pieces).
 // ---------------------------------------------------------------------------------------------
-// STAMP (diagnostic build only, ltx_gemm_set_variant 19 + ltx_gemm_set_stamps): thread 0 of every
-// workgroup writes s_memrealtime (100 MHz) at start / after the prologue wait / after the main
-// loop / after the epilogue image barrier / at the end, plus HW_ID and XCC_ID, into a buffer of
-// its own (8 u64 per workgroup); no output value depends on them.
-static __device__ __forceinline__ uint64_t rt_stamp() { return __builtin_amdgcn_s_memrealtime(); }
-
-// NW = 4: four waves (one per SIMD, 256 threads), each a 128 x 128 (BMT 256) or 112 x 128 (BMT 224)
-// piece with 256 / 224 accumulator registers (hipBLASLt's MT256x256x64 geometry on gfx950): a third
-// less LDS fragment traffic per MFMA. Measured with this schedule (2 stages, one barrier per
-// K-tile): bit-identical results but 10-25 % slower than NW = 8 on every training shape -- at one
-// wave per SIMD nothing covers the mid-tile DMA wait. Not dispatched; kept for the next schedule.
-// XR3: the X operand (activations, streamed from HBM / Infinity Cache) in a ring of THREE tiles
-// and W in a ring of two ([X0 X1 X2 | W0 W1]: 160 KiB at BMT 256, 148 KiB at 224). Tile t+2's X
-// pieces go out at the start of tile t (its buffer held tile t-1, free since tile t-1's mid-tile
-// barrier), its W pieces right after tile t's mid-tile barrier; that barrier then waits only for
-// tile t+1 and leaves tile t+2's X in flight: X gets 1.75 K-tiles to land, W a whole one (the
-// two-stage schedule gives them one and 0.75).
-template <int BMT, int XR3>
-constexpr int lds_t_bytes() {
-  return XR3 ? 3 * BMT * BK * 2 + 2 * WT2 : LDS2;
-}
-
-template <int EPI, int R, int BMT, int DMAW, int STAMP = 0, int SPLIT = 0, int NW = 8, int XR3 = 0>
-__global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams p) {
+template <int EPI, int R, int BMT, int DMAW, int SPLIT = 0>
+__global__ __launch_bounds__(512, 1) void gemm_nt_kernel_t(const GemmParams p) {
   static_assert(BMT == 256 || BMT == 224, "tile height");
-  static_assert(NW == 8 || NW == 4, "waves");
-  static_assert(DMAW <= NW, "DMA waves");
-  constexpr int NT = NW * 64;
-  uint64_t st0 = 0, st1 = 0, st2 = 0, st3 = 0;
-  if constexpr (STAMP) st0 = rt_stamp();
-  constexpr int WMW = (NW == 4) ? 2 : ((BMT == 256) ? 4 : 2);  // waves along m
+  static_assert(DMAW <= 8, "DMA waves");
+  constexpr int NW = 8, NT = NW * 64;
+  constexpr int WMW = (BMT == 256) ? 4 : 2;  // waves along m
   constexpr int WNW = NW / WMW;               // waves along n
-  constexpr int WTM = BMT / WMW;              // 64 | 112 | 128
-  constexpr int WTN = BN2 / WNW;              // 128 | 64 | 128
-  constexpr int MF = WTM / 16;                // 4 | 7 | 8
-  constexpr int NF = WTN / 16;                // 8 | 4 | 8
+  constexpr int WTM = BMT / WMW;              // 64 | 112
+  constexpr int WTN = BN2 / WNW;              // 128 | 64
+  constexpr int MF = WTM / 16;                // 4 | 7
+  constexpr int NF = WTN / 16;                // 8 | 4
   constexpr int NFH = NF / 2;                 // n-fragments per quarter
   constexpr int XPIECES = BMT / 8;            // 32 | 28
   constexpr int XT = BMT * BK * 2;            // X tile bytes
@@ -389,8 +364,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   };
   const bool dma_batch = p.dma_batch != 0;
   // LDS byte offsets of X / W buffer `buf`
-  auto xaddr = [&](int buf) -> int { return XR3 ? buf * XT : buf * ST; };
-  auto waddr = [&](int buf) -> int { return XR3 ? 3 * XT + buf * WT2 : buf * ST + XT; };
+  auto xaddr = [&](int buf) -> int { return buf * ST; };
+  auto waddr = [&](int buf) -> int { return buf * ST + XT; };
   auto stage_x = [&](int st, int kt) {
     if (kt == nk_main && nk_main > 0) set_x(true);  // ext tiles come last, in issue order
     const char* sb = xb + (kt < nk_main ? kt : kt - nk_main) * (BK * 2);
@@ -453,7 +428,6 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   } else {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  if constexpr (STAMP) st1 = rt_stamp();
   s16x8 aE[NFH], aO[NFH], b0[MF], b1[MF];  // A even/odd quarter sets, B per k-half
 #pragma unroll
   for (int i = 0; i < NFH; ++i) aE[i] = *(const s16x8*)(smem + waddr(0) + aoff[0][i]);
@@ -465,20 +439,17 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
   _Pragma("unroll") for (int j = 0; j < MF; ++j)                                                      \
     acc[(NH) * NFH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AS[i], BS[j], acc[(NH) * NFH + i][j], 0, 0, 0); \
   __builtin_amdgcn_sched_barrier(0);
-  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 
-  int cur = 0;           // two-stage schedule: tile kt's stage; XR3: tile kt's W buffer
-  int xcur = 0;          // XR3: tile kt's X buffer (kt % 3)
-  bool pend_w = false;   // two-stage: W half of tile kt+1's DMA still to issue in Q0
+  int cur = 0;           // tile kt's stage
+  bool pend_w = false;   // W half of tile kt+1's DMA still to issue in Q0
   for (int kt = 0; kt < nk; ++kt) {
-    const char* xs = smem + (XR3 ? xaddr(xcur) : xaddr(cur));
+    const char* xs = smem + xaddr(cur);
     const char* ws = smem + waddr(cur);
     // Q0 (h0, n0): prefetch A(Q1)
 #pragma unroll
     for (int i = 0; i < NFH; ++i) aO[i] = *(const s16x8*)(ws + aoff[1][i]);
-    if constexpr (XR3) {
-      if (kt + 2 < nk) stage_x(xcur == 0 ? 2 : xcur - 1, kt + 2);  // tile kt-1's X buffer
-    } else if (pend_w) {
+    if (pend_w) {
       stage_w(cur ^ 1, kt + 1);
       pend_w = false;
     }
@@ -495,23 +466,12 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     LTX_MFMA_T(aE, b1, 0)
     // all reads of tile t issued: wait tile t+1, free tile t's stage, DMA tile t+2's X into it
     if (kt + 1 < nk) {
-      if constexpr (XR3) {
-        // tile t+1 landed; tile t+2's X (this wave's youngest xp pieces) may stay in flight
-        if (kt + 2 < nk && xp == 8)
-          asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else if (kt + 2 < nk && xp == 4)
-          asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (kt + 2 < nk) stage_w(cur, kt + 2);  // tile t's W buffer
-      } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (kt + 2 < nk) {
-          stage_x(cur, kt + 2);
-          pend_w = true;
-        }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (kt + 2 < nk) {
+        stage_x(cur, kt + 2);
+        pend_w = true;
       }
-      const char* xn = smem + (XR3 ? xaddr(xcur == 2 ? 0 : xcur + 1) : xaddr(cur ^ 1));
+      const char* xn = smem + xaddr(cur ^ 1);
       const char* wn_ = smem + waddr(cur ^ 1);
       // Q3 (h1, n1) of tile t: prefetch A(Q0), B(h0) of tile t+1
 #pragma unroll
@@ -521,11 +481,9 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     }
     LTX_MFMA_T(aO, b1, 1)
     cur ^= 1;
-    xcur = xcur == 2 ? 0 : xcur + 1;
   }
 #undef LTX_MFMA_T
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if constexpr (STAMP) st2 = rt_stamp();
   if constexpr (SPLIT) {  // raw f32 partial: lane holds 4 consecutive n of one m (16-B stores)
     float* part = p.ws + (int64_t)split * p.M * p.N;
 #pragma unroll
@@ -595,22 +553,11 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_nt_kernel_t(const GemmParams 
     for (int u = 0; u < NPASS; ++u)  // clamped: every load is in bounds, rows past M are not stored
       epi_load<EPI>(p, min(m0 + (tid >> 5) + u * RPP, p.M - 1), min(n0 + cgrp * 8, p.N - 8), ax[u]);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // C image complete
-    if constexpr (STAMP) st3 = rt_stamp();
 #pragma unroll
     for (int u = 0; u < NPASS; ++u) row_out((tid >> 5) + u * RPP, &ax[u]);
   } else {
     __syncthreads();
-    if constexpr (STAMP) st3 = rt_stamp();
     for (int rr = tid >> 5; rr < BMT; rr += RPP) row_out(rr, nullptr);
-  }
-  if constexpr (STAMP) {
-    if (tid == 0) {
-      uint64_t* o = (uint64_t*)p.ws + (int64_t)blockIdx.x * 8;
-      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = rt_stamp();
-      o[5] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
-      o[6] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-      o[7] = (uint64_t)(tm * 65536 + tn);
-    }
   }
 }
 
@@ -637,8 +584,9 @@ static SplitWs ws_for(hipStream_t s) {
   return it != g_ws_stream.end() ? it->second : g_ws_default;
 }
 // tuning knob (ltx_gemm_set_variant, or LTX_GEMM_VARIANT at load for whole-step A/B runs): 0 default,
-// 13 / 14 t-kernel with 256 / 224-row tiles, 30-32 w4 kernel, 40-42 ns kernel, 50 XR3 schedule,
-// 60 / 61 / 62 tw kernel (auto / 256 / 224-row tiles)
+// 13 / 14 large-tile kernel forced to 256 / 224-row tiles. (The not-adopted schedules -- one wave
+// per SIMD, 4-slot ring, three-tile X ring, persistent four-wave kernel -- live in
+// tools/experiments/ and are not part of the library.)
 static int g_variant = [] {
   const char* e = getenv("LTX_GEMM_VARIANT");
   return e ? atoi(e) : 0;
@@ -657,13 +605,12 @@ static int g_epi_batch = [] {
 
 // The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can
 // attribute its per-launch timings to the kernel rocprof will name).
-enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_W4 = 2, PATH_SMALL = 3, PATH_NS = 4, PATH_TW = 5 };
+enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_SMALL = 3 };
 struct GemmPlan {
   GemmPath path;
-  int bmt;     // PATH_T / PATH_W4: tile height (256 or 224)
+  int bmt;     // PATH_T: tile height (256 or 224)
   int splitk;  // PATH_SPLIT_T / PATH_SMALL: K slices (1 = none)
   int nst;     // PATH_SMALL: LDS stages
-  int xr3 = 0; // PATH_T: three-tile X ring (gemm_nt_kernel_t XR3)
 };
 
 static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
@@ -697,24 +644,9 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
     const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
     // fraction of the last round of 256 CUs that has work, per tile height
     auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
-    if (g_variant >= 33 && g_variant <= 36) return GemmPlan{PATH_W4, 32 - g_variant, 1, 2};  // measurement
-    if (g_variant >= 40 && g_variant <= 42) {  // 4-slot ring of 32-deep steps: 40 auto, 41 BMT 256, 42 BMT 224
-      const bool use224 = g_variant == 42 || (g_variant == 40 && fill(t224) > fill(t256) + 0.02);
-      return GemmPlan{PATH_NS, use224 ? 224 : 256, 1, 2};
-    }
-    if (g_variant >= 30 && g_variant <= 32) {  // one-wave-per-SIMD kernel: 30 auto, 31 BMT 256, 32 BMT 224
-      const bool use224 = g_variant == 32 || (g_variant == 30 && fill(t224) > fill(t256) + 0.02);
-      return GemmPlan{PATH_W4, use224 ? 224 : 256, 1, 2};
-    }
     // the tile height that fills the last round best; variant 13 forces BMT 256, 14 forces 224
     const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
-    // four-wave kernel (gemm_tw.hip) on tile-aligned shapes: variant 60 (auto), 61 (256), 62 (224)
-    if (g_variant >= 60 && g_variant <= 62 && p.N % BN2 == 0 && R == 0 && tw_supports(epi) &&
-        (p.K / BK + p.K2 / BK) % 2 == 0) {
-      const bool tw224 = g_variant == 62 || (g_variant == 60 && use224);
-      if (p.M % (tw224 ? 224 : 256) == 0) return GemmPlan{PATH_TW, tw224 ? 224 : 256, 1, 2};
-    }
-    return GemmPlan{PATH_T, use224 ? 224 : 256, 1, 2, g_variant == 50 ? 1 : 0};
+    return GemmPlan{PATH_T, use224 ? 224 : 256, 1, 2};
   }
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int tiles = ntm * ntn;
@@ -738,24 +670,11 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
 static void describe_plan(const GemmPlan& pl, int epi, int R, char* buf, size_t len) {
   switch (pl.path) {
     case PATH_SPLIT_T:
-      snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, 256, 8, 0, 1, 8>(ltx::GemmParams)", epi, R);
+      snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, 256, 8, 1>(ltx::GemmParams)", epi, R);
       break;
     case PATH_T:
-      if (pl.xr3)
-        snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0, 0, 8, 1>(ltx::GemmParams)", epi, R, pl.bmt,
-                 pl.bmt == 224 ? 4 : 8);
-      else
-        snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0, 0, 8>(ltx::GemmParams)", epi, R, pl.bmt,
-                 pl.bmt == 224 ? 4 : 8);
-      break;
-    case PATH_W4:
-      snprintf(buf, len, "ltx::gemm_w4 (BMT %d)", pl.bmt);
-      break;
-    case PATH_NS:
-      snprintf(buf, len, "ltx::gemm_ns_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt);
-      break;
-    case PATH_TW:
-      snprintf(buf, len, "ltx::gemm_tw_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt);
+      snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0>(ltx::GemmParams)", epi, R, pl.bmt,
+               pl.bmt == 224 ? 4 : 8);
       break;
     default:
       snprintf(buf, len, "ltx::gemm_nt_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.nst);
@@ -769,7 +688,7 @@ static int launch(const GemmParams& p, hipStream_t s) {
   if (pl.path == PATH_SPLIT_T) {
     static bool sk_set = false;
     if (!sk_set) {
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>,
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 1>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       sk_set = true;
     }
@@ -777,7 +696,7 @@ static int launch(const GemmParams& p, hipStream_t s) {
     GemmParams q = p;
     q.ws = ws_for(s).ptr;
     q.splitk = pl.splitk;
-    hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 0, 1>), dim3((unsigned)(big_tiles * pl.splitk)), dim3(512),
+    hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 1>), dim3((unsigned)(big_tiles * pl.splitk)), dim3(512),
                        LDS2, s, q);
     LTX_LAUNCH_CHECK();
     const int64_t n8 = (int64_t)p.M * (p.N / 8);
@@ -785,29 +704,16 @@ static int launch(const GemmParams& p, hipStream_t s) {
     LTX_LAUNCH_CHECK();
     return LTX_OK;
   }
-  if (pl.path == PATH_W4) return launch_w4(EPI, pl.bmt, p, s);
-  if (pl.path == PATH_NS) return launch_ns(EPI, pl.bmt, p, s);
-  if (pl.path == PATH_TW) return launch_tw(EPI, pl.bmt, p, s);
   if (pl.path == PATH_T) {
     static bool t_set = false;
     if (!t_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8, 0, 0, 8, 1>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_t_bytes<256, 1>());
-      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 224, 4, 0, 0, 8, 1>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_t_bytes<224, 1>());
       t_set = true;
     }
     const int64_t ntn = (p.N + BN2 - 1) / BN2;
     const dim3 g224((unsigned)(((p.M + 223) / 224) * ntn)), g256((unsigned)(((p.M + 255) / 256) * ntn));
-    constexpr int L224 = lds_t_bytes<224, 1>(), L256 = lds_t_bytes<256, 1>();
-    if (pl.xr3) {
-      if (pl.bmt == 224)
-        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4, 0, 0, 8, 1>), g224, dim3(512), L224, s, p);
-      else
-        hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8, 0, 0, 8, 1>), g256, dim3(512), L256, s, p);
-    } else if (pl.bmt == 224) {  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
+    if (pl.bmt == 224) {  // 224-row tiles: DMA by waves 0-3 measured +2-3 % (fits in 250 VGPRs)
       hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 224, 4>), g224, dim3(512), LDS2, s, p);
     } else {
       hipLaunchKernelGGL((gemm_nt_kernel_t<EPI, R, 256, 8>), g256, dim3(512), LDS2, s, p);
@@ -868,6 +774,7 @@ static int launch_lora(const GemmParams& p, hipStream_t s) {
 using namespace ltx;
 
 extern "C" int ltx_gemm_set_variant(int variant) {
+  LTX_CHECK_ARG(variant == 0 || variant == 13 || variant == 14, "gemm_set_variant: 0, 13 or 14");
   g_variant = variant;
   return LTX_OK;
 }

@@ -1,4 +1,4 @@
-// Shared pieces of the bf16 GEMM kernels (gemm.hip, gemm_w4.hip): parameters, block order,
+// Shared pieces of the bf16 GEMM kernels (gemm.hip): parameters, block order,
 // fused epilogues.
 #pragma once
 #include "common.h"
@@ -222,9 +222,5 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
 constexpr int BM2 = 256, BN2 = 256;
 constexpr int C_STRIDE2 = BN2 * 2 + 8;  // bf16 C image row stride of the 256-wide tiles
 
-int launch_w4(int epi, int bmt, const GemmParams& p, hipStream_t s);  // gemm_w4.hip
-int launch_ns(int epi, int bmt, const GemmParams& p, hipStream_t s);  // gemm_ns.hip
-int launch_tw(int epi, int bmt, const GemmParams& p, hipStream_t s);  // gemm_tw.hip
-bool tw_supports(int epi);                                              // gemm_tw.hip
 
 }  // namespace ltx

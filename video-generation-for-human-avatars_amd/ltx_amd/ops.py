@@ -310,13 +310,14 @@ def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
     elif d == 64 and int(os.environ.get("LTX_ATTN_W8", "1")) & 1:  # 8 waves x 32 queries
         label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}, 8>"
     else:
-        label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}>"
+        label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}, 4>"
     timer = _timer if (_timer is not None and _timer.wants(label)) else None
     ev0 = timer.start() if timer is not None else None
     call("ltx_attn_fwd", _p(q), _rows(q, "q"), _p(k), _rows(k, "k"), _p(v), _rows(v, "v"), _p(o),
          _rows(o, "o"), _p(lse), _p(key_bias), B, H, Nq, Nk, 0 if kv_shared else Nk, d, scale, _s())
     if timer is not None:
-        timer.stop(label, 4.0 * B * H * Nq * Nk * d, ev0)
+        bk = 1 if kv_shared else B  # q, k, v read once, o + lse written once
+        timer.stop(label, 4.0 * B * H * Nq * Nk * d, ev0, 2.0 * H * d * (2 * B * Nq + 2 * bk * Nk) + 4.0 * B * H * Nq)
     return o, lse
 
 
@@ -342,7 +343,7 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
         b1 = "true" if (key_bias is not None or Nk != 256) else "false"
         kern = f"ltx::attn_bwd1_kernel<{d}, {b1}>"
     else:
-        kern = f"ltx::attn_dkdv_kernel<{d}, {bias}> + ltx::attn_q_kernel<{d}, 1, {bias}>"
+        kern = f"ltx::attn_dkdv_kernel<{d}, {bias}, 4> + ltx::attn_q_kernel<{d}, 1, {bias}, 4>"
     label = ("attention backward: " + ("" if ready else f"ltx::attn_delta_kernel<{d}> + ") + kern)
     timer = _timer if (_timer is not None and _timer.wants(label)) else None
     ev0 = timer.start() if timer is not None else None
@@ -352,7 +353,9 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
          1 if dq.dtype == F32 else 0, _p(dk), _rows(dk, "dk"), _p(dv), _rows(dv, "dv"), B, H, Nq,
          Nk, 0 if kv_shared else Nk, d, scale, _s())
     if timer is not None:
-        timer.stop(label, 8.0 * B * H * Nq * Nk * d, ev0)
+        bk = 1 if kv_shared else B  # q, do, k, v, lse, delta read once; dq, dk, dv written once
+        nb = 2.0 * H * d * (3 * B * Nq + 2 * bk * Nk + 2 * B * Nk) + 8.0 * B * H * Nq
+        timer.stop(label, 8.0 * B * H * Nq * Nk * d, ev0, nb)
     return dq, dk, dv
 
 
@@ -373,10 +376,12 @@ class LaunchTimer:
     GEMM and attention launch while installed (set_launch_timer), each tagged with the kernel
     rocprofv3 names for it (GEMMs: ltx_gemm_describe, the dispatcher's own choice) and the
     launch's ALGORITHMIC FLOPs (GEMM 2*M*N*K without the LoRA K-extension; attention forward
-    4*B*H*Nq*Nk*d, backward twice that -- SURVEY 8d, no recompute)."""
+    4*B*H*Nq*Nk*d, backward twice that -- SURVEY 8d, no recompute) and ALGORITHMIC bytes (every
+    operand read once and every output written once at its stored dtype: for a GEMM
+    2*(M*K + N*K + M*N) + its epilogue's aux rows and K-extension tiles)."""
 
     def __init__(self, only=None):
-        self.records = []  # (label, flops, ev0, ev1)
+        self.records = []  # (label, flops, bytes, ev0, ev1)
         self.only = only   # time only the launches of this label (None: every launch)
 
     def start(self):
@@ -384,23 +389,24 @@ class LaunchTimer:
         ev.record()
         return ev
 
-    def stop(self, label, flops, ev0):
+    def stop(self, label, flops, ev0, nbytes=0.0):
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
-        self.records.append((label, float(flops), ev0, ev1))
+        self.records.append((label, float(flops), float(nbytes), ev0, ev1))
 
     def wants(self, label):
         return self.only is None or self.only == label
 
     def summary(self):
-        """[{kernel, launches, ms, flops}] per label, largest total time first."""
+        """[{kernel, launches, ms, flops, bytes}] per label, largest total time first."""
         torch.cuda.synchronize()
         agg = {}
-        for label, flops, a, b in self.records:
-            e = agg.setdefault(label, {"kernel": label, "launches": 0, "ms": 0.0, "flops": 0.0})
+        for label, flops, nbytes, a, b in self.records:
+            e = agg.setdefault(label, {"kernel": label, "launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             e["launches"] += 1
             e["ms"] += a.elapsed_time(b)
             e["flops"] += flops
+            e["bytes"] += nbytes
         return sorted(agg.values(), key=lambda e: -e["ms"])
 
 
@@ -480,8 +486,24 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
          K2, gcols, gstride, _p(out), _rows(out, "out"), M, N, K, EPI[epilogue], _p(bias),
          _p(aux0), ld0, _p(aux1), ld1, _p(aux2), ld2, float(alpha), rank, rows_per_batch, _s())
     if timer is not None:
-        timer.stop(label, 2.0 * M * N * K, ev0)
+        timer.stop(label, 2.0 * M * N * K, ev0, gemm_algorithmic_bytes(M, N, K, K2, epilogue, aux0 is not None,
+                                                                       aux2 is not None))
     return out
+
+
+_AUX_ROW_READ = {"gated_residual", "gelu_bwd", "accum", "store_rowdot", "lora_residual"}
+
+
+def gemm_algorithmic_bytes(M, N, K, K2, epilogue, has_aux0, has_aux2):
+    """Bytes one ltx_gemm launch must move at minimum: A, W (and the K-extension A2, W2) read once,
+    C written once, plus the epilogue's [M, N] bf16 aux rows (residual / GELU pre-activation /
+    accumulator / attention output for delta) read or written once."""
+    b = 2.0 * (M * K + N * K + M * N) + 2.0 * (M + N) * K2
+    if epilogue in _AUX_ROW_READ or (epilogue == "lora_dgrad_accum" and has_aux0):
+        b += 2.0 * M * N
+    if (epilogue == "gelu" and has_aux0) or (epilogue == "gated_residual" and has_aux2):
+        b += 2.0 * M * N  # pre-activation / pre-gate store
+    return b
 
 
 def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_out=None,

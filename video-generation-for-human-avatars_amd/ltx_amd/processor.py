@@ -99,8 +99,11 @@ class _AttnCall(torch.autograd.Function):
         k_raw, u_k = pk.fwd(e2)
         v, u_v = pv.fwd(e2)
         rope = st["rope"]
-        if rope is not None:
+        if rope is not None and st["eps"] == st["k_eps"]:  # one launch for q and k
             q, k, rq, rk = ops.qk_norm_rope_fwd(q_raw, k_raw, gq, gk, rope, eps=st["eps"])
+        elif rope is not None:  # q_norm / k_norm with different eps: each its own
+            q, _, rq, _ = ops.qk_norm_rope_fwd(q_raw, None, gq, None, rope, eps=st["eps"])
+            k, _, rk, _ = ops.qk_norm_rope_fwd(k_raw, None, gk, None, rope, eps=st["k_eps"])
         else:
             q, _, rq, _ = ops.qk_norm_rope_fwd(q_raw, None, gq, None, None, B=B, N=N, eps=st["eps"])
             k, _, rk, _ = ops.qk_norm_rope_fwd(k_raw, None, gk, None, None, B=B, N=L, eps=st["k_eps"])

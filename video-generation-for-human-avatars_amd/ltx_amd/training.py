@@ -13,6 +13,7 @@ Differences that are deliberate and documented:
     quantile clamp takes the bounds as 0-dim device tensors instead of `float(t_low)`, which gives
     the same f32 result without the device->host round trip in every micro-step.
 """
+import functools
 import math
 
 import torch
@@ -201,6 +202,7 @@ class GradAllReduce:
         self._launched = 0     # buckets [0, _launched) have their all-reduce in flight
         self._works = []
         self._hooks = []
+        self._block_cbs = []  # (weakref to block, callback) appended to its _grad_ready_hooks
 
     # ---- buffers -------------------------------------------------------------------------
     def _world(self):
@@ -246,23 +248,49 @@ class GradAllReduce:
 
     # ---- overlap with the backward -----------------------------------------------------------
     def install(self, model):
-        """Hook the model: each block reports its finished grads (LoRA, written by the block's
-        kernels) at the end of its backward; autograd-accumulated params report through
-        post-accumulate-grad hooks."""
-        block_params = {}
+        """Hook the model: each block reports, at the end of its backward, the grads its own
+        kernels wrote into .grad (the attn1 / attn2 parameters: LoRA adapters, and in
+        train_mode='full' the attention weights, biases and q/k norm weights); every other
+        trainable parameter -- including a block's scale_shift_table, whose gradient autograd
+        accumulates AFTER the block's backward returns (through _AdaModFn) -- reports through a
+        post-accumulate-grad hook. ``uninstall()`` removes both kinds of hook."""
+        import weakref
+        self.uninstall()
+        me = weakref.ref(self)
+
+        def block_cb(b, done=None, ps=None, ids=None):
+            # done: the subset the block has finished (None: all it writes); only parameters the
+            # block's kernels write are reported here
+            red = me()
+            if red is not None:
+                red._ready(ps if done is None else [p for p in done if id(p) in ids])
+
+        in_blocks = set()
         for blk in getattr(model, "transformer_blocks", ()):
-            mine = [p for p in blk.parameters() if id(p) in self._where]
-            if mine:
-                block_params[id(blk)] = mine
-                hooks = blk.__dict__.setdefault("_grad_ready_hooks", [])
-                # the block reports the params it has finished (None: all of its own)
-                hooks.append(lambda b, done=None, ps=mine: self._ready(
-                    ps if done is None else [p for p in done if id(p) in self._where]))
-        in_blocks = {id(p) for ps in block_params.values() for p in ps}
+            written = [p for name in ("attn1", "attn2") if name in blk._modules
+                       for p in blk._modules[name].parameters() if id(p) in self._where]
+            if written:
+                in_blocks.update(id(p) for p in written)
+                cb = functools.partial(block_cb, ps=written, ids={id(p) for p in written})
+                blk.__dict__.setdefault("_grad_ready_hooks", []).append(cb)
+                self._block_cbs.append((weakref.ref(blk), cb))
         for p in self.params:
             if id(p) not in in_blocks:
-                self._hooks.append(p.register_post_accumulate_grad_hook(lambda q: self._ready([q])))
+                self._hooks.append(p.register_post_accumulate_grad_hook(
+                    lambda q: me() is not None and me()._ready([q])))
         return self
+
+    def uninstall(self):
+        """Remove this reducer's block callbacks and post-accumulate-grad hooks."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        for bref, cb in self._block_cbs:
+            blk = bref()
+            hooks = blk.__dict__.get("_grad_ready_hooks") if blk is not None else None
+            if hooks is not None:
+                hooks[:] = [h for h in hooks if h is not cb]
+        self._block_cbs = []
 
     def arm(self):
         """The next backward is the last of the accumulation cycle: reduce during it."""

@@ -1302,7 +1302,10 @@ class Transformer3DModel(nn.Module):
                      per_token)
         sh.full = full
         ckpt = self.training and self.gradient_checkpointing and keep
-        if keep and not full and self._text_batchable():
+        # the stack's backward (adapter grads of every to_k / to_v) runs as the backward of enc2,
+        # so it needs enc2 in the graph: with a frozen caption_projection the per-block text path
+        # computes those adapter grads instead
+        if keep and not full and enc2.requires_grad and self._text_batchable():
             sh.text_stack = _TextStack(self, enc2)
             enc2 = _TextStackFn.apply(enc2, sh.text_stack)
         strat = None
