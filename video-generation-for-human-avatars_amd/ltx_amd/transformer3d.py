@@ -570,11 +570,14 @@ class _BlockFn(torch.autograd.Function):
             dkv = tx.block_dkv(blk)
         else:
             dkv = torch.empty(k2raw.shape[0], 2 * D, dtype=torch.bfloat16, device=h.device)
+        dk2b = dv2b = None
         if sh.text_shared:  # gradient of the shared text rows = sum over the query batches
-            dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
-                                         key_bias=sh.enc_bias, kv_shared=True, delta=delta2)
-            dk2 = ops.batch_sum(dk2, B)
-            dv2 = ops.batch_sum(dv2, B, out=dkv[:, D:])
+            dq2, dk2b, dv2b = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
+                                           key_bias=sh.enc_bias, kv_shared=True, delta=delta2)
+            dk2 = ops.batch_sum(dk2b, B)
+            dv2 = ops.batch_sum(dv2b, B, out=dkv[:, D:])
+            if not full:
+                dk2b = dv2b = None
         else:
             dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
                                          key_bias=sh.enc_bias, dv=dkv[:, D:], delta=delta2)
@@ -584,13 +587,29 @@ class _BlockFn(torch.autograd.Function):
                                          dq_out=dkv[:, :D])
         if full:  # attn2 q/k norm weights, to_q / to_k / to_v
             ops.qk_norm_wgrad_into(dq2, q2raw, rq2, _pgrad(a2.q_norm.weight), B=B, N=N)
-            ops.qk_norm_wgrad_into(dk2, k2raw, rk2, _pgrad(a2.k_norm.weight), B=sh.Bt, N=L)
             ops.wgrad_into(_pgrad(a2.to_q.weight), dq2raw, h1)
             ops.colsum_into(_pgrad(a2.to_q.bias), dq2raw)
-            ops.wgrad_into(_pgrad(a2.to_k.weight), dk2raw, enc2)
-            ops.colsum_into(_pgrad(a2.to_k.bias), dk2raw)
-            ops.wgrad_into(_pgrad(a2.to_v.weight), dv2, enc2)
-            ops.colsum_into(_pgrad(a2.to_v.bias), dv2)
+            if dk2b is not None:
+                # one prompt expanded over the batch: the reference runs to_k / k_norm / to_v on B
+                # identical copies of the text rows (training.py:113-117), so its k / v parameter
+                # grads sum B per-sample bf16 SDPA / k-norm gradients in f32. Summing the batch
+                # first (one bf16 rounding of the sum, as the K/V input gradient above does) loses
+                # the small, cancelling to_k.bias gradient (measured 2.3x the reference's bf16
+                # noise at 2B widths): these grads take the per-sample rows instead.
+                krep, erep, rrep = k2raw.repeat(B, 1), enc2.repeat(B, 1), rk2.repeat(B)
+                dk2raw_b, _ = ops.qk_norm_rope_bwd(dk2b, krep, a2.k_norm.weight, rrep, B=B, N=L)
+                ops.qk_norm_wgrad_into(dk2b, krep, rrep, _pgrad(a2.k_norm.weight), B=B, N=L)
+                ops.wgrad_into(_pgrad(a2.to_k.weight), dk2raw_b, erep)
+                ops.colsum_into(_pgrad(a2.to_k.bias), dk2raw_b)
+                ops.wgrad_into(_pgrad(a2.to_v.weight), dv2b, erep)
+                ops.colsum_into(_pgrad(a2.to_v.bias), dv2b)
+                del krep, erep, rrep, dk2raw_b, dk2b, dv2b
+            else:
+                ops.qk_norm_wgrad_into(dk2, k2raw, rk2, _pgrad(a2.k_norm.weight), B=sh.Bt, N=L)
+                ops.wgrad_into(_pgrad(a2.to_k.weight), dk2raw, enc2)
+                ops.colsum_into(_pgrad(a2.to_k.bias), dk2raw)
+                ops.wgrad_into(_pgrad(a2.to_v.weight), dv2, enc2)
+                ops.colsum_into(_pgrad(a2.to_v.bias), dv2)
         del dq2, dk2
         denc = None
         if has_lora:
