@@ -606,3 +606,4 @@ def test_fused_adamw_multi_tensor_bitwise():
     a, b = run(True), run(False)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
