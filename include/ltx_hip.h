@@ -266,6 +266,18 @@ int ltx_lora_down_grouped(const void* x, int64_t ldx, const float* Wr, int64_t w
  * to ~2^-16 relative. */
 int ltx_lora_split_bf16(const float* src, int64_t rs, int64_t cs, float scale, int64_t R,
                         int64_t r, int role, void* out, int64_t ldo, int64_t K2, void* stream);
+/* Three bf16 pieces (hi, mid, lo: 24 significant bits) of an f32 [r, K] operand, element (j,k)
+ * at src[j*rs + k*cs]: out bf16 [3*RP, K] (ldo), row p*RP + j = piece p of row j, RP = max(r, 16)
+ * with zero rows past r. The operand of ltx_lora_rows. */
+int ltx_lora_pieces(const float* src, int64_t rs, int64_t cs, int64_t r, int64_t K, void* out,
+                    int64_t ldo, void* stream);
+/* ltx_lora_down for token-sized M on the bf16 matrix core: out[m,j] = alpha * sum_k x[m,k] *
+ * (w3[j] + w3[RP+j] + w3[2RP+j])[k] with w3 the ltx_lora_pieces of the f32 weight (exact bf16
+ * products, f32 sums: peft's f32 contraction to summation order). K % 512 == 0. split as in
+ * ltx_lora_down. */
+int ltx_lora_rows(const void* x, int64_t ldx, const void* w3, int64_t ldw, float* out, int64_t ldo,
+                  int64_t M, int64_t K, int64_t r, float alpha, void* split, int64_t ld_split,
+                  int64_t K2, void* stream);
 /* dW(n,j) (+)= alpha * sum_m Y[m,n] * U[m,j] at dw[n*on + j*oj] (f32; overwritten, or added to
  * when accumulate != 0, e.g. straight into a .grad buffer across micro-steps):
  * lora_B grad (Y = dY, U = u: on = r, oj = 1) and lora_A grad (Y = x, U = w: on = 1, oj = K).

@@ -261,6 +261,41 @@ def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
     assert rel(o1, _sdpa_ref(q, kx, vx, B, H, d, bx)) < 1e-2
 
 
+@pytest.mark.parametrize("B,H,Nq,Nk,valid,shared", [(8, 4, 1792, 256, 16, True),   # bench's attn2
+                                                     (2, 3, 300, 256, 70, False),
+                                                     (2, 2, 200, 200, 5, False)])
+def test_attention_padding_blocks_skipped_exactly(B, H, Nq, Nk, valid, shared, monkeypatch):
+    """The one-pass cross-attention kernels skip key blocks that are all caption padding (bias
+    -10000): the skipped probabilities underflow to exactly 0, so O, lse, dQ, dK and dV are bitwise
+    those with every block computed (LTX_ATTN_SKIP=0), and dK / dV of padding keys are 0."""
+    from ltx_amd import ops
+    d = 64
+    scale = d ** -0.5
+    Bk = 1 if shared else B
+    q = g(B * Nq, H * d, seed=51)
+    k = g(Bk * Nk, H * d, seed=52)
+    v = g(Bk * Nk, H * d, seed=53)
+    do = g(B * Nq, H * d, seed=54)
+    keep = torch.arange(Nk, device=DEV)[None, :] < (valid + torch.arange(Bk, device=DEV)[:, None])
+    bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("LTX_ATTN_SKIP", mode)
+        o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias, kv_shared=shared)
+        dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, kv_shared=shared)
+        res[mode] = (o, lse, dq, dk, dv)
+    for a, b_ in zip(res["1"], res["0"]):
+        assert torch.equal(a, b_)
+    o, lse, dq, dk, dv = res["1"]
+    kx = k.repeat(B, 1) if shared else k
+    vx = v.repeat(B, 1) if shared else v
+    bx = bias.repeat(B, 1) if shared else bias
+    assert rel(o, _sdpa_ref(q, kx, vx, B, H, d, bx)) < 1e-2
+    pad = ~(keep.repeat(B, 1) if shared else keep).reshape(-1)
+    assert float(dk.view(-1, H * d)[pad].abs().max()) == 0.0
+    assert float(dv.view(-1, H * d)[pad].abs().max()) == 0.0
+
+
 def test_attention_strided_fused_qkv():
     """Q/K/V read in place from the fused [M, 3*H*d] projection buffer (attn1 layout)."""
     from ltx_amd import ops

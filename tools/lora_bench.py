@@ -45,3 +45,18 @@ ops.lora_wgrad(xs, us, alpha=0.5, out=dB0, accumulate=True)
 refw = 0.5 * xs.float().t() @ us
 res["text_wgrad_rel"] = float((dB0 - refw).norm() / refw.norm())
 print(json.dumps({k: round(v, 7) for k, v in res.items()}), flush=True)
+# LDS-DMA row contraction on the bf16 pieces (ltx_lora_rows) vs the f32 kernel
+pA = ops.lora_pieces(A)
+pB = ops.lora_pieces(Bm, transposed=True)
+r2 = {"rows_A_us": t(lambda: ops.lora_rows(x, pA, r)),
+      "rows_Bt_split_us": t(lambda: ops.lora_rows(x, pB, r, alpha=0.5, split=True)),
+      "pieces_us": t(lambda: ops.lora_pieces(A))}
+o_new = ops.lora_rows(x, pA, r)
+o_old = ops.lora_down(x, A)
+r2["rows_rel_vs_f64"] = float((o_new.double() - x.double() @ A.double().t()).norm() / (x.double() @ A.double().t()).norm())
+r2["down_rel_vs_f64"] = float((o_old.double() - x.double() @ A.double().t()).norm() / (x.double() @ A.double().t()).norm())
+on, sn = ops.lora_rows(x, pB, r, alpha=0.5, split=True)
+oo, so = ops.lora_down(x, Bm, alpha=0.5, transposed=True, split=True)
+r2["rows_Bt_rel_vs_old"] = float((on - oo).norm() / oo.norm())
+r2["split_equal_frac"] = float((sn == so).float().mean())
+print(json.dumps({k: round(v, 9) for k, v in r2.items()}), flush=True)

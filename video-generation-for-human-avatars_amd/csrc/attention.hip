@@ -157,6 +157,7 @@ struct AttnParams {
   int kvb;                             // rows between batches of K, V and key_bias (Nk, or 0: shared)
   float scale;
   int xcd_order;                       // 1: XCD-aware block order (xcd_block), 0: hardware order
+  int skip_masked;                     // 1: skip all-padding key blocks (one-pass kernels), 0: keep
 };
 
 // per-key additive term in log2 units for keys key0..key0+63 -> LDS
@@ -601,6 +602,10 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_dkdv_kernel(con
 // key ranges of at most this many run the one-pass kernels (one 8-wave workgroup holds them all)
 constexpr int BWD1_KEYS = 256;
 constexpr int BWD1_THREADS = 512;
+// key bias (log2 units) at or below which a key counts as padding for tile skipping: the caption
+// mask's bf16(-10000) * log2(e) = -14404, and -inf past Nk. Exact as long as the scaled scores of
+// a row differ by less than ~(14404 - 10000) - 150 log2 units from its unmasked maximum.
+constexpr float KEY_MASKED = -10000.0f;
 
 // =============================================================================================
 // Forward for key ranges of at most 256 (the attn2 cross-attention): a workgroup = 8 waves per
@@ -642,6 +647,17 @@ __global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BI
   __syncthreads();
   const int ntiles = (p.Nk + KT - 1) / KT;
   const int nslices = (p.Nq + 31) / 32;
+  // Key tiles whose every key is padding (bias <= KEY_MASKED: the caption mask's -10000) hold
+  // probabilities that underflow to exactly 0 behind any unmasked key, so skipping them leaves O
+  // and lse bitwise unchanged (a leading masked tile is erased by the first rescale, alpha = 0).
+  // A row with no unmasked key at all keeps every tile (the reference's uniform softmax).
+  unsigned act = ~0u;
+  if (BIAS && p.skip_masked) {
+    act = 0u;
+    for (int t = 0; t < ntiles; ++t)
+      if (__any(kb[min(t * KT + lane, BWD1_KEYS - 1)] > KEY_MASKED)) act |= 1u << t;
+    if (act == 0u) act = ~0u;
+  }
   const bf16_t* qb = p.q + (int64_t)b * p.Nq * p.ldq + hh * HD;
   s16x8 qn[KS];
   auto load_q = [&](int sl) {
@@ -666,6 +682,7 @@ __global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BI
       for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
     float m_run = -1e30f, l_run = 0.f;
     for (int t = 0; t < ntiles; ++t) {
+      if (!((act >> t) & 1u)) continue;
       const int k0 = t * KT;
       f32x16 s[2];
 #pragma unroll
@@ -792,6 +809,11 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
     if (kl < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + kl] * LOG2E : 0.f;
   }
   const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  // 32-key blocks (one per wave) whose keys are all padding have P = dS = 0 exactly behind any
+  // unmasked key: their S / dP / dK / dV work and their dQ k-steps are skipped (dK = dV = 0 are
+  // still stored), which leaves every output bitwise unchanged (see attn_fwd1_kernel).
+  __shared__ unsigned wact[8];
+  if (lane == 0) wact[wave] = (BIAS && p.skip_masked) ? (__any(kbias > KEY_MASKED) ? 1u : 0u) : 1u;
   s16x8 kf[KS], vf[KS];
   {
     const bf16_t* kr = kbase + (int64_t)kc * p.ldk;
@@ -829,11 +851,13 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   auto tr4 = [](const char* a) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
   };
+  unsigned kmask = 0xffu;  // 32-key blocks with an unmasked key (set after the staging barrier)
   // dQ^T += K^T . dS^T over 32-key steps [k0, k1) of the dS image `sim`
   f32x4 dqa[QBW];
   auto dq_steps = [&](const char* sim, int k0, int k1) {
 #pragma unroll
     for (int ks = k0; ks < k1; ++ks) {
+      if (!((kmask >> ks) & 1u)) continue;
       const char* ka = kimg + ks * 32 * (HD * 2) + offk;
       const s16x4 a0 = tr4(ka), a1 = tr4(ka + 16 * (HD * 2));
       s16x8 av;
@@ -896,6 +920,11 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   stage_stats(0, 0);
   __syncthreads();
   __builtin_amdgcn_s_waitcnt(0);  // retire the pre-loop loads (see attn_dkdv_kernel)
+  kmask = 0u;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) kmask |= wact[w] << w;
+  if (kmask == 0u) kmask = 0xffu;  // no unmasked key at all: keep everything
+  const bool mine = (kmask >> wave) & 1u;
 
   // Tile t's dQ product runs during tile t+1's S / dP / dK / dV (its dS image is the other
   // buffer): one barrier interval holds both, so the dQ MFMAs fill the softmax VALU gaps.
@@ -915,6 +944,10 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
     for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      if (!mine) {  // padding keys: only this wave's share of the dQ product
+        if (t > 0) dq_steps(sprev, u * (KSTEPS / 2), (u + 1) * (KSTEPS / 2));
+        continue;
+      }
       f32x16 s, dp;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -1052,6 +1085,12 @@ static int waves8_flag(int bit) {
   return (v >> bit) & 1;
 }
 
+// LTX_ATTN_SKIP=0: the one-pass kernels keep all-padding key blocks (A/B and exactness tests)
+static int skip_flag() {
+  const char* e = getenv("LTX_ATTN_SKIP");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 // LTX_ATTN_FWD1=0: the tiled forward (attn_q_kernel) for every key range
 static int fwd1_flag() {
   const char* e = getenv("LTX_ATTN_FWD1");
@@ -1061,6 +1100,7 @@ static int fwd1_flag() {
 template <int HD>
 static int launch_fwd(AttnParams p, hipStream_t s) {
   p.xcd_order = xcd_order_flag();
+  p.skip_masked = skip_flag();
   if constexpr (HD == 64) {
     if (p.Nk <= BWD1_KEYS && fwd1_flag()) {  // every key staged once per (batch, head)
       // two workgroups per (batch, head) when that still leaves >= 8 slices each: 2 per CU
@@ -1103,6 +1143,7 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   }
   p.delta = delta;
   p.xcd_order = xcd_order_flag();
+  p.skip_masked = skip_flag();
   if constexpr (HD == 64) {  // (head dim 32, the tiny config, keeps the split kernels)
     if (p.Nk <= BWD1_KEYS && bwd1_flag()) {  // every key in one workgroup: one-pass backward
       const dim3 g1((unsigned)p.H, (unsigned)p.B);

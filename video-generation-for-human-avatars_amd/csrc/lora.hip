@@ -134,6 +134,192 @@ __global__ __launch_bounds__(64 * KW) void lora_down_kernel(const bf16_t* __rest
   }
 }
 
+// Three bf16 pieces of an f32 [R, K] operand (element (j, k) at src[j*rs + k*cs]): hi = bf16(v),
+// mid = bf16(v - hi), lo = bf16(v - hi - mid) hold v to 24 significant bits, so the exact
+// bf16 x bf16 products of the matrix core against an exact bf16 activation, summed in f32, stand
+// in for peft's f32 contraction. Row p*RP + j of out is piece p of row j; rows j >= R (RP = 16
+// for R = 8) are zero, so a 16-wide fragment never reads past the pieces.
+__global__ void lora_pieces_kernel(const float* __restrict__ src, int64_t rs, int64_t cs, int R, int RP, int K,
+                                   bf16_t* __restrict__ out, int64_t ldo) {
+  const int64_t total = (int64_t)RP * K;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(i / K), k = (int)(i % K);
+    const float v = j < R ? src[(int64_t)j * rs + (int64_t)k * cs] : 0.f;
+    const bf16_t hi = f2bf(v);
+    const float r1 = v - bf2f(hi);
+    const bf16_t mid = f2bf(r1);
+    const bf16_t lo = f2bf(r1 - bf2f(mid));
+    out[(int64_t)j * ldo + k] = hi;
+    out[(int64_t)(RP + j) * ldo + k] = mid;
+    out[(int64_t)(2 * RP + j) * ldo + k] = lo;
+  }
+}
+
+// The adapter row contraction for token-sized M: out[m,j] = alpha * sum_k x[m,k] * W[j,k] with W
+// as its three bf16 pieces (lora_pieces_kernel), on v_mfma_f32_16x16x32_bf16. The rows stream
+// through LDS by LDS-DMA (one 8-row x 128-B piece per wave-instruction, whole cache lines)
+// instead of per-lane register loads of 16 rows x 64 B. Block = NW waves on 32 rows; wave w owns
+// K range [w K/NW, (w+1) K/NW) and streams its own 32 x 64 slots (4 KiB) through a private
+// NR-slot ring (DMA NR-1 slots ahead), with the pieces' fragments (L2-resident, shared by every
+// block) loaded two slots ahead into three register sets, so no workgroup barrier is needed
+// before the cross-wave sum. The loads are inline asm with counted waits: step s issues the
+// fragments of slot s+2, then the DMA of slot s+NR-1; its wait leaves in flight only what was
+// issued after slot s's fragments.
+// LDS slot image: row r (128 B) holds k chunk c (8 bf16) at physical chunk c ^ ((r >> 1) & 7):
+// conflict-free for the 16-lane groups of ds_read_b128 over rows 0-15 (two rows per 64 banks).
+template <int R, int NW, int NR>
+__global__ __launch_bounds__(64 * NW) void lora_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                            const bf16_t* __restrict__ w3, int64_t ldw,
+                                                            float* __restrict__ out, int64_t ldo, int M, int K,
+                                                            float alpha, bf16_t* __restrict__ split, int64_t lds,
+                                                            int K2) {
+  static_assert(NR >= 4, "ring depth (the counted waits assume D(s) precedes W(s))");
+  constexpr int RP = R >= 16 ? R : 16;
+  constexpr int JT = RP / 16;
+  constexpr int NF = 3 * JT;  // piece fragments per 32-deep k step
+  constexpr int WL = 2 * NF;  // fragment loads per slot
+  __shared__ __attribute__((aligned(16))) char ring[NW][NR][4096];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar DMA / load bases
+  const int m0 = blockIdx.x * 32;
+  const int kw = K / NW, kw0 = wave * kw, nslot = kw / 64;
+  // DMA: piece i of a slot = rows 8i .. 8i+7; lane -> row 8i + (lane >> 3), physical chunk lane & 7
+  uint32_t xo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * i + (lane >> 3);
+    const int lchunk = (lane & 7) ^ ((row >> 1) & 7);
+    xo[i] = (uint32_t)(((int64_t)min(m0 + row, M - 1) * ldx + lchunk * 8) * 2);
+  }
+  const char* xbase = (const char*)(x + kw0);
+  const uint32_t lbase = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)&ring[wave][0][0]);
+  auto dma = [&](int s) {
+    const char* sb = xbase + s * 128;
+    const uint32_t l = lbase + (s % NR) * 4096;
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %5\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(xo[0]), "v"(xo[1]), "v"(xo[2]), "v"(xo[3]), "s"(sb), "s"(l)
+        : "memory", "scc");
+  };
+  // piece fragments: lane -> column j = 16t + (lane & 15), k chunk lane >> 4; k half by offset
+  uint32_t wo[NF];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int t = 0; t < JT; ++t)
+      wo[p * JT + t] = (uint32_t)((((int64_t)(p * RP + t * 16 + (lane & 15))) * ldw + (lane >> 4) * 8) * 2);
+  const char* wbase = (const char*)(w3 + kw0);
+  s16x8 wf[3][2][NF];  // [register set][k half][fragment]
+  auto wload = [&](int s, s16x8 (&dst)[2][NF]) {
+    const char* sb = wbase + s * 128;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(dst[0][f]) : "v"(wo[f]), "s"(sb) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, %2 offset:64" : "=v"(dst[1][f]) : "v"(wo[f]), "s"(sb) : "memory");
+    }
+  };
+  // fragment reads: rows 16q + (lane & 15), logical chunk 4h + (lane >> 4)
+  int roff[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 16 * q + (lane & 15);
+      roff[q][h] = row * 128 + (((4 * h + (lane >> 4)) ^ ((row >> 1) & 7)) * 16);
+    }
+  f32x4 acc[2][JT];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int t = 0; t < JT; ++t) acc[q][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  auto step = [&](int s, s16x8 (&cur)[2][NF], s16x8 (&nxt2)[2][NF]) {
+    // issued after slot s's fragments: D(s+NR-2), W(s+1), D(s+NR-1) (those that exist)
+    const int younger = 4 * (s + NR - 2 < nslot) + WL * (s + 1 < nslot) + 4 * (s + NR - 1 < nslot);
+    switch (younger) {
+      case 4 + WL + 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 + WL + 4) : "memory"); break;
+      case WL + 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WL + 4) : "memory"); break;
+      case WL: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WL) : "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+    const char* sl = &ring[wave][s % NR][0];
+    s16x8 xf[2][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) xf[q][h] = *(const s16x8*)(sl + roff[q][h]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (s + 2 < nslot) wload(s + 2, nxt2);
+    if (s + NR - 1 < nslot) dma(s + NR - 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int t = 0; t < JT; ++t)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            acc[q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[q][h], cur[h][p * JT + t], acc[q][t], 0, 0, 0);
+  };
+  // prologue = steps -2 and -1 of the steady pattern: D(0 .. NR-4), W(0), D(NR-3), W(1), D(NR-2)
+  for (int i = 0; i + 3 < NR; ++i)
+    if (i < nslot) dma(i);
+  wload(0, wf[0]);
+  if (NR - 3 < nslot) dma(NR - 3);
+  if (nslot > 1) wload(1, wf[1]);
+  if (NR - 2 < nslot) dma(NR - 2);
+  for (int s = 0; s < nslot; s += 3) {
+    step(s, wf[0], wf[2]);
+    if (s + 1 < nslot) step(s + 1, wf[1], wf[0]);
+    if (s + 2 < nslot) step(s + 2, wf[2], wf[1]);
+  }
+  // cross-wave sum through LDS (the ring is free once every wave is past its last reads)
+  __syncthreads();
+  float(*part)[32][RP + 1] = (float(*)[32][RP + 1])&ring[0][0][0];
+  static_assert(NW * 32 * (RP + 1) * 4 <= NW * NR * 4096, "partials fit the ring");
+  // C layout: col j = lane & 15 (+16t), row m = (lane >> 4) * 4 + reg
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int t = 0; t < JT; ++t)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) part[wave][16 * q + (lane >> 4) * 4 + rr][t * 16 + (lane & 15)] = acc[q][t][rr];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 32 * R; e += 64 * NW) {
+    const int rr = e / R, j = e % R;
+    const int m = m0 + rr;
+    if (m >= M) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += part[w][rr][j];
+    const float v = sum * alpha;
+    out[(int64_t)m * ldo + j] = v;
+    if (split) {
+      const bf16_t hi = f2bf(v);
+      const bf16_t lo = f2bf(v - bf2f(hi));
+      bf16_t* sr = split + (int64_t)m * lds;
+      sr[j] = hi;
+      sr[R + j] = hi;
+      sr[2 * R + j] = lo;
+    }
+  }
+  if (split) {  // zero padding columns 3R .. K2
+    const int pad = K2 - 3 * R;
+    for (int e = threadIdx.x; e < 32 * pad; e += 64 * NW) {
+      const int rr = e / pad, c = 3 * R + e % pad;
+      const int m = m0 + rr;
+      if (m < M) split[(int64_t)m * lds + c] = (bf16_t)0;
+    }
+  }
+}
+
 // dw(n,j) (+)= alpha * sum_m y[m,n] * u[m,j]   (f32 atomics across row splits)
 // Computed as C[j][n] += U^T[j][m] . Y[m][n] on v_mfma_f32_16x16x4_f32: per 4 rows a lane loads
 // u[m][j] (4 B) and 8 consecutive columns of y (one 16-B load; 16 lanes = 128 columns, 256 B
@@ -301,6 +487,49 @@ extern "C" int ltx_lora_down(const void* x, int64_t ldx, const float* Wr, int64_
                              int64_t ld_split, int64_t K2, void* stream) {
   return ltx_lora_down_grouped(x, ldx, Wr, wj, wk, out, ldo, M, K, r, alpha, split, ld_split, K2, 1, 0, 0, 0, 0,
                                stream);
+}
+
+extern "C" int ltx_lora_pieces(const float* src, int64_t rs, int64_t cs, int64_t r, int64_t K, void* out,
+                               int64_t ldo, void* stream) {
+  LTX_CHECK_ARG(src && out && K > 0 && ldo >= K && (r == 8 || r == 16 || r == 32),
+                "lora_pieces: bad args (rank 8, 16 or 32)");
+  const int RP = r >= 16 ? (int)r : 16;
+  const int64_t total = (int64_t)RP * K;
+  int64_t g = (total + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(lora_pieces_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, src, rs, cs, (int)r, RP,
+                     (int)K, (bf16_t*)out, ldo);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+extern "C" int ltx_lora_rows(const void* x, int64_t ldx, const void* w3, int64_t ldw, float* out, int64_t ldo,
+                             int64_t M, int64_t K, int64_t r, float alpha, void* split, int64_t ld_split, int64_t K2,
+                             void* stream) {
+  LTX_CHECK_ARG(x && w3 && out && M > 0 && K > 0 && ldo >= r, "lora_rows: bad args");
+  LTX_CHECK_ARG(K % 256 == 0 && ldx % 8 == 0 && ((uintptr_t)x % 16) == 0 && ldw % 8 == 0 &&
+                    ((uintptr_t)w3 % 16) == 0 && ldw >= K,
+                "lora_rows: K % 256, 16-B aligned rows of x and of the pieces");
+  LTX_CHECK_ARG((int64_t)ldx * 2 * (M - 1) + 2 * K < ((int64_t)1 << 32) && (int64_t)ldw * 2 * 3 * 32 < ((int64_t)1 << 32),
+                "lora_rows: 32-bit DMA offsets");
+  LTX_CHECK_ARG(!split || (K2 >= 3 * r && K2 % 64 == 0 && ld_split >= K2), "lora_rows: split needs K2 >= 3r, %64");
+  const dim3 grid((unsigned)((M + 31) / 32));
+  hipStream_t s = (hipStream_t)stream;
+  bf16_t* sp = (bf16_t*)split;
+  // 4 waves x K/4 per 32-row block, 4-slot ring: 16.3 us at M = 14336, K = 2048, r = 16 against
+  // 19.9 us for lora_down_kernel (8 waves x K/8 with a 3-slot ring: 17.8 us)
+#define LTX_LORA_ROWS(RR)                                                                             \
+  hipLaunchKernelGGL((lora_rows_kernel<RR, 4, 4>), grid, dim3(256), 0, s, (const bf16_t*)x, ldx,     \
+                     (const bf16_t*)w3, ldw, out, ldo, (int)M, (int)K, alpha, sp, ld_split, (int)K2);
+  switch (r) {
+    case 8: LTX_LORA_ROWS(8) break;
+    case 16: LTX_LORA_ROWS(16) break;
+    case 32: LTX_LORA_ROWS(32) break;
+    default: return fail(LTX_ERR_BAD_ARG, "lora_rows: rank must be 8, 16 or 32");
+  }
+#undef LTX_LORA_ROWS
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
 }
 
 extern "C" int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw,

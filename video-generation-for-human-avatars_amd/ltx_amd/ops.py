@@ -506,15 +506,22 @@ def gemm_algorithmic_bytes(M, N, K, K2, epilogue, has_aux0, has_aux2):
     return b
 
 
+_LORA_ROWS = os.environ.get("LTX_LORA_ROWS", "1") != "0"  # A/B switch: 0 = the f32 kernel only
+
+
 def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_out=None,
-              groups=1, group_strides=(0, 0, 0, 0)):
+              groups=1, group_strides=(0, 0, 0, 0), pieces=None):
     """out[m,j] = alpha * x[m,:] . Wr[j,:]; Wr = lora_A [r,K]; transposed=True takes lora_B [K,r]
     (i.e. uses B^T) for the dgrad w = s * dY . B. split=True also returns the activation
     K-extension operand of the rows (what lora_split(out, "act") makes), written by the same
     kernel. groups > 1 runs `groups` adapters in one launch (ltx_lora_down_grouped): wr is the
     first adapter, group_strides = element offsets per group of (x, wr, out, split); the caller
-    passes out (and split_out) covering every group."""
+    passes out (and split_out) covering every group. pieces = lora_pieces(wr, transposed) (the
+    caller's cache) routes token-sized calls to the bf16-matrix-core kernel (ltx_lora_rows)."""
     M, K = x.shape
+    if pieces is not None and _LORA_ROWS and groups == 1 and M >= 8192 and K % 256 == 0:
+        return lora_rows(x, pieces, wr.shape[1] if transposed else wr.shape[0], alpha=alpha,
+                         out=out, split=split, split_out=split_out)
     if transposed:
         r = wr.shape[1]
         wj, wk = 1, wr.stride(0)
@@ -532,6 +539,35 @@ def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_o
     gx, gw, go, gs = group_strides
     call("ltx_lora_down_grouped", _p(x), _rows(x, "x"), _p(wr), wj, wk, _p(out), _rows(out, "out"),
          M, K, r, float(alpha), _p(sp), lds, K2, groups, gx, gw, go, gs, _s())
+    return (out, sp) if split else out
+
+
+def lora_pieces(wr, transposed=False, out=None):
+    """bf16 [3*RP, K] pieces (hi, mid, lo) of lora_A [r, K] (or of B^T for lora_B [K, r] with
+    transposed=True): the weight operand of lora_rows."""
+    if transposed:
+        K, r = wr.shape
+        rs, cs = wr.stride(1), wr.stride(0)
+    else:
+        r, K = wr.shape
+        rs, cs = wr.stride(0), wr.stride(1)
+    RP = max(r, 16)
+    out = torch.empty(3 * RP, K, dtype=BF16, device=wr.device) if out is None else out
+    call("ltx_lora_pieces", _p(wr), rs, cs, r, K, _p(out), _rows(out, "out"), _s())
+    return out
+
+
+def lora_rows(x, w3, r, alpha=1.0, out=None, split=False, split_out=None):
+    """lora_down for token-sized M from the weight's lora_pieces (ltx_lora_rows)."""
+    M, K = x.shape
+    out = torch.empty(M, r, dtype=F32, device=x.device) if out is None else out
+    sp, K2, lds = None, 0, 0
+    if split:
+        K2 = lora_k2(r)
+        sp = torch.empty(M, K2, dtype=BF16, device=x.device) if split_out is None else split_out
+        lds = _rows(sp, "split_out")
+    call("ltx_lora_rows", _p(x), _rows(x, "x"), _p(w3), _rows(w3, "w3"), _p(out), _rows(out, "out"),
+         M, K, r, float(alpha), _p(sp), lds, K2, _s())
     return (out, sp) if split else out
 
 

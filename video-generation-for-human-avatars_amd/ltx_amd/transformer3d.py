@@ -128,6 +128,20 @@ class LoraLinear(nn.Module):
             self._split_cache[which] = hit
         return hit[1]
 
+    def weight_pieces(self, which):
+        """Cached bf16 pieces (ops.lora_pieces) of 'A' (lora_A) or 'Bt' (lora_B^T): the weight
+        operand of the token-sized adapter contractions (ltx_lora_rows); same keys as
+        weight_split."""
+        p = _ab(self)[1 if which == "Bt" else 0]
+        key = (p.data_ptr(), p._version, ops.weight_generation())
+        hit = self._split_cache.get("pieces_" + which)
+        if hit is None or hit[0] != key:
+            with torch.no_grad():
+                t = ops.lora_pieces(p, transposed=(which == "Bt"))
+            hit = (key, t)
+            self._split_cache["pieces_" + which] = hit
+        return hit[1]
+
     @property
     def weight(self):
         return self.base_layer.weight
@@ -463,7 +477,7 @@ class _BlockFn(torch.autograd.Function):
         if has_lora:
             # peft LoRA fused into the K loop: [x | split(x.A^T)] . [W | split(s*B)]^T
             Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo = lora_ab
-            u_q, su = ops.lora_down(h1, Aq, split=True)
+            u_q, su = ops.lora_down(h1, Aq, split=True, pieces=lora[0].weight_pieces("A"))
             q2raw = ops.gemm(h1, wq, bias=bq, ext=(su, lora[0].weight_split("B")))
             del su
         else:
@@ -480,7 +494,7 @@ class _BlockFn(torch.autograd.Function):
         o2, lse2 = ops.attn_fwd(q2, k2, v2, B, H, d, a2.scale, key_bias=sh.enc_bias,
                                 kv_shared=sh.text_shared)
         if has_lora:
-            u_o, su = ops.lora_down(o2, Ao, split=True)
+            u_o, su = ops.lora_down(o2, Ao, split=True, pieces=lora[3].weight_pieces("A"))
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1,
                           ext=(su, lora[3].weight_split("B")))
             del su
@@ -554,7 +568,8 @@ class _BlockFn(torch.autograd.Function):
         if has_lora:
             lq, lk, lv, lo = lora
             ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
-            w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True)
+            w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True,
+                                     pieces=lo.weight_pieces("Bt"))
             ops.lora_wgrad(o2, w_o, transpose_out=True, out=_grad_buf(lo, "A"), accumulate=True)
             do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")), **rd)
         else:
@@ -614,7 +629,8 @@ class _BlockFn(torch.autograd.Function):
         denc = None
         if has_lora:
             ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
-            w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True)
+            w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True,
+                                     pieces=lq.weight_pieces("Bt"))
             ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
                            ext=(sw, lq.weight_split("A")))
