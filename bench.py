@@ -452,7 +452,11 @@ def main():
                                + (", per-block gradient checkpointing" if args.grad_ckpt else ""),
                    "model": "LTX-Video-2B (28 layers, D 2048, 32x64 heads)", "global_batch": B_PER_GPU * world,
                    "micro_batch_per_gpu": B_PER_GPU, "seq_len": N, "text_len": L_TXT,
-                   "grad_accum": ACCUM, "parallelism": f"zero2-dp{world}" if full else f"dp{world}"},
+                   "grad_accum": ACCUM, "parallelism": f"zero2-dp{world}" if full else f"dp{world}",
+                   # 16 of 256 caption tokens are valid: the cross-attention kernels skip all-padding
+                   # key blocks (exact: bitwise-equal outputs); FLOPs still count Nk = 256
+                   "attn2_padding_blocks": ("kept (LTX_ATTN_SKIP=0)" if os.environ.get("LTX_ATTN_SKIP") == "0"
+                                            else "skipped, exact")},
         "step_tflops_per_gpu": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
         "roofline": {"bound": "mfma", "kernel": dom["kernel"],
