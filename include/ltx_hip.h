@@ -43,7 +43,9 @@ enum {
                                    Lb = aux2 f32 [N,rank]      peft lora.Linear, training.py:50-68 */
   LTX_EPI_LORA_RESIDUAL = 4,    /* C = bf16(R + bf16(LORA)); R = aux0        attention.py:285 */
   LTX_EPI_GELU_BWD = 5,         /* C = bf16(bf16(acc) * gelu_tanh'(F)); F = aux0 (pre-act) */
-  LTX_EPI_ACCUM = 6,            /* C = bf16(R + bf16(acc)); R = aux0 (may alias C) */
+  LTX_EPI_ACCUM = 6,            /* C = bf16(R + bf16(acc)); R = aux0 (may alias C); with aux1 (gate
+                                   rows, one per batch) also aux2 = bf16(C * gate[m / rows_per_batch])
+                                   (the backward's gate multiply, bitwise ltx_gate_mul_bf16) */
   LTX_EPI_LORA_DGRAD_ACCUM = 7, /* C = [R +] bf16(bf16(acc) + bf16(alpha * Wd[m,:].A[:,n]));
                                    Wd = aux1 f32 [M,rank], A = aux2 f32 [rank,N], R = aux0 opt. */
   LTX_EPI_STORE_ROWDOT = 8,     /* C = y, and the attention backward's delta of the rows:

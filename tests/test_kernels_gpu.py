@@ -115,6 +115,30 @@ def test_gemm_epilogues(M, N, K):
     assert rel(out, R.float() + acc + (Wd @ A).to(torch.bfloat16).float()) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K,ext", [(14336, 2048, 2048, True),   # large tile + LoRA ext (dh1)
+                                       (14336, 2048, 2048, False),
+                                       (512, 256, 256, False),       # 128x128, one pass
+                                       (256, 2048, 8192, True)])     # 128x128, split-K + ext
+def test_gemm_accum_gated_copy(M, N, K, ext):
+    """LTX_EPI_ACCUM with a gate (aux1) and aux2: C is bitwise the plain accumulate and aux2 is
+    bitwise gate_mul(C, gate) (the backward's d_y1 = bf16(dh1 * g_msa) from dh1's own epilogue)."""
+    from ltx_amd import ops
+    B = 8
+    a, w = g(M, K, seed=61), g(N, K, seed=62, scale=K ** -0.5)
+    R = g(M, N, seed=63)
+    mods = g(B, 6, N, seed=64)  # the gate is a [B, N] row view of the modulation tensor
+    gate = mods[:, 2]
+    kw = {}
+    if ext:
+        K2 = 64
+        kw["ext"] = (g(M, K2, seed=65), g(N, K2, seed=66, scale=0.1))
+    c0 = ops.gemm(a, w, epilogue="accum", aux0=R, **kw)
+    d = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    c1 = ops.gemm(a, w, epilogue="accum", aux0=R, aux1=gate, aux2=d, rows_per_batch=M // B, **kw)
+    assert torch.equal(c1, c0)
+    assert torch.equal(d, ops.gate_mul(c0, gate, M // B))
+
+
 @pytest.mark.parametrize("M,N,K,hd,ext", [(14336, 2048, 2048, 64, False),  # large tile (224 rows)
                                           (512, 256, 256, 64, False),     # 128x128, one pass
                                           (256, 2048, 8192, 64, True),    # 128x128, split-K + LoRA ext

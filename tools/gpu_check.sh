@@ -1,3 +1,2 @@
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
-timeout -k 10 120 python -u tools/pp_check.py 2>&1 | grep -v amdgpu.ids || exit 1
-for i in 1 2; do for v in 0 1; do echo "== PP=$v"; LTX_ATTN_PP=$v timeout -k 10 120 python -u tools/attn_bench.py --which self --iters 30 2>&1 | grep -v amdgpu.ids || exit 1; done; done
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_model_gpu.py tests/test_full_gpu.py tests/test_parity_2b_gpu.py tests/test_full_2b_gpu.py > gpurun_out/t_check.log 2>&1; rc=$?; tail -2 gpurun_out/t_check.log; exit $rc

@@ -897,6 +897,8 @@ extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, 
       return launch<LTX_EPI_GELU_BWD>(p, s);
     case LTX_EPI_ACCUM:
       LTX_CHECK_ARG(aux0, "gemm accum: needs the accumulator input (aux0)");
+      LTX_CHECK_ARG(!aux1 == !aux2 && (!aux1 || (ld1 % 8 == 0 && ld2 % 8 == 0 && ld2 >= N && M % p.rows_per_batch == 0)),
+                    "gemm accum: the gated copy needs both the gate rows (aux1) and its output (aux2), 16-B rows");
       return launch<LTX_EPI_ACCUM>(p, s);
     case LTX_EPI_LORA_DGRAD_ACCUM:
       LTX_CHECK_ARG(aux1 && aux2, "gemm lora dgrad: needs Wd (aux1) and A (aux2)");

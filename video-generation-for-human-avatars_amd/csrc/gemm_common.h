@@ -91,6 +91,8 @@ __device__ __forceinline__ void epi_load(const GemmParams& p, int m, int n0, Epi
   if constexpr (epi_has_aux<EPI>()) x.a = *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
   if constexpr (EPI == LTX_EPI_GATED_RESIDUAL)
     x.g = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)(m / p.rows_per_batch) * p.ld1 + n0);
+  if constexpr (EPI == LTX_EPI_ACCUM)
+    if (p.aux1) x.g = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)(m / p.rows_per_batch) * p.ld1 + n0);
 }
 
 template <int EPI, int R>
@@ -189,10 +191,24 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       out8[j + 1] = g[1];
     }
   } else if constexpr (EPI == LTX_EPI_ACCUM) {
-    // out = R + bf16(acc): R = aux0 (ld0); C may alias R
+    // out = R + bf16(acc): R = aux0 (ld0); C may alias R. With aux1 (gate rows of the batch,
+    // ld1) and aux2 (ld2) also aux2 = bf16(bf16(out) * gate[m / rows_per_batch]): the backward's
+    // gate multiply (ltx_gate_mul_bf16, bitwise) fused into the pass that writes out
     const u32x4 r4 = pre ? pre->a : *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + v[j];
+    if (p.aux1) {
+      const u32x4 g4 = pre ? pre->g
+                           : *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)(m / p.rows_per_batch) * p.ld1 + n0);
+      u32x4 pk;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float lo = rbf(out8[2 * j]) * bf2f((bf16_t)g4[j]);
+        const float hi = rbf(out8[2 * j + 1]) * bf2f((bf16_t)(g4[j] >> 16));
+        pk[j] = pack2(lo, hi);
+      }
+      *(u32x4*)((bf16_t*)p.aux2 + (int64_t)m * p.ld2 + n0) = pk;
+    }
   } else if constexpr (EPI == LTX_EPI_LORA_DGRAD_ACCUM) {
     // out = [R +] bf16( bf16(acc) + bf16(alpha * Wd[m,:] . A[:,n]) ), Wd = aux1 f32 [M,rank]
     // (ld1), A = aux2 f32 [rank, N] (ld2 = row stride of A), R = aux0 optional (ld0)

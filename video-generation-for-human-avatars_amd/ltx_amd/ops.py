@@ -501,8 +501,8 @@ def gemm_algorithmic_bytes(M, N, K, K2, epilogue, has_aux0, has_aux2):
     b = 2.0 * (M * K + N * K + M * N) + 2.0 * (M + N) * K2
     if epilogue in _AUX_ROW_READ or (epilogue == "lora_dgrad_accum" and has_aux0):
         b += 2.0 * M * N
-    if (epilogue == "gelu" and has_aux0) or (epilogue == "gated_residual" and has_aux2):
-        b += 2.0 * M * N  # pre-activation / pre-gate store
+    if (epilogue == "gelu" and has_aux0) or (epilogue in ("gated_residual", "accum") and has_aux2):
+        b += 2.0 * M * N  # pre-activation / pre-gate store, or the accumulate's gated copy
     return b
 
 

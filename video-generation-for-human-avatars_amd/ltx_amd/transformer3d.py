@@ -627,13 +627,16 @@ class _BlockFn(torch.autograd.Function):
                 ops.colsum_into(_pgrad(a2.to_v.bias), dv2)
         del dq2, dk2
         denc = None
+        # dh1 = dh2 + dq2raw . W_q2 (+ LoRA) and, from the same epilogue, d_y1 = bf16(dh1 * g_msa)
+        d_y1 = torch.empty_like(dh2)
+        gated = dict(aux1=mods[:, 2], aux2=d_y1, rows_per_batch=rpm)
         if has_lora:
             ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
             w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True,
                                      pieces=lq.weight_pieces("Bt"))
             ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
-                           ext=(sw, lq.weight_split("A")))
+                           ext=(sw, lq.weight_split("A")), **gated)
             if tx is None:
                 K2 = ops.lora_k2(r)
                 swkv = torch.empty(dkv.shape[0], 2 * K2, dtype=torch.bfloat16, device=h.device)
@@ -654,12 +657,12 @@ class _BlockFn(torch.autograd.Function):
             # the kernels' atomics); autograd gets None for them
             grads_lora = [None] * 8
         else:
-            dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2)
+            dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2, **gated)
             if tx is None:
                 denc = ops.gemm(dkv, W["kv2_wT"])
         del dq2raw, dk2raw, dv2, dh2, dkv
         # ---- attn1: h1 = h + g_msa * to_out(sdpa(rope(qn(q)), rope(kn(k)), v))
-        d_y1 = ops.gate_mul(dh1, mods[:, 2], rpm)
+        # (d_y1 = bf16(dh1 * g_msa) came out of the dh1 GEMM's epilogue: `gated` above)
         delta1 = torch.empty(B, H, N, dtype=torch.float32, device=h.device) if _DELTA_FUSED else None
         rd = dict(epilogue="store_rowdot", aux0=o1, aux1=delta1, rank=d, rows_per_batch=N) \
             if _DELTA_FUSED else {}
