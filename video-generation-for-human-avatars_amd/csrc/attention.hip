@@ -25,203 +25,10 @@
 // atomic rate at these sizes).
 #include <cstdlib>
 
-#include "common.h"
+#include "attention_common.h"
 #include "ltx_hip.h"
 
 namespace ltx {
-
-constexpr float LOG2E = 1.4426950408889634f;
-constexpr int ATT_THREADS = 256;
-
-// Chunk swizzle of row `row`. HD = 64 (128-B rows, 8 chunks): x = (row >> 1) & 7 bit-reversed.
-//  * 16-B row reads (ds_read_b128, lane groups of 16 over rows {0-3,12-15,20-27} / {4-11,16-19,
-//    28-31}): the 8 rows of one parity in a group have distinct x, so distinct chunks.
-//  * transposed reads (ds_read_b64_tr_b16, 32-lane halves over rows R..R+3, R = 0 mod 4, one
-//    aligned group of 4 chunks): rows R and R+2 (same bank half) differ in x's bit 0, which the
-//    reversal moves to bit 2, so their chunk groups are disjoint. With the plain (row >> 1) & 7
-//    they coincide: a 2-way conflict on every transposed read (SQ_LDS_BANK_CONFLICT, r02_pmc_sq).
-// HD = 32 (64-B rows): four consecutive rows already cover the 64 banks.
-template <int HD>
-__device__ __forceinline__ int swz(int row) {
-  if constexpr (HD == 64) {
-    const int x = (row >> 1) & 7;
-    return ((x & 1) << 2) | (x & 2) | (x >> 2);
-  } else {
-    return (row >> 1) & (HD / 8 - 1);
-  }
-}
-
-template <int HD>
-__device__ __forceinline__ int toff(int row, int chunk) {
-  return row * (HD * 2) + ((chunk ^ swz<HD>(row)) << 4);
-}
-
-// Per-lane LDS byte offsets of the fragment reads, computed once per kernel. Both kinds of
-// read start at a row that is a multiple of 16 (rbase = 32u, + 16s), and swz depends on
-// (row >> 1) mod 8 only, so a read is this lane offset + a wave-uniform constant.
-template <int HD>
-struct LaneOfs {
-  static constexpr int KS = HD / 16, DS = HD / 32;
-  int row[KS];    // 16-B row fragment: row (lane & 31), dims ks*16 + 8*(lane >> 5) .. +7
-  int tr[DS][2];  // transposed fragment: rows 4h + q (+8), columns d*32 + (lane & 31)
-  __device__ __forceinline__ explicit LaneOfs(int lane) {
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) row[ks] = toff<HD>(lane & 31, ks * 2 + (lane >> 5));
-    const int h = lane >> 5, g = (lane >> 4) & 1, q = (lane & 15) >> 2, p = lane & 3;
-#pragma unroll
-    for (int d = 0; d < DS; ++d) {
-      const int col = d * 32 + 16 * g + 4 * p;
-      tr[d][0] = toff<HD>(4 * h + q, col >> 3) + ((col & 7) << 1);
-      tr[d][1] = toff<HD>(4 * h + q + 8, col >> 3) + ((col & 7) << 1);
-    }
-  }
-};
-
-// 16-B row fragment: lane reads row (base + (l&31)), dims ks*16 + 8*(l>>5) .. +7
-template <int HD>
-__device__ __forceinline__ s16x8 row_frag(const char* tile, int base, int ks, const LaneOfs<HD>& lo) {
-  return *(const s16x8*)(tile + base * (HD * 2) + lo.row[ks]);
-}
-
-// Transposed fragment for an A operand that sums over the tile's ROW axis, matching an
-// accumulator-as-B operand (k-step s of a 32-row accumulator tile): element j of lane half h
-// is row 16s + 8(j>>2) + 4h + (j&3) (+ rbase), column 32d + (lane & 31).
-template <int HD>
-__device__ __forceinline__ s16x8 tr_frag(const char* tile, int rbase, int s, int d, const LaneOfs<HD>& lo) {
-  const char* t = tile + (rbase + 16 * s) * (HD * 2);
-  const s16x4 lo4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(t + lo.tr[d][0]));
-  const s16x4 hi4 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(t + lo.tr[d][1]));
-  s16x8 r;
-  r[0] = lo4[0]; r[1] = lo4[1]; r[2] = lo4[2]; r[3] = lo4[3];
-  r[4] = hi4[0]; r[5] = hi4[1]; r[6] = hi4[2]; r[7] = hi4[3];
-  return r;
-}
-
-// accumulator registers 8s..8s+7 -> bf16 B-operand fragment for k-step s
-__device__ __forceinline__ s16x8 acc_frag(const f32x16& a, int s) {
-  s16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(a[8 * s + j]);
-  return r;
-}
-
-__device__ __forceinline__ f32x16 mfma32(const s16x8& a, const s16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-// row (in the register axis) of accumulator register r for lane half h
-__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
-
-// global 16-B loads of a [ROWS][HD] tile, staged in registers, written swizzled. A thread moves
-// chunk c = tid % CH of rows tid / CH + i * RSTEP: its byte offsets inside a tile are constant,
-// so a tile is one scalar base (row0 * ld) + a 24-bit-multiply lane offset per load (no per-tile
-// 64-bit address math, no lane predicates); rows past a ragged end re-read the last row.
-template <int HD, int ROWS, int NTH = ATT_THREADS>
-struct TileStage {
-  static constexpr int CH = HD / 8;
-  static constexpr int PER = ROWS * CH / NTH;
-  static constexpr int RSTEP = NTH / CH;
-  static_assert(ROWS * CH % NTH == 0, "a tile must split evenly over the workgroup");
-  u32x4 v[PER];
-  __device__ __forceinline__ void load(const bf16_t* base, int64_t ld, int row0, int nrows, int tid) {
-    const int r = tid / CH, c = tid % CH;
-    const char* tb = (const char*)(base + (int64_t)row0 * ld);  // wave-uniform
-    const int lim = nrows - 1 - row0;                             // rows past the end re-read the last
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const uint32_t off = __umul24((uint32_t)min(r + i * RSTEP, lim), (uint32_t)(ld * 2)) + (uint32_t)(c * 16);
-      v[i] = *(const u32x4*)(tb + off);
-    }
-  }
-  __device__ __forceinline__ void store(char* tile, int tid) const {
-    const int r = tid / CH, c = tid % CH;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) *(u32x4*)(tile + toff<HD>(r + i * RSTEP, c)) = v[i];
-  }
-};
-
-struct AttnParams {
-  const bf16_t* q; int64_t ldq;
-  const bf16_t* k; int64_t ldk;
-  const bf16_t* v; int64_t ldv;
-  const bf16_t* o; int64_t ldo;      // forward output (bwd: the saved output, for delta)
-  bf16_t* o_out;
-  const bf16_t* dout; int64_t lddo;
-  float* lse;                          // [B,H,Nq] log2 units
-  const float* delta;                  // [B,H,Nq]
-  const float* key_bias;               // [B,Nk] natural units, or null
-  void* dq; int64_t lddq; int dq_f32;  // dQ output
-  bf16_t* dk; int64_t lddk;
-  bf16_t* dv; int64_t lddv;
-  int B, H, Nq, Nk;
-  int kvb;                             // rows between batches of K, V and key_bias (Nk, or 0: shared)
-  float scale;
-  int xcd_order;                       // 1: XCD-aware block order (xcd_block), 0: hardware order
-  int skip_masked;                     // 1: skip all-padding key blocks (one-pass kernels), 0: keep
-};
-
-// per-key additive term in log2 units for keys key0..key0+63 -> LDS
-__device__ __forceinline__ void key_bias_tile(float* kb, const AttnParams& p, int b, int key0, int n, int tid) {
-  if (tid < n) {
-    const int key = key0 + tid;
-    float v = -INFINITY;
-    if (key < p.Nk) v = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + key] * LOG2E : 0.f;
-    kb[tid] = v;
-  }
-}
-
-// =============================================================================================
-// forward (MODE 0) and dQ (MODE 1): queries on lanes, keys in registers.
-// BIAS: keys carry an additive term (encoder mask bias, or -inf past a ragged Nk); without it
-// (self-attention, Nk % 64 == 0) the per-key LDS reads and adds disappear.
-// VALU diet (the forward is VALU-bound at head dim 64): the running max is taken on the raw
-// scores (scale > 0), each probability is one v_fma + one v_exp_f32, and the O rescale is skipped
-// unless some lane's max grew by more than RESCALE_TAU (deferred max, above).
-// =============================================================================================
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-// Deferred max (forward kernels): the running max m_run (log2 units) and with it O and l are
-// rescaled only when some lane's tile max exceeds it by more than RESCALE_TAU; below that the
-// probabilities 2^(s - m_run) stay <= 2^TAU (exact in f32, bf16 keeps its relative precision for
-// the P.V MFMA) and lse = m_run + log2(l) is unchanged in meaning. Most 64-key tiles then skip the
-// O rescale pass.
-#ifndef LTX_RESCALE_TAU
-#define LTX_RESCALE_TAU 8.0f
-#endif
-constexpr float RESCALE_TAU = LTX_RESCALE_TAU;
-
-// lane l and lane l ^ 32 combined without an LDS round trip (v_permlane32_swap): both halves
-// get the bit-identical result (same operand order in every lane)
-__device__ __forceinline__ float xor32_max(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float xor32_sum(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// XCD-aware block order: the hardware deals consecutive workgroups round-robin over the 8 XCDs,
-// which would spread the blocks of one (batch, head) -- all reading the same K/V (or Q/dO) --
-// over 8 L2s and fetch those operands 8 times from beyond L2 (~1 GB per launch measured at
-// config A). Bijective remap: XCD x takes a contiguous range of the (x fastest, head, batch)
-// block order.
-__device__ __forceinline__ void xcd_block(int xcd_order, int& bx, int& by, int& bz) {
-  if (!xcd_order) {
-    bx = blockIdx.x;
-    by = blockIdx.y;
-    bz = blockIdx.z;
-    return;
-  }
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int total = gx * gy * gridDim.z;
-  const int L = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
-  const int q = total / 8, r = total % 8, xcd = L % 8, idx = L / 8;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-  bx = wg % gx;
-  by = (wg / gx) % gy;
-  bz = wg / (gx * gy);
-}
 
 // NW waves (NW x 32 queries) per workgroup: 4, or 8 to halve the K/V staging per query
 template <int HD, int MODE, bool BIAS, int NW = 4>
@@ -304,59 +111,94 @@ __global__ __launch_bounds__(NW * 64, MODE == 1 ? 3 : 2) void attn_q_kernel(cons
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(kf[u][ks], qf[ks], s[u]);
       }
-    } else {  // forward: stay at <= 128 VGPRs (4 waves / SIMD)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(ktile, u * 32, ks, lofs), qf[ks], s[u]);
-      }
     }
     if constexpr (MODE == 0) {
-      float mt = -1e30f;
-      if constexpr (BIAS) {
+      // forward: stay at <= 128 VGPRs (4 waves / SIMD). S^T for the tile's 64 keys:
+      auto scores = [&]() {
+        // opaque zero offset: keeps the K fragment reads inside the pass loop below (hoisted out
+        // of it they would hold 32 more VGPRs for the whole tile)
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const char* kt = ktile + z;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(kt, u * 32, ks, lofs), qf[ks], s[u]);
+        }
+      };
+      // probabilities at the running max, the row sum in 4 chains (not one 32-deep add chain)
+      float ls[4];
+      auto probs = [&]() {
+        const float nm = -m_run;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ls[i] = 0.f;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const f32x4 kb4 = *(const f32x4*)&kb[u * 32 + 8 * g + 4 * h];
+            f32x4 kb4;
+            if constexpr (BIAS) kb4 = *(const f32x4*)&kb[u * 32 + 8 * g + 4 * h];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float x = fmaf(s[u][4 * g + i], c2, kb4[i]);
-              s[u][4 * g + i] = x;
-              mt = fmaxf(mt, x);
+              const int r = 4 * g + i;
+              const float e = BIAS ? fast_exp2(fmaf(s[u][r], c2, kb4[i]) + nm) : fast_exp2(fmaf(s[u][r], c2, nm));
+              s[u][r] = e;
+              ls[r & 3] += e;
             }
           }
-      } else {
-        float mr[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};  // 4 chains: ILP for v_max3
+      };
+      // Speculative fast path (every tile but the first): exponentiate at the running max straight
+      // away. A lane whose 32 probabilities sum to <= 2^TAU holds no score past m_run + TAU, so if
+      // no lane of the wave exceeds that the deferred-max rule below would not rescale, and these
+      // ARE the tile's probabilities: the per-tile max (16 v_max3 + a lane swap) is skipped. Else
+      // (the first tile, or a max that grew by more than TAU) S is recomputed and the rule runs.
+      // One loop body for both passes keeps a single copy of the S and P registers.
+      float alpha = 1.f;
+      bool rescale = false;
+#pragma unroll 1
+      for (int pass = (t == 0); pass < 2; ++pass) {
+        scores();
+        if (pass) {
+          float mt = -1e30f;
+          if constexpr (BIAS) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < 2; ++u)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) mr[r & 3] = fmaxf(mr[r & 3], s[u][r]);
-        mt = fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3])) * c2;
+              for (int g = 0; g < 4; ++g) {
+                const f32x4 kb4 = *(const f32x4*)&kb[u * 32 + 8 * g + 4 * h];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mt = fmaxf(mt, fmaf(s[u][4 * g + i], c2, kb4[i]));
+              }
+          } else {
+            float mr[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};  // 4 chains: ILP for v_max3
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) mr[r & 3] = fmaxf(mr[r & 3], s[u][r]);
+            mt = fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3])) * c2;
+          }
+          mt = xor32_max(mt);
+          const float m_new = fmaxf(m_run, mt);
+          if (__any(m_new > m_run + RESCALE_TAU)) {
+            alpha = fast_exp2(m_run - m_new);
+            rescale = true;
+            m_run = m_new;
+          }
+        }
+        probs();
+        if (pass || !__any(((ls[0] + ls[1]) + (ls[2] + ls[3])) > RESCALE_SUM)) break;
       }
-      mt = xor32_max(mt);
-      const float m_new = fmaxf(m_run, mt);
-      if (__any(m_new > m_run + RESCALE_TAU)) {
-        const float alpha = fast_exp2(m_run - m_new);
+      // O and l at the old max, rescaled once outside the pass loop (inside it, the conditionally
+      // written O registers cost a copy of all of them per pass)
+      if (rescale) {
         l_run *= alpha;
 #pragma unroll
         for (int d = 0; d < DS; ++d)
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc[d][r] *= alpha;
-        m_run = m_new;
       }
-      const float nm = -m_run;
-      float ls[4] = {0.f, 0.f, 0.f, 0.f};  // 4 chains instead of one 32-deep dependent add chain
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = BIAS ? fast_exp2(s[u][r] + nm) : fast_exp2(fmaf(s[u][r], c2, nm));
-          s[u][r] = e;
-          ls[r & 3] += e;
-        }
       l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
@@ -508,18 +350,29 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_dkdv_kernel(con
   const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
   TileStage<HD, QT, NW * 64> qs_, os_;
   const int ntiles = (p.Nq + QT - 1) / QT;
-  auto stage_stats = [&](int qb) {
+  // the next tile's -lse2 / delta ride in registers with the Q/dO prefetch (wave 0's lanes): a
+  // load issued after the loop body would put one L2 round trip in every barrier interval
+  float nl_next = 0.f, dl_next = 0.f;
+  auto load_stats = [&](int qb) {
     if (tid < QT) {
-      const int qq = qb + tid;
-      st_lse[tid] = qq < p.Nq ? -lbase[qq] : -INFINITY;  // -lse2 (rows past Nq: P = 0)
-      st_dl[tid] = qq < p.Nq ? dbase[qq] : 0.f;
+      const int qq = min(qb + tid, p.Nq - 1);
+      nl_next = -lbase[qq];
+      dl_next = dbase[qq];
+    }
+  };
+  auto store_stats = [&](int qb) {
+    if (tid < QT) {
+      const bool in = qb + tid < p.Nq;
+      st_lse[tid] = in ? nl_next : -INFINITY;  // -lse2 (rows past Nq: P = 0)
+      st_dl[tid] = in ? -dl_next : 0.f;  // -delta: the dP accumulator's initial value
     }
   };
   qs_.load(qbase, p.ldq, 0, p.Nq, tid);
   os_.load(obase, p.lddo, 0, p.Nq, tid);
+  load_stats(0);
   qs_.store(qtile, tid);
   os_.store(otile, tid);
-  stage_stats(0);
+  store_stats(0);
   __syncthreads();
 
   // Retire every pre-loop global load (Q/dO/K/V fragments) with a counter wait hipcc can see:
@@ -531,14 +384,20 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_dkdv_kernel(con
     if (t + 1 < ntiles) {
       qs_.load(qbase, p.ldq, qb + QT, p.Nq, tid);
       os_.load(obase, p.lddo, qb + QT, p.Nq, tid);
+      load_stats(qb + QT);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      // dP^T accumulates from -delta (st_dl holds -delta): dS = P * dP' needs no subtraction
       f32x16 s, dp;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s[r] = 0.f;
-        dp[r] = 0.f;
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 dl4 = *(const f32x4*)&st_dl[u * 32 + 8 * g + 4 * h];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s[4 * g + i] = 0.f;
+          dp[4 * g + i] = dl4[i];
+        }
       }
       s16x8 qfr[KS], ofr[KS];
 #pragma unroll
@@ -554,13 +413,12 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_dkdv_kernel(con
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 nl4 = *(const f32x4*)&st_lse[u * 32 + 8 * g + 4 * h];
-        const f32x4 dl4 = *(const f32x4*)&st_dl[u * 32 + 8 * g + 4 * h];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g + i;
           const float pr = fast_exp2(fmaf(s[r], c2, BIAS ? kbias + nl4[i] : nl4[i]));
           s[r] = pr;
-          dp[r] = pr * (dp[r] - dl4[i]);
+          dp[r] = pr * dp[r];
         }
       }
 #pragma unroll
@@ -578,7 +436,7 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_dkdv_kernel(con
       __syncthreads();
       qs_.store(qtile, tid);
       os_.store(otile, tid);
-      stage_stats(qb + QT);
+      store_stats(qb + QT);
       __syncthreads();
     }
   }
@@ -1159,6 +1017,14 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   bool k8 = false;
   if constexpr (HD == 64) k8 = waves8_flag(1);
   dim3 gk((unsigned)(k8 ? (p.Nk + 255) / 256 : (p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
+  if (HD == 64 && !k8 && dkdv_pipe_enabled()) {
+    if (needs_bias(p))
+      hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_q_kernel<HD, 1, false>), gq, dim3(ATT_THREADS), 0, s, p);
+    LTX_LAUNCH_CHECK();
+    return launch_dkdv_pipe(p, s);
+  }
   if (needs_bias(p)) {
     hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
     LTX_LAUNCH_CHECK();

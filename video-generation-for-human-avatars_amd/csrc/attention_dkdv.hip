@@ -1,0 +1,341 @@
+// dK / dV of F.scaled_dot_product_attention (attention.py:1057-1064) for head dim 64, software
+// pipelined: the self-attention backward's dominant kernel at config A (N = 1792).
+//
+// Same algorithm and layout as attn_dkdv_kernel (attention.hip): a workgroup = 4 waves x 32 keys,
+// each wave's K / V fragments in registers, dK^T and dV^T accumulated over 32-query halves:
+//   A(j): S^T = K.Q^T and dP'^T = delta - V.dO^T (the accumulator starts at delta, V is negated
+//         once at load), 8 MFMAs;
+//   B(j): P = exp2(S.c - lse), dS = P (dP - delta) = -P dP', both to bf16 B operands (VALU);
+//   C(j): dV^T += dO^T.P, dK^T += Q^T.dS, 8 MFMAs with transposed LDS reads.
+// At head dim 64 a half's VALU (16 exp + 16 fma + 16 mul + 16 cvt) is as long as its 8 S/dP
+// MFMAs, and in the plain kernel it sits between them and the 8 dV/dK MFMAs that need its
+// results, so each wave alternates MFMA and VALU phases (MFMA-busy 0.40, r02d_pmc_sq). Here
+// iteration j issues C(j-1), A(j+1) and B(j) together: the 16 MFMAs have no dependence on the
+// iteration's VALU, which the scheduler spreads into their issue gaps.
+//
+// Q / dO / lse / delta tiles of 64 queries arrive by LDS-DMA (global_load_lds: no staging
+// registers, no LDS write pass) into a 3-buffer ring: one barrier per tile. At iteration 2t+1
+// tile t+1 must be resident (its DMA was issued at iteration 2t-1) and tile t-1 is no longer read,
+// so its buffer takes tile t+2's DMA.
+#include <cstdlib>
+
+#include "attention_common.h"
+#include "ltx_hip.h"
+
+namespace ltx {
+
+namespace {
+constexpr int PHD = 64;                               // head dim
+constexpr int PQT = 64;                               // queries per LDS tile
+constexpr int P_TILE = PQT * PHD * 2;                 // one [64][64] bf16 tile: 8 KiB
+constexpr int P_STAT = PQT * 4;                       // one f32 statistic per query
+constexpr int P_BUF = 2 * P_TILE + 2 * P_STAT;        // Q | dO | lse | delta
+constexpr int P_NBUF = 3;
+constexpr int P_KEYS = 128;                           // keys per workgroup (4 waves x 32)
+}  // namespace
+
+// LDS-DMA pieces in inline asm: hipcc tracks its own global_load_lds builtin as an LDS write
+// and waits vmcnt(0) before the next ds_read, which would drain the tile prefetch every
+// iteration; hidden from it, the DMA is retired only by tile_sync's explicit wait + barrier.
+// M0 (the wave-uniform LDS destination) is written in the same statement (compiler-reserved).
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p);
+}
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+
+// two f32 -> one word of two bf16 (round to nearest even): one v_cvt_pk_bf16_f32
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+template <bool BIAS>
+__global__ __launch_bounds__(256, 2) void attn_dkdv_pipe_kernel(const AttnParams p) {
+  constexpr int HD = PHD, KS = HD / 16, DS = HD / 32;
+  // ONE shared array: a second __shared__ object beside the DMA target makes hipcc wait for the
+  // DMA before unrelated LDS reads
+  __shared__ __attribute__((aligned(16))) char smem[P_NBUF * P_BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int key = bx * P_KEYS + wave * 32 + (lane & 31);
+  const int kc = min(key, p.Nk - 1);
+  const float c2 = p.scale * LOG2E;
+  float kbias = 0.f;
+  if (BIAS) {
+    kbias = -INFINITY;
+    if (key < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + key] * LOG2E : 0.f;
+  }
+
+  s16x8 kf[KS], vf[KS];  // K and -V (sign flipped: exact) of the lane's key
+  {
+    const bf16_t* kr = p.k + ((int64_t)b * p.kvb + kc) * p.ldk + hh * HD;
+    const bf16_t* vr = p.v + ((int64_t)b * p.kvb + kc) * p.ldv + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = *(const s16x8*)(kr + ks * 16 + 8 * h);
+      u32x4 w = *(const u32x4*)(vr + ks * 16 + 8 * h);
+      w ^= 0x80008000u;
+      vf[ks] = __builtin_bit_cast(s16x8, w);
+    }
+  }
+  f32x16 dka[DS], dva[DS];
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dka[d][r] = 0.f;
+      dva[d][r] = 0.f;
+    }
+
+  const bf16_t* qbase = p.q + (int64_t)b * p.Nq * p.ldq + hh * HD;
+  const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
+  const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
+  const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
+  const int ntiles = (p.Nq + PQT - 1) / PQT;
+
+  // Tile t -> buffer: wave w moves Q and dO rows 16w..16w+15 (two 1-KiB pieces of 8 rows each,
+  // the chunk swizzle applied on the source address), wave 0 the lse words, wave 1 the delta
+  // words. Rows past Nq re-read the last row (their lse is fixed to +inf below: P = 0).
+  auto dma = [&](int t, int buf) {
+    char* base = smem + buf * P_BUF;
+    const int q0 = t * PQT;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = wave * 2 + i;
+      const int row = piece * 8 + (lane >> 3);
+      const int64_t qr = min(q0 + row, p.Nq - 1);
+      const int c = (lane & 7) ^ swz<HD>(row);
+      dma16(qbase + qr * p.ldq + c * 8, lds_u32(base + piece * 1024));
+      dma16(obase + qr * p.lddo + c * 8, lds_u32(base + P_TILE + piece * 1024));
+    }
+    if (wave < 2) {
+      const float* src = (wave == 0 ? lbase : dbase) + min(q0 + lane, p.Nq - 1);
+      dma4(src, lds_u32(base + 2 * P_TILE + wave * P_STAT));
+    }
+  };
+  // after the wait that retires tile t's DMA (wave 0 issued the lse words): rows past Nq -> +inf
+  auto fix_stats = [&](int t, int buf) {
+    if (wave == 0 && t * PQT + PQT > p.Nq && t * PQT + lane >= p.Nq)
+      ((float*)(smem + buf * P_BUF + 2 * P_TILE))[lane] = INFINITY;
+  };
+
+  // A: S^T, dP'^T of half u of the tile in buffer `bf`
+  auto stage_A = [&](int bf, int u, f32x16& s, f32x16& dp) {
+    const char* qt = smem + bf * P_BUF;
+    const char* ot = qt + P_TILE;
+    const float* dl = (const float*)(qt + 2 * P_TILE + P_STAT);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 d4 = *(const f32x4*)&dl[u * 32 + 8 * g + 4 * h];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s[4 * g + i] = 0.f;
+        dp[4 * g + i] = d4[i];
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      s = mfma32(row_frag<HD>(qt, u * 32, ks, lofs), kf[ks], s);
+      dp = mfma32(row_frag<HD>(ot, u * 32, ks, lofs), vf[ks], dp);
+    }
+  };
+  // B: P and dS of half u -> bf16 B-operand fragments (k-steps 0, 1 of the 32 queries)
+  auto stage_B = [&](int bf, int u, f32x16& s, f32x16& dp, s16x8 (&pb)[2], s16x8 (&sb)[2]) {
+    const float* ls = (const float*)(smem + bf * P_BUF + 2 * P_TILE);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 l4 = *(const f32x4*)&ls[u * 32 + 8 * g + 4 * h];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * g + i;
+        const float pr = fast_exp2(fmaf(s[r], c2, BIAS ? kbias - l4[i] : -l4[i]));
+        s[r] = pr;
+        dp[r] = -(pr * dp[r]);
+      }
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      pb[ss] = acc_frag(s, ss);
+      sb[ss] = acc_frag(dp, ss);
+    }
+  };
+  // C: dV^T += dO^T.P, dK^T += Q^T.dS for half u
+  auto stage_C = [&](int bf, int u, const s16x8 (&pb)[2], const s16x8 (&sb)[2]) {
+    const char* qt = smem + bf * P_BUF;
+    const char* ot = qt + P_TILE;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int d = 0; d < DS; ++d) {
+        dva[d] = mfma32(tr_frag<HD>(ot, u * 32, ss, d, lofs), pb[ss], dva[d]);
+        dka[d] = mfma32(tr_frag<HD>(qt, u * 32, ss, d, lofs), sb[ss], dka[d]);
+      }
+  };
+  f32x16 s0, d0, s1, d1;  // S / dP' of even and odd halves
+  s16x8 pb[2], sb[2];     // P, dS of the half whose C stage is next
+  // One steady-state iteration j, hand-placed: C(j-1) from half uc of buffer bc (pb, sb in),
+  // B(j) on (sj, dj) with the lse words of half ub of buffer bb (pb, sb out), A(j+1) into
+  // (sn, dn) from half ua of buffer ba. Phase 0 issues C's transposed reads and the lse words;
+  // phase 1 pairs each C MFMA with two exponentials of B and A's operand reads; phase 2 pairs
+  // each A MFMA with two dS products and two bf16 packs of B. sched_barrier(0) pins each slot.
+  auto iteration = [&](int bc, int uc, int bb, int ub, f32x16& sj, f32x16& dj, int ba, int ua,
+                       f32x16& sn, f32x16& dn) {
+    const char* cq = smem + bc * P_BUF;
+    const char* co = cq + P_TILE;
+    const float* ls = (const float*)(smem + bb * P_BUF + 2 * P_TILE);
+    const char* aq = smem + ba * P_BUF;
+    const char* ao = aq + P_TILE;
+    const float* dl = (const float*)(aq + 2 * P_TILE + P_STAT);
+    f32x4 l4[4];  // first: slot 0's exponentials wait for them
+#pragma unroll
+    for (int g = 0; g < 4; ++g) l4[g] = *(const f32x4*)&ls[ub * 32 + 8 * g + 4 * h];
+    s16x8 to_[2][DS], tq[2][DS];  // in MFMA order
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int d = 0; d < DS; ++d) {
+        to_[ss][d] = tr_frag<HD>(co, uc * 32, ss, d, lofs);
+        tq[ss][d] = tr_frag<HD>(cq, uc * 32, ss, d, lofs);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    s16x8 qa[KS], oa[KS];
+    f32x4 d4[4];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int ss = m >> 2, d = (m >> 1) & 1;
+      if (m & 1) dka[d] = mfma32(tq[ss][d], sb[ss], dka[d]);
+      else dva[d] = mfma32(to_[ss][d], pb[ss], dva[d]);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int r = 2 * m + e;
+        const float lv = l4[r >> 2][r & 3];
+        sj[r] = fast_exp2(fmaf(sj[r], c2, BIAS ? kbias - lv : -lv));
+      }
+      if (m < 4) {
+        qa[m] = row_frag<HD>(aq, ua * 32, m, lofs);
+        oa[m] = row_frag<HD>(ao, ua * 32, m, lofs);
+      } else {
+        d4[m - 4] = *(const f32x4*)&dl[ua * 32 + 8 * (m - 4) + 4 * h];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    u32x4 pw[2], sw[2];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int ks = m >> 1;
+      if (m & 1) {
+        if (ks == 0) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dn[4 * g + i] = d4[g][i];
+        }
+        dn = mfma32(oa[ks], vf[ks], dn);
+      } else {
+        if (ks == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sn[r] = 0.f;
+        }
+        sn = mfma32(qa[ks], kf[ks], sn);
+      }
+      const int r = 2 * m;
+      dj[r] = -(sj[r] * dj[r]);
+      dj[r + 1] = -(sj[r + 1] * dj[r + 1]);
+      uint32_t wp = cvt_pk(sj[r], sj[r + 1]), ws = cvt_pk(dj[r], dj[r + 1]);
+      asm volatile("" : "+v"(wp), "+v"(ws));  // keeps the packs in this slot (not sunk to the end)
+      pw[m >> 2][m & 3] = wp;
+      sw[m >> 2][m & 3] = ws;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      pb[ss] = __builtin_bit_cast(s16x8, pw[ss]);
+      sb[ss] = __builtin_bit_cast(s16x8, sw[ss]);
+    }
+  };
+  // retire this wave's DMA, fix the ragged tile's statistics, then the workgroup barrier
+  auto tile_sync = [&](int t, int buf) {
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): DMA landed, LDS reads back
+    fix_stats(t, buf);
+    __builtin_amdgcn_s_waitcnt(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  dma(0, 0);
+  if (ntiles > 1) dma(1, 1);
+  __builtin_amdgcn_s_waitcnt(0);
+  if (ntiles > 1) fix_stats(1, 1);
+  tile_sync(0, 0);
+
+  stage_A(0, 0, s0, d0);                // A(0)
+  stage_A(0, 1, s1, d1);                // iteration 0: A(1), B(0)
+  stage_B(0, 0, s0, d0, pb, sb);
+  int b0 = 0, b1 = 1, b2 = 2;           // buffers of tiles t, t+1, t+2
+  for (int t = 0; t + 1 < ntiles; ++t) {
+    // iteration 2t+1: tile t+1 resident, tile t-1's buffer free for tile t+2
+    tile_sync(t + 1, b1);
+    if (t + 2 < ntiles) dma(t + 2, b2);
+    iteration(b0, 0, b0, 1, s1, d1, b1, 0, s0, d0);  // C(2t), B(2t+1), A(2t+2)
+    iteration(b0, 1, b1, 0, s0, d0, b1, 1, s1, d1);  // C(2t+1), B(2t+2), A(2t+3)
+    const int bt = b0;
+    b0 = b1;
+    b1 = b2;
+    b2 = bt;
+  }
+  // iteration J-1 (J = 2 ntiles): C(J-2), B(J-1); then C(J-1)
+  stage_C(b0, 0, pb, sb);
+  stage_B(b0, 1, s1, d1, pb, sb);
+  stage_C(b0, 1, pb, sb);
+
+  if (key >= p.Nk) return;
+  bf16_t* krow = p.dk + ((int64_t)b * p.Nk + key) * p.lddk + hh * HD;
+  bf16_t* vrow = p.dv + ((int64_t)b * p.Nk + key) * p.lddv + hh * HD;
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 wk, wv;
+      wk[0] = pack2(dka[d][4 * g] * p.scale, dka[d][4 * g + 1] * p.scale);
+      wk[1] = pack2(dka[d][4 * g + 2] * p.scale, dka[d][4 * g + 3] * p.scale);
+      wv[0] = pack2(dva[d][4 * g], dva[d][4 * g + 1]);
+      wv[1] = pack2(dva[d][4 * g + 2], dva[d][4 * g + 3]);
+      *(u32x2*)(krow + d * 32 + 8 * g + 4 * h) = wk;
+      *(u32x2*)(vrow + d * 32 + 8 * g + 4 * h) = wv;
+    }
+}
+
+bool dkdv_pipe_enabled() {  // LTX_ATTN_DKDV_PIPE=0: the plain dK/dV kernel (A/B switch)
+  static const int v = [] {
+    const char* e = std::getenv("LTX_ATTN_DKDV_PIPE");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+int launch_dkdv_pipe(const AttnParams& p, hipStream_t s) {
+  const dim3 g((unsigned)((p.Nk + P_KEYS - 1) / P_KEYS), (unsigned)p.H, (unsigned)p.B);
+  if (p.key_bias != nullptr || (p.Nk % 64) != 0)
+    hipLaunchKernelGGL(attn_dkdv_pipe_kernel<true>, g, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_dkdv_pipe_kernel<false>, g, dim3(256), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+}  // namespace ltx
