@@ -176,7 +176,11 @@ def _sdpa_ref(q, k, v, B, H, d, bias=None):
 @pytest.mark.parametrize("B,H,Nq,Nk,d,masked", [(2, 4, 128, 128, 64, False), (1, 3, 100, 77, 64, True),
                                                  (2, 4, 64, 4, 32, True), (2, 2, 256, 256, 32, False),
                                                  (1, 32, 1792, 256, 64, True), (2, 2, 640, 300, 64, False),
-                                                 (1, 2, 200, 520, 64, True)])
+                                                 (1, 2, 200, 520, 64, True),
+                                                 # split backward without key bias (the pipelined dQ and
+                                                 # dK/dV kernels): ragged queries, one and several key tiles
+                                                 (2, 3, 1000, 768, 64, False), (1, 2, 70, 320, 64, False),
+                                                 (1, 2, 320, 1792, 64, False)])
 def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
     from ltx_amd import ops
     scale = d ** -0.5

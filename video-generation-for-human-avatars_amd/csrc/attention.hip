@@ -1018,11 +1018,16 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   if constexpr (HD == 64) k8 = waves8_flag(1);
   dim3 gk((unsigned)(k8 ? (p.Nk + 255) / 256 : (p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   if (HD == 64 && !k8 && dkdv_pipe_enabled()) {
-    if (needs_bias(p))
+    if (needs_bias(p)) {
       hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
-    else
+      LTX_LAUNCH_CHECK();
+    } else if (dq_pipe_enabled()) {
+      const int rc = launch_dq_pipe(p, s);
+      if (rc != LTX_OK) return rc;
+    } else {
       hipLaunchKernelGGL((attn_q_kernel<HD, 1, false>), gq, dim3(ATT_THREADS), 0, s, p);
-    LTX_LAUNCH_CHECK();
+      LTX_LAUNCH_CHECK();
+    }
     return launch_dkdv_pipe(p, s);
   }
   if (needs_bias(p)) {

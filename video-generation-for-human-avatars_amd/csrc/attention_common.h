@@ -205,5 +205,8 @@ __device__ __forceinline__ void xcd_block(int xcd_order, int& bx, int& by, int& 
 // the dK/dV kernel with the software-pipelined, LDS-DMA-staged loop (attention_dkdv.hip)
 int launch_dkdv_pipe(const AttnParams& p, hipStream_t s);
 bool dkdv_pipe_enabled();
+// the dQ kernel with the same structure, for key ranges without bias (Nk % 64 == 0)
+int launch_dq_pipe(const AttnParams& p, hipStream_t s);
+bool dq_pipe_enabled();
 
 }  // namespace ltx

@@ -320,6 +320,217 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_pipe_kernel(const AttnParams
     }
 }
 
+// =============================================================================================
+// dQ (attn_q_kernel MODE 1 semantics) for self-attention shapes (no key bias, Nk % 64 == 0),
+// software pipelined the same way. A workgroup = 4 waves x 32 queries (Q, dO fragments, -lse and
+// delta of the lane's query in registers); per 32-key half j:
+//   A(j): S^T = K.Q^T and dP'^T = V.dO^T - delta (the dP chain starts from a register tuple
+//         holding -delta: no subtraction per element), 8 MFMAs;
+//   B(j): dS = exp2(S c - lse) dP' -> bf16 (16 fma + 16 exp + 16 mul + 8 cvt);
+//   C(j): dQ^T += K^T.dS^T, 4 MFMAs with transposed K reads.
+// Iteration j issues C(j-1) and A(j+1) (12 MFMAs) around B(j)'s VALU; K / V tiles of 64 keys by
+// LDS-DMA into a 3-buffer ring, one barrier per tile.
+// =============================================================================================
+namespace {
+constexpr int D_KT = 64;                        // keys per LDS tile
+constexpr int D_TILE = D_KT * PHD * 2;          // 8 KiB
+constexpr int D_BUF = 2 * D_TILE;               // K | V
+constexpr int D_QUERIES = 128;                  // queries per workgroup (4 waves x 32)
+}  // namespace
+
+__global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p) {
+  constexpr int HD = PHD, KS = HD / 16, DS = HD / 32;
+  __shared__ __attribute__((aligned(16))) char smem[P_NBUF * D_BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int qi = bx * D_QUERIES + wave * 32 + (lane & 31);
+  const int qc = min(qi, p.Nq - 1);
+  const float c2 = p.scale * LOG2E;
+
+  s16x8 qf[KS], of[KS];
+  {
+    const bf16_t* qr = p.q + ((int64_t)b * p.Nq + qc) * p.ldq + hh * HD;
+    const bf16_t* dr = p.dout + ((int64_t)b * p.Nq + qc) * p.lddo + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qf[ks] = *(const s16x8*)(qr + ks * 16 + 8 * h);
+      of[ks] = *(const s16x8*)(dr + ks * 16 + 8 * h);
+    }
+  }
+  const int64_t si = ((int64_t)b * p.H + hh) * p.Nq + qc;
+  const float nlse = -p.lse[si];
+  f32x16 ndl;  // -delta in every register: the dP' chain's initial accumulator
+  {
+    const float v = -p.delta[si];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ndl[r] = v;
+  }
+  f32x16 acc[DS];
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
+
+  const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  const bf16_t* vbase = p.v + (int64_t)b * p.kvb * p.ldv + hh * HD;
+  const int ntiles = p.Nk / D_KT;
+
+  // key tile t -> buffer: wave w moves K and V rows 16w..16w+15 (two 1-KiB pieces each)
+  auto dma = [&](int t, int buf) {
+    char* base = smem + buf * D_BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int piece = wave * 2 + i;
+      const int row = piece * 8 + (lane >> 3);
+      const int64_t kr = t * D_KT + row;
+      const int c = (lane & 7) ^ swz<HD>(row);
+      dma16(kbase + kr * p.ldk + c * 8, lds_u32(base + piece * 1024));
+      dma16(vbase + kr * p.ldv + c * 8, lds_u32(base + D_TILE + piece * 1024));
+    }
+  };
+  auto tile_sync = [&]() {
+    __builtin_amdgcn_s_waitcnt(0);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto stage_A = [&](int bf, int u, f32x16& s, f32x16& dp) {
+    const char* kt = smem + bf * D_BUF;
+    const char* vt = kt + D_TILE;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      s = mfma32(row_frag<HD>(kt, u * 32, ks, lofs), qf[ks], ks == 0 ? f32x16{} : s);
+      dp = mfma32(row_frag<HD>(vt, u * 32, ks, lofs), of[ks], ks == 0 ? ndl : dp);
+    }
+  };
+  s16x8 sbf[2];  // dS of the half whose C stage is next
+  auto stage_B = [&](f32x16& s, f32x16& dp) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dp[r] = fast_exp2(fmaf(s[r], c2, nlse)) * dp[r];
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) sbf[ss] = acc_frag(dp, ss);
+  };
+  auto stage_C = [&](int bf, int u) {
+    const char* kt = smem + bf * D_BUF;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(kt, u * 32, ss, d, lofs), sbf[ss], acc[d]);
+  };
+  // steady-state iteration j, hand-placed: C(j-1) from half uc of buffer bc, B(j) on (sj, dj),
+  // A(j+1) into (sn, dn) from half ua of buffer ba
+  auto iteration = [&](int bc, int uc, f32x16& sj, f32x16& dj, int ba, int ua, f32x16& sn, f32x16& dn) {
+    const char* ck = smem + bc * D_BUF;
+    const char* ak = smem + ba * D_BUF;
+    const char* av = ak + D_TILE;
+    s16x8 tk[2][DS];
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int d = 0; d < DS; ++d) tk[ss][d] = tr_frag<HD>(ck, uc * 32, ss, d, lofs);
+    __builtin_amdgcn_sched_barrier(0);
+    s16x8 ka[KS], va[KS];
+    u32x4 sw[2];
+#pragma unroll
+    for (int m = 0; m < 12; ++m) {
+      if (m < 4) {
+        acc[m & 1] = mfma32(tk[m >> 1][m & 1], sbf[m >> 1], acc[m & 1]);
+        ka[m] = row_frag<HD>(ak, ua * 32, m, lofs);
+        va[m] = row_frag<HD>(av, ua * 32, m, lofs);
+      } else {
+        const int ks = (m - 4) >> 1;
+        if (m & 1) dn = mfma32(va[ks], of[ks], ks == 0 ? ndl : dn);
+        else sn = mfma32(ka[ks], qf[ks], ks == 0 ? f32x16{} : sn);
+      }
+      if (m < 8) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int r = 2 * m + e;
+          sj[r] = fast_exp2(fmaf(sj[r], c2, nlse));
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int w = 2 * (m - 8) + e, r = 2 * w;
+          dj[r] = sj[r] * dj[r];
+          dj[r + 1] = sj[r + 1] * dj[r + 1];
+          uint32_t ws = cvt_pk(dj[r], dj[r + 1]);
+          asm volatile("" : "+v"(ws));
+          sw[w >> 2][w & 3] = ws;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) sbf[ss] = __builtin_bit_cast(s16x8, sw[ss]);
+  };
+
+  dma(0, 0);
+  if (ntiles > 1) dma(1, 1);
+  tile_sync();
+  f32x16 s0, d0, s1, d1;
+  stage_A(0, 0, s0, d0);                // A(0)
+  stage_A(0, 1, s1, d1);                // iteration 0: A(1), B(0)
+  stage_B(s0, d0);
+  int b0 = 0, b1 = 1, b2 = 2;
+  for (int t = 0; t + 1 < ntiles; ++t) {
+    tile_sync();
+    if (t + 2 < ntiles) dma(t + 2, b2);
+    iteration(b0, 0, s1, d1, b1, 0, s0, d0);  // C(2t), B(2t+1), A(2t+2)
+    iteration(b0, 1, s0, d0, b1, 1, s1, d1);  // C(2t+1), B(2t+2), A(2t+3)
+    const int bt = b0;
+    b0 = b1;
+    b1 = b2;
+    b2 = bt;
+  }
+  stage_C(b0, 0);                       // C(J-2)
+  stage_B(s1, d1);                      // B(J-1)
+  stage_C(b0, 1);                       // C(J-1)
+
+  if (qi >= p.Nq) return;
+  if (p.dq_f32) {
+    float* qrow = (float*)p.dq + ((int64_t)b * p.Nq + qi) * p.lddq + hh * HD;
+#pragma unroll
+    for (int d = 0; d < DS; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 w = {acc[d][4 * g] * p.scale, acc[d][4 * g + 1] * p.scale, acc[d][4 * g + 2] * p.scale,
+                   acc[d][4 * g + 3] * p.scale};
+        *(f32x4*)(qrow + d * 32 + 8 * g + 4 * h) = w;
+      }
+  } else {
+    bf16_t* qrow = (bf16_t*)p.dq + ((int64_t)b * p.Nq + qi) * p.lddq + hh * HD;
+#pragma unroll
+    for (int d = 0; d < DS; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        u32x2 w;
+        w[0] = pack2(acc[d][4 * g] * p.scale, acc[d][4 * g + 1] * p.scale);
+        w[1] = pack2(acc[d][4 * g + 2] * p.scale, acc[d][4 * g + 3] * p.scale);
+        *(u32x2*)(qrow + d * 32 + 8 * g + 4 * h) = w;
+      }
+  }
+}
+
+bool dq_pipe_enabled() {  // LTX_ATTN_DQ_PIPE=0: the plain dQ kernel (A/B switch)
+  static const int v = [] {
+    const char* e = std::getenv("LTX_ATTN_DQ_PIPE");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v != 0;
+}
+
+int launch_dq_pipe(const AttnParams& p, hipStream_t s) {
+  const dim3 g((unsigned)((p.Nq + D_QUERIES - 1) / D_QUERIES), (unsigned)p.H, (unsigned)p.B);
+  hipLaunchKernelGGL(attn_dq_pipe_kernel, g, dim3(256), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
 bool dkdv_pipe_enabled() {  // LTX_ATTN_DKDV_PIPE=0: the plain dK/dV kernel (A/B switch)
   static const int v = [] {
     const char* e = std::getenv("LTX_ATTN_DKDV_PIPE");
