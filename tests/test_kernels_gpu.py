@@ -280,6 +280,7 @@ def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
     monkeypatch.setenv("LTX_ATTN_FWD1", "1")
     o1, l1 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)
     monkeypatch.setenv("LTX_ATTN_FWD1", "0")
+    monkeypatch.setenv("LTX_ATTN_FWD_PIPE", "0")  # the tiled kernel whose arithmetic fwd1 mirrors
     o0, l0 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)
     assert torch.equal(o1, o0)
     assert torch.equal(l1, l0)

@@ -973,6 +973,7 @@ static int launch_fwd(AttnParams p, hipStream_t s) {
     }
   }
   if constexpr (HD == 64) {
+    if (!needs_bias(p) && fwd_pipe_enabled()) return launch_fwd_pipe(p, s);
     if (waves8_flag(0)) {
       dim3 grid((unsigned)((p.Nq + 255) / 256), (unsigned)p.H, (unsigned)p.B);
       if (needs_bias(p))

@@ -517,10 +517,8 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
 }
 
 bool dq_pipe_enabled() {  // LTX_ATTN_DQ_PIPE=0: the plain dQ kernel (A/B switch)
-  static const int v = [] {
-    const char* e = std::getenv("LTX_ATTN_DQ_PIPE");
-    return e ? std::atoi(e) : 1;
-  }();
+  const char* e = std::getenv("LTX_ATTN_DQ_PIPE");  // read per call: tests compare paths in one process
+  const int v = e ? std::atoi(e) : 1;
   return v != 0;
 }
 
@@ -531,11 +529,192 @@ int launch_dq_pipe(const AttnParams& p, hipStream_t s) {
   return LTX_OK;
 }
 
+// =============================================================================================
+// Forward for self-attention shapes (no key bias, Nk % 64 == 0): attn_q_kernel<64, 0, false, 8>'s
+// arithmetic (8 waves x 32 queries, K/V tiles of 64 keys, speculative probabilities at the running
+// max, deferred rescale) in 32-key sub-tiles, with the K / V tiles brought by LDS-DMA into a
+// 3-buffer ring: no staging registers, no LDS write pass, one barrier per tile instead of two.
+// Barrier t: every wave has finished tile t-1 (whose buffer then takes tile t+2's DMA) and has
+// retired its DMA of tile t+1 (issued after barrier t-1).
+// =============================================================================================
+namespace {
+constexpr int F_KT = 64;
+constexpr int F_TILE = F_KT * PHD * 2;  // 8 KiB
+constexpr int F_BUF = 2 * F_TILE;       // K | V
+constexpr int F_QUERIES = 256;          // 8 waves x 32
+}  // namespace
+
+template <bool STAGGER>
+__global__ __launch_bounds__(512, 2) void attn_fwd_pipe_kernel(const AttnParams p) {
+  constexpr int HD = PHD, KS = HD / 16, DS = HD / 32;
+  __shared__ __attribute__((aligned(16))) char smem[P_NBUF * F_BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int qi = bx * F_QUERIES + wave * 32 + (lane & 31);
+  const int qc = min(qi, p.Nq - 1);
+  const float c2 = p.scale * LOG2E;
+
+  s16x8 qf[KS];
+  {
+    const bf16_t* qr = p.q + ((int64_t)b * p.Nq + qc) * p.ldq + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *(const s16x8*)(qr + ks * 16 + 8 * h);
+  }
+  f32x16 acc[DS];
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;
+
+  const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  const bf16_t* vbase = p.v + (int64_t)b * p.kvb * p.ldv + hh * HD;
+  const int ntiles = p.Nk / F_KT;
+  // key tile t -> buffer: wave w moves K rows 8w..8w+7 and V rows 8w..8w+7 (one piece each)
+  auto dma = [&](int t, int buf) {
+    char* base = smem + buf * F_BUF;
+    const int row = wave * 8 + (lane >> 3);
+    const int64_t kr = t * F_KT + row;
+    const int c = (lane & 7) ^ swz<HD>(row);
+    dma16(kbase + kr * p.ldk + c * 8, lds_u32(base + wave * 1024));
+    dma16(vbase + kr * p.ldv + c * 8, lds_u32(base + F_TILE + wave * 1024));
+  };
+  auto barrier = [&]() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // barrier t: this wave's DMA of tile t+1 (issued after barrier t-1) retired first; after it,
+  // every wave is done with tile t-1, whose buffer takes tile t+2
+  auto sync = [&](int t) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    barrier();
+    if (t + 2 < ntiles) dma(t + 2, (t + 2) % P_NBUF);
+  };
+  __builtin_amdgcn_s_waitcnt(0);  // the Q fragments: no ordinary load stays pending in the loop
+  dma(0, 0);
+  if (ntiles > 1) dma(1, 1);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  barrier();
+
+  // one 32-key sub-tile (half u of the tile in kt / vt): S^T, speculative probabilities at the
+  // running max (the deferred-max rule when a lane's sum exceeds 2^TAU), O^T += V^T.P^T
+  bool first = true;
+  auto subtile = [&](const char* kt, const char* vt, int u) {
+    f32x16 s;
+    float ls[4];
+    auto scores = [&]() {
+      int z = 0;  // opaque: K fragment reads stay inside the pass loop (see attn_q_kernel)
+      asm volatile("" : "+s"(z));
+      const char* k2 = kt + z;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s = mfma32(row_frag<HD>(k2, u * 32, ks, lofs), qf[ks], s);
+    };
+    auto probs = [&]() {
+      const float nm = -m_run;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ls[i] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = fast_exp2(fmaf(s[r], c2, nm));
+        s[r] = e;
+        ls[r & 3] += e;
+      }
+    };
+    float alpha = 1.f;
+    bool rescale = false;
+#pragma unroll 1
+    for (int pass = first; pass < 2; ++pass) {
+      scores();
+      if (pass) {
+        float mr[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mr[r & 3] = fmaxf(mr[r & 3], s[r]);
+        const float mt = xor32_max(fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3])) * c2);
+        const float m_new = fmaxf(m_run, mt);
+        if (__any(m_new > m_run + RESCALE_TAU)) {
+          alpha = fast_exp2(m_run - m_new);
+          rescale = true;
+          m_run = m_new;
+        }
+      }
+      probs();
+      if (pass || !__any(((ls[0] + ls[1]) + (ls[2] + ls[3])) > RESCALE_SUM)) break;
+    }
+    first = false;
+    if (rescale) {
+      l_run *= alpha;
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[d][r] *= alpha;
+    }
+    l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const s16x8 pb = acc_frag(s, ss);
+#pragma unroll
+      for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vt, u * 32, ss, d, lofs), pb, acc[d]);
+    }
+  };
+
+  // STAGGER: waves 4-7 run half a tile behind waves 0-3 (barrier t sits mid-tile t for the leaders
+  // and at the start of tile t for the laggards), so on each SIMD one wave's softmax VALU meets
+  // the other's MFMAs instead of both waves reaching each phase together
+  const bool lead = !STAGGER || wave < 4;
+  for (int t = 0; t < ntiles; ++t) {
+    const char* kt = smem + (t % P_NBUF) * F_BUF;
+    const char* vt = kt + F_TILE;
+    if (!lead) sync(t);
+    subtile(kt, vt, 0);
+    if (lead) sync(t);
+    subtile(kt, vt, 1);
+  }
+
+  if (qi >= p.Nq) return;
+  const float l_tot = xor32_sum(l_run);
+  const float inv = 1.0f / l_tot;
+  bf16_t* orow = p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD;
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 w;
+      w[0] = pack2(acc[d][4 * g] * inv, acc[d][4 * g + 1] * inv);
+      w[1] = pack2(acc[d][4 * g + 2] * inv, acc[d][4 * g + 3] * inv);
+      *(u32x2*)(orow + d * 32 + 8 * g + 4 * h) = w;
+    }
+  if (h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
+}
+
+// LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8>; 1: the DMA-ring kernel; 2: the same with
+// waves 4-7 staggered by half a tile (default)
+static int fwd_pipe_mode() {
+  const char* e = std::getenv("LTX_ATTN_FWD_PIPE");  // read per call: tests compare paths in one process
+  const int v = e ? std::atoi(e) : 2;
+  return v;
+}
+bool fwd_pipe_enabled() { return fwd_pipe_mode() != 0; }
+
+int launch_fwd_pipe(const AttnParams& p, hipStream_t s) {
+  const dim3 g((unsigned)((p.Nq + F_QUERIES - 1) / F_QUERIES), (unsigned)p.H, (unsigned)p.B);
+  if (fwd_pipe_mode() == 1)
+    hipLaunchKernelGGL(attn_fwd_pipe_kernel<false>, g, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_fwd_pipe_kernel<true>, g, dim3(512), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
 bool dkdv_pipe_enabled() {  // LTX_ATTN_DKDV_PIPE=0: the plain dK/dV kernel (A/B switch)
-  static const int v = [] {
-    const char* e = std::getenv("LTX_ATTN_DKDV_PIPE");
-    return e ? std::atoi(e) : 1;
-  }();
+  const char* e = std::getenv("LTX_ATTN_DKDV_PIPE");  // read per call: tests compare paths in one process
+  const int v = e ? std::atoi(e) : 1;
   return v != 0;
 }
 
