@@ -46,6 +46,12 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
+// scalar-base form: per-lane 32-bit byte offset + wave-uniform 64-bit base (no per-lane 64-bit math)
+__device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
 __device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds) {
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -110,17 +116,27 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_pipe_kernel(const AttnParams
   // Tile t -> buffer: wave w moves Q and dO rows 16w..16w+15 (two 1-KiB pieces of 8 rows each,
   // the chunk swizzle applied on the source address), wave 0 the lse words, wave 1 the delta
   // words. Rows past Nq re-read the last row (their lse is fixed to +inf below: P = 0).
+  // per-lane byte offsets inside a tile (constant but for the ragged last tile), scalar tile bases
+  uint32_t qoff[2], ooff[2];
+  auto set_offsets = [&](int nrows) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wave * 2 + i) * 8 + (lane >> 3);
+      const int rr = min(row, nrows - 1), c = (lane & 7) ^ swz<HD>(row);
+      qoff[i] = (uint32_t)(rr * p.ldq + c * 8) * 2;
+      ooff[i] = (uint32_t)(rr * p.lddo + c * 8) * 2;
+    }
+  };
+  set_offsets(PQT);
   auto dma = [&](int t, int buf) {
     char* base = smem + buf * P_BUF;
     const int q0 = t * PQT;
+    if (q0 + PQT > p.Nq) set_offsets(p.Nq - q0);  // the ragged last tile (its DMA is the last)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int piece = wave * 2 + i;
-      const int row = piece * 8 + (lane >> 3);
-      const int64_t qr = min(q0 + row, p.Nq - 1);
-      const int c = (lane & 7) ^ swz<HD>(row);
-      dma16(qbase + qr * p.ldq + c * 8, lds_u32(base + piece * 1024));
-      dma16(obase + qr * p.lddo + c * 8, lds_u32(base + P_TILE + piece * 1024));
+      dma16s(qoff[i], qbase + (int64_t)q0 * p.ldq, lds_u32(base + piece * 1024));
+      dma16s(ooff[i], obase + (int64_t)q0 * p.lddo, lds_u32(base + P_TILE + piece * 1024));
     }
     if (wave < 2) {
       const float* src = (wave == 0 ? lbase : dbase) + min(q0 + lane, p.Nq - 1);
@@ -380,16 +396,20 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
   const int ntiles = p.Nk / D_KT;
 
   // key tile t -> buffer: wave w moves K and V rows 16w..16w+15 (two 1-KiB pieces each)
+  uint32_t koff[2], voff[2];  // per-lane byte offsets inside a key tile (same for every tile)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
+    koff[i] = (uint32_t)(row * p.ldk + c * 8) * 2;
+    voff[i] = (uint32_t)(row * p.ldv + c * 8) * 2;
+  }
   auto dma = [&](int t, int buf) {
     char* base = smem + buf * D_BUF;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int piece = wave * 2 + i;
-      const int row = piece * 8 + (lane >> 3);
-      const int64_t kr = t * D_KT + row;
-      const int c = (lane & 7) ^ swz<HD>(row);
-      dma16(kbase + kr * p.ldk + c * 8, lds_u32(base + piece * 1024));
-      dma16(vbase + kr * p.ldv + c * 8, lds_u32(base + D_TILE + piece * 1024));
+      dma16s(koff[i], kbase + (int64_t)t * D_KT * p.ldk, lds_u32(base + piece * 1024));
+      dma16s(voff[i], vbase + (int64_t)t * D_KT * p.ldv, lds_u32(base + D_TILE + piece * 1024));
     }
   };
   auto tile_sync = [&]() {
@@ -532,10 +552,10 @@ int launch_dq_pipe(const AttnParams& p, hipStream_t s) {
 // =============================================================================================
 // Forward for self-attention shapes (no key bias, Nk % 64 == 0): attn_q_kernel<64, 0, false, 8>'s
 // arithmetic (8 waves x 32 queries, K/V tiles of 64 keys, speculative probabilities at the running
-// max, deferred rescale) in 32-key sub-tiles, with the K / V tiles brought by LDS-DMA into a
-// 3-buffer ring: no staging registers, no LDS write pass, one barrier per tile instead of two.
-// Barrier t: every wave has finished tile t-1 (whose buffer then takes tile t+2's DMA) and has
-// retired its DMA of tile t+1 (issued after barrier t-1).
+// max, deferred rescale) with the K / V tiles brought by LDS-DMA into a 3-buffer ring: no staging
+// registers, no LDS write pass, one barrier per tile instead of two (-2 % in tools/attn_bench.py).
+// Measured and not kept: 32-key sub-tiles with waves 4-7 staggered half a tile behind waves 0-3
+// (neutral to +3 %).
 // =============================================================================================
 namespace {
 constexpr int F_KT = 64;
@@ -544,8 +564,7 @@ constexpr int F_BUF = 2 * F_TILE;       // K | V
 constexpr int F_QUERIES = 256;          // 8 waves x 32
 }  // namespace
 
-template <bool STAGGER>
-__global__ __launch_bounds__(512, 2) void attn_fwd_pipe_kernel(const AttnParams p) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void attn_fwd_pipe_kernel(const AttnParams p) {
   constexpr int HD = PHD, KS = HD / 16, DS = HD / 32;
   __shared__ __attribute__((aligned(16))) char smem[P_NBUF * F_BUF];
 
@@ -574,68 +593,74 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_pipe_kernel(const AttnParams 
   const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
   const bf16_t* vbase = p.v + (int64_t)b * p.kvb * p.ldv + hh * HD;
   const int ntiles = p.Nk / F_KT;
-  // key tile t -> buffer: wave w moves K rows 8w..8w+7 and V rows 8w..8w+7 (one piece each)
+  // key tile t -> buffer: wave w moves K rows 8w..8w+7 and V rows 8w..8w+7 (one piece each); a
+  // lane's byte offset inside a tile is the same for every tile, the tile base is scalar
+  const int drow = wave * 8 + (lane >> 3), dchunk = (lane & 7) ^ swz<HD>(drow);
+  const uint32_t koff = (uint32_t)(drow * p.ldk + dchunk * 8) * 2, voff = (uint32_t)(drow * p.ldv + dchunk * 8) * 2;
   auto dma = [&](int t, int buf) {
-    char* base = smem + buf * F_BUF;
-    const int row = wave * 8 + (lane >> 3);
-    const int64_t kr = t * F_KT + row;
-    const int c = (lane & 7) ^ swz<HD>(row);
-    dma16(kbase + kr * p.ldk + c * 8, lds_u32(base + wave * 1024));
-    dma16(vbase + kr * p.ldv + c * 8, lds_u32(base + F_TILE + wave * 1024));
+    const uint32_t base = lds_u32(smem + buf * F_BUF + wave * 1024);
+    dma16s(koff, kbase + (int64_t)t * F_KT * p.ldk, base);
+    dma16s(voff, vbase + (int64_t)t * F_KT * p.ldv, base + F_TILE);
   };
   auto barrier = [&]() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   };
-  // barrier t: this wave's DMA of tile t+1 (issued after barrier t-1) retired first; after it,
-  // every wave is done with tile t-1, whose buffer takes tile t+2
+  // barrier before tile t: this wave's DMA of tile t retired (issued two tiles ago; tile t+1's, issued
+  // one tile ago, stays in flight), every wave done with tile t-1, whose buffer then takes tile t+2
   auto sync = [&](int t) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (t + 1 < ntiles) __builtin_amdgcn_s_waitcnt(0x0F72);  // vmcnt(2)
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
     barrier();
     if (t + 2 < ntiles) dma(t + 2, (t + 2) % P_NBUF);
   };
   __builtin_amdgcn_s_waitcnt(0);  // the Q fragments: no ordinary load stays pending in the loop
   dma(0, 0);
   if (ntiles > 1) dma(1, 1);
-  __builtin_amdgcn_s_waitcnt(0x0F70);
-  barrier();
+  sync(0);
 
-  // one 32-key sub-tile (half u of the tile in kt / vt): S^T, speculative probabilities at the
-  // running max (the deferred-max rule when a lane's sum exceeds 2^TAU), O^T += V^T.P^T
-  bool first = true;
-  auto subtile = [&](const char* kt, const char* vt, int u) {
-    f32x16 s;
-    float ls[4];
+  f32x16 s[2];
+  float ls[4];
+  for (int t = 0; t < ntiles; ++t) {
+    const char* kt = smem + (t % P_NBUF) * F_BUF;
+    const char* vt = kt + F_TILE;
     auto scores = [&]() {
       int z = 0;  // opaque: K fragment reads stay inside the pass loop (see attn_q_kernel)
       asm volatile("" : "+s"(z));
       const char* k2 = kt + z;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) s = mfma32(row_frag<HD>(k2, u * 32, ks, lofs), qf[ks], s);
+        for (int r = 0; r < 16; ++r) s[u][r] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(k2, u * 32, ks, lofs), qf[ks], s[u]);
+      }
     };
     auto probs = [&]() {
       const float nm = -m_run;
 #pragma unroll
       for (int i = 0; i < 4; ++i) ls[i] = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = fast_exp2(fmaf(s[r], c2, nm));
-        s[r] = e;
-        ls[r & 3] += e;
-      }
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float e = fast_exp2(fmaf(s[u][r], c2, nm));
+          s[u][r] = e;
+          ls[r & 3] += e;
+        }
     };
     float alpha = 1.f;
     bool rescale = false;
 #pragma unroll 1
-    for (int pass = first; pass < 2; ++pass) {
+    for (int pass = (t == 0); pass < 2; ++pass) {
       scores();
       if (pass) {
         float mr[4] = {-3.0e38f, -3.0e38f, -3.0e38f, -3.0e38f};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mr[r & 3] = fmaxf(mr[r & 3], s[r]);
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mr[r & 3] = fmaxf(mr[r & 3], s[u][r]);
         const float mt = xor32_max(fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3])) * c2);
         const float m_new = fmaxf(m_run, mt);
         if (__any(m_new > m_run + RESCALE_TAU)) {
@@ -647,7 +672,6 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_pipe_kernel(const AttnParams 
       probs();
       if (pass || !__any(((ls[0] + ls[1]) + (ls[2] + ls[3])) > RESCALE_SUM)) break;
     }
-    first = false;
     if (rescale) {
       l_run *= alpha;
 #pragma unroll
@@ -657,24 +681,14 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_pipe_kernel(const AttnParams 
     }
     l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
 #pragma unroll
-    for (int ss = 0; ss < 2; ++ss) {
-      const s16x8 pb = acc_frag(s, ss);
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vt, u * 32, ss, d, lofs), pb, acc[d]);
-    }
-  };
-
-  // STAGGER: waves 4-7 run half a tile behind waves 0-3 (barrier t sits mid-tile t for the leaders
-  // and at the start of tile t for the laggards), so on each SIMD one wave's softmax VALU meets
-  // the other's MFMAs instead of both waves reaching each phase together
-  const bool lead = !STAGGER || wave < 4;
-  for (int t = 0; t < ntiles; ++t) {
-    const char* kt = smem + (t % P_NBUF) * F_BUF;
-    const char* vt = kt + F_TILE;
-    if (!lead) sync(t);
-    subtile(kt, vt, 0);
-    if (lead) sync(t);
-    subtile(kt, vt, 1);
+      for (int ss = 0; ss < 2; ++ss) {
+        const s16x8 pb = acc_frag(s[u], ss);
+#pragma unroll
+        for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vt, u * 32, ss, d, lofs), pb, acc[d]);
+      }
+    if (t + 1 < ntiles) sync(t + 1);
   }
 
   if (qi >= p.Nq) return;
@@ -693,21 +707,15 @@ __global__ __launch_bounds__(512, 2) void attn_fwd_pipe_kernel(const AttnParams 
   if (h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
 }
 
-// LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8>; 1: the DMA-ring kernel; 2: the same with
-// waves 4-7 staggered by half a tile (default)
-static int fwd_pipe_mode() {
+bool fwd_pipe_enabled() {  // LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8> (A/B switch)
   const char* e = std::getenv("LTX_ATTN_FWD_PIPE");  // read per call: tests compare paths in one process
-  const int v = e ? std::atoi(e) : 2;
-  return v;
+  const int v = e ? std::atoi(e) : 1;
+  return v != 0;
 }
-bool fwd_pipe_enabled() { return fwd_pipe_mode() != 0; }
 
 int launch_fwd_pipe(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nq + F_QUERIES - 1) / F_QUERIES), (unsigned)p.H, (unsigned)p.B);
-  if (fwd_pipe_mode() == 1)
-    hipLaunchKernelGGL(attn_fwd_pipe_kernel<false>, g, dim3(512), 0, s, p);
-  else
-    hipLaunchKernelGGL(attn_fwd_pipe_kernel<true>, g, dim3(512), 0, s, p);
+  hipLaunchKernelGGL(attn_fwd_pipe_kernel, g, dim3(512), 0, s, p);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
