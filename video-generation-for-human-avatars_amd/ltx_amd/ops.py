@@ -297,6 +297,12 @@ def qk_norm_rope_bwd(dq, q_raw, q_w, rq, dk=None, k_raw=None, k_w=None, rk=None,
 # ---------------------------------------------------------------------------------------------
 # attention
 # ---------------------------------------------------------------------------------------------
+def _env_on(var):
+    """A/B switch the library reads per call (attention_pipe.hip): unset or non-zero = on."""
+    v = os.environ.get(var)
+    return v is None or v.strip() not in ("0", "")
+
+
 def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
     """q [B*Nq, >=H*d] row view, k/v [B*Nk, ...] -> (o [B*Nq, H*d], lse [B,H,Nq] f32 log2).
     kv_shared: k/v/key_bias hold ONE batch ([Nk, ...], [1, Nk]) attended by every query batch."""
@@ -307,6 +313,8 @@ def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
     bias = "true" if (key_bias is not None or Nk % 64) else "false"
     if d == 64 and Nk <= 256 and os.environ.get("LTX_ATTN_FWD1", "1") != "0":
         label = f"attention forward: ltx::attn_fwd1_kernel<{d}, {bias}>"  # K/V staged once
+    elif d == 64 and bias == "false" and _env_on("LTX_ATTN_FWD_PIPE"):  # attention_pipe.hip
+        label = "attention forward: ltx::attn_fwd_pipe_kernel"
     elif d == 64 and int(os.environ.get("LTX_ATTN_W8", "1")) & 1:  # 8 waves x 32 queries
         label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}, 8>"
     else:
@@ -342,6 +350,11 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
         # every key in one workgroup: the one-pass kernel (attention.hip attn_bwd1_kernel)
         b1 = "true" if (key_bias is not None or Nk != 256) else "false"
         kern = f"ltx::attn_bwd1_kernel<{d}, {b1}>"
+    elif d == 64 and _env_on("LTX_ATTN_DKDV_PIPE"):  # the pipelined kernels (attention_pipe.hip)
+        kb = "true" if (key_bias is not None or Nk % 64) else "false"
+        dqk = ("ltx::attn_dq_pipe_kernel" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
+               else f"ltx::attn_q_kernel<{d}, 1, {kb}, 4>")
+        kern = f"ltx::attn_dkdv_pipe_kernel<{kb}> + {dqk}"
     else:
         kern = f"ltx::attn_dkdv_kernel<{d}, {bias}, 4> + ltx::attn_q_kernel<{d}, 1, {bias}, 4>"
     label = ("attention backward: " + ("" if ready else f"ltx::attn_delta_kernel<{d}> + ") + kern)
