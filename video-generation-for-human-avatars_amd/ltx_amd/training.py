@@ -23,12 +23,24 @@ from . import ops
 from .patchifier import SymmetricPatchifier
 
 
+_LOGN_PARAMS = {}  # (mu, sigma, device) -> the LogNormal's 0-dim device loc / scale
+
+
 def sample_timesteps(batch, config, device):
-    """training.py:124-132."""
+    """training.py:124-132. The same LogNormal draw as the reference, without its two host syncs
+    per micro-step: torch.tensor(x, device=cuda) is a blocking H2D copy (PyTorch synchronises the
+    stream after it) and the distribution's argument validation reads a device bool back. Both
+    drained the device queue at the top of every step, so the step prologue ran host-bound with
+    the GPU idle. The 0-dim loc / scale are built once per (mu, sigma, device) and the
+    distribution skips validation (its arguments are finite constants)."""
     mu = config.rf_log_normal_mu if config.rf_log_normal_mu is not None else 0.0
     sigma = config.rf_log_normal_sigma if config.rf_log_normal_sigma is not None else 1.0
-    logn = torch.distributions.LogNormal(torch.tensor(mu, device=device),
-                                         torch.tensor(sigma, device=device))
+    key = (float(mu), float(sigma), str(torch.device(device)))
+    params = _LOGN_PARAMS.get(key)
+    if params is None:
+        params = (torch.tensor(mu, device=device), torch.tensor(sigma, device=device))
+        _LOGN_PARAMS[key] = params
+    logn = torch.distributions.LogNormal(params[0], params[1], validate_args=False)
     raw = logn.sample((batch,))
     t_raw = raw / (1 + raw)
     t_low = torch.quantile(t_raw, config.rf_quantile_min)
