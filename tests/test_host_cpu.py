@@ -513,3 +513,23 @@ def test_zero2_gloo_world2_matches_single_process_math():
             assert (res[r][i] != e).float().mean() < 0.02, (r, i)  # bf16 ulp flips only
     for i in range(len(expect)):
         assert torch.equal(res[0][i], res[1][i])  # every rank holds the same weights
+
+
+def test_sample_timesteps_is_the_lognormal_draw_bitwise():
+    """train_step's timestep draw writes LogNormal(mu, sigma).sample((B,)) out (normal_(0, 1),
+    mul_(sigma), add_(mu), exp) to avoid the distribution's host syncs; it must stay the same draw
+    and the same roundings as the reference's (training.py:124-132)."""
+    from ltx_amd.training import sample_timesteps
+
+    class C:
+        rf_log_normal_mu, rf_log_normal_sigma = -0.5, 1.0
+        rf_quantile_min, rf_quantile_max = 0.01, 0.99
+
+    for seed in (0, 7, 123):
+        torch.manual_seed(seed)
+        a = sample_timesteps(16, C, "cpu")
+        torch.manual_seed(seed)
+        raw = torch.distributions.LogNormal(torch.tensor(-0.5), torch.tensor(1.0)).sample((16,))
+        t = raw / (1 + raw)
+        b = t.clamp(min=float(torch.quantile(t, 0.01)), max=float(torch.quantile(t, 0.99)))
+        assert torch.equal(a, b)

@@ -199,6 +199,9 @@ def layernorm_modulate_bwd(dy, x, mean, rstd, onep, ld_mod, rows_per_batch):
     return dx
 
 
+_ROPE_OMEGA = {}  # (dim, theta, device) -> the f32 device frequency vector
+
+
 class RopeSpec:
     """Per-forward RoPE state: the bf16 cos/sin table of precompute_freqs_cis
     (transformer3d.py:209-277), built once on the device by ltx_rope_table and read by every
@@ -219,10 +222,16 @@ class RopeSpec:
         if self.is_float and grid.dtype != F32:
             grid = grid.to(F32)
         self.grid = grid
-        idx = theta ** torch.linspace(math.log(1, theta), math.log(theta, theta), dim // 6,
-                                      dtype=torch.float32)
-        idx = idx.to(torch.float32) * math.pi / 2
-        self.omega = idx.to(indices_grid.device)
+        # the frequency vector is built on the host once per (dim, theta, device): a blocking
+        # H2D copy per forward would drain the device queue (PyTorch syncs the stream after it)
+        key = (dim, float(theta), str(indices_grid.device))
+        omega = _ROPE_OMEGA.get(key)
+        if omega is None:
+            idx = theta ** torch.linspace(math.log(1, theta), math.log(theta, theta), dim // 6,
+                                          dtype=torch.float32)
+            idx = idx.to(torch.float32) * math.pi / 2
+            omega = _ROPE_OMEGA[key] = idx.to(indices_grid.device)
+        self.omega = omega
         self.max_pos = [float(m) for m in max_pos]
         bt = grid.shape[0]
         self.cs_batch_rows = 0 if shared else self.N

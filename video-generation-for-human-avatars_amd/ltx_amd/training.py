@@ -27,12 +27,15 @@ _LOGN_PARAMS = {}  # (mu, sigma, device) -> the LogNormal's 0-dim device loc / s
 
 
 def sample_timesteps(batch, config, device):
-    """training.py:124-132. The same LogNormal draw as the reference, without its two host syncs
-    per micro-step: torch.tensor(x, device=cuda) is a blocking H2D copy (PyTorch synchronises the
-    stream after it) and the distribution's argument validation reads a device bool back. Both
-    drained the device queue at the top of every step, so the step prologue ran host-bound with
-    the GPU idle. The 0-dim loc / scale are built once per (mu, sigma, device) and the
-    distribution skips validation (its arguments are finite constants)."""
+    """training.py:124-132: LogNormal(mu, sigma).sample((B,)) -> r/(1+r) -> batch-quantile clamp.
+
+    The draw is the distribution's own arithmetic written out, without its three host syncs per
+    micro-step (each drains the device queue, so the step prologue then ran host-bound with the
+    GPU idle): torch.tensor(x, device=cuda) is a blocking H2D copy, the distribution validates
+    its arguments by reading a device bool back, and torch.normal(mean, std) checks
+    std.min() >= 0 with .item(). torch.normal(mean, std) is normal_(0, 1) on its output, then
+    output.mul_(std).add_(mean) (ATen normal_out_impl), and LogNormal.sample exponentiates it:
+    the same generator draw and the same f32 roundings here."""
     mu = config.rf_log_normal_mu if config.rf_log_normal_mu is not None else 0.0
     sigma = config.rf_log_normal_sigma if config.rf_log_normal_sigma is not None else 1.0
     key = (float(mu), float(sigma), str(torch.device(device)))
@@ -40,8 +43,9 @@ def sample_timesteps(batch, config, device):
     if params is None:
         params = (torch.tensor(mu, device=device), torch.tensor(sigma, device=device))
         _LOGN_PARAMS[key] = params
-    logn = torch.distributions.LogNormal(params[0], params[1], validate_args=False)
-    raw = logn.sample((batch,))
+    loc, scale = params
+    z = torch.empty(batch, dtype=loc.dtype, device=device).normal_(0.0, 1.0)
+    raw = z.mul_(scale).add_(loc).exp_()
     t_raw = raw / (1 + raw)
     t_low = torch.quantile(t_raw, config.rf_quantile_min)
     t_high = torch.quantile(t_raw, config.rf_quantile_max)
