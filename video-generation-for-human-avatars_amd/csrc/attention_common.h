@@ -202,6 +202,34 @@ __device__ __forceinline__ void xcd_block(int xcd_order, int& bx, int& by, int& 
 }
 
 
+// Row-contiguous store of a wave's 32 x HD output block (O, dQ, dK or dV): the accumulator holds
+// a row's dims in 4-wide groups at a stride of 8 (acc_row), so direct stores are 8-B pieces of 64
+// different lines per instruction. Staged through a wave-private 4-KiB LDS slot (16-B chunks XOR
+// row & 7: conflict-free both ways), each store instruction then writes 8 whole 128-B rows.
+// `scale` multiplies before the bf16 rounding (the same values as the per-lane path).
+template <int HD>
+__device__ __forceinline__ void store_rows_lds(char* stage, const f32x16* acc, float scale, bf16_t* out,
+                                               int64_t ld, int row0, int nrows, int lane) {
+  static_assert(HD == 64, "128-B rows");
+  const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+  for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = d * 32 + 8 * g + 4 * h;  // 4 dims: chunk col >> 3, half (col >> 2) & 1
+      u32x2 w;
+      w[0] = pack2(acc[d][4 * g] * scale, acc[d][4 * g + 1] * scale);
+      w[1] = pack2(acc[d][4 * g + 2] * scale, acc[d][4 * g + 3] * scale);
+      *(u32x2*)(stage + r * 128 + ((((col >> 3) ^ (r & 7))) << 4) + ((col >> 2) & 1) * 8) = w;
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int rr = i * 8 + (lane >> 3), c = lane & 7;
+    const u32x4 v = *(const u32x4*)(stage + rr * 128 + ((c ^ (rr & 7)) << 4));
+    if (rr < nrows) *(u32x4*)(out + (int64_t)(row0 + rr) * ld + c * 8) = v;
+  }
+}
+
 // the dK/dV kernel with the software-pipelined, LDS-DMA-staged loop (attention_dkdv.hip)
 int launch_dkdv_pipe(const AttnParams& p, hipStream_t s);
 bool dkdv_pipe_enabled();

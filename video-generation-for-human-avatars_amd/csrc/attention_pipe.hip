@@ -319,21 +319,14 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_pipe_kernel(const AttnParams
   stage_B(b0, 1, s1, d1, pb, sb);
   stage_C(b0, 1, pb, sb);
 
-  if (key >= p.Nk) return;
-  bf16_t* krow = p.dk + ((int64_t)b * p.Nk + key) * p.lddk + hh * HD;
-  bf16_t* vrow = p.dv + ((int64_t)b * p.Nk + key) * p.lddv + hh * HD;
-#pragma unroll
-  for (int d = 0; d < DS; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      u32x2 wk, wv;
-      wk[0] = pack2(dka[d][4 * g] * p.scale, dka[d][4 * g + 1] * p.scale);
-      wk[1] = pack2(dka[d][4 * g + 2] * p.scale, dka[d][4 * g + 3] * p.scale);
-      wv[0] = pack2(dva[d][4 * g], dva[d][4 * g + 1]);
-      wv[1] = pack2(dva[d][4 * g + 2], dva[d][4 * g + 3]);
-      *(u32x2*)(krow + d * 32 + 8 * g + 4 * h) = wk;
-      *(u32x2*)(vrow + d * 32 + 8 * g + 4 * h) = wv;
-    }
+  // dK, dV as whole rows through wave-private LDS slots (the ring is free past the last tile)
+  __syncthreads();
+  const int k0 = bx * P_KEYS + wave * 32, nk = min(32, p.Nk - k0);
+  if (nk <= 0) return;
+  store_rows_lds<HD>(smem + wave * 8192, dka, p.scale, p.dk + (int64_t)b * p.Nk * p.lddk + hh * HD, p.lddk, k0, nk,
+                     lane);
+  store_rows_lds<HD>(smem + wave * 8192 + 4096, dva, 1.0f, p.dv + (int64_t)b * p.Nk * p.lddv + hh * HD, p.lddv, k0,
+                     nk, lane);
 }
 
 // =============================================================================================
@@ -511,6 +504,14 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
   stage_B(s1, d1);                      // B(J-1)
   stage_C(b0, 1);                       // C(J-1)
 
+  if (!p.dq_f32) {  // dQ as whole rows through wave-private LDS slots
+    __syncthreads();
+    const int q0 = bx * D_QUERIES + wave * 32;
+    if (q0 < p.Nq)
+      store_rows_lds<HD>(smem + wave * 4096, acc, p.scale, (bf16_t*)p.dq + (int64_t)b * p.Nq * p.lddq + hh * HD,
+                         p.lddq, q0, min(32, p.Nq - q0), lane);
+    return;
+  }
   if (qi >= p.Nq) return;
   if (p.dq_f32) {
     float* qrow = (float*)p.dq + ((int64_t)b * p.Nq + qi) * p.lddq + hh * HD;
@@ -691,20 +692,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     if (t + 1 < ntiles) sync(t + 1);
   }
 
-  if (qi >= p.Nq) return;
   const float l_tot = xor32_sum(l_run);
   const float inv = 1.0f / l_tot;
-  bf16_t* orow = p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD;
-#pragma unroll
-  for (int d = 0; d < DS; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      u32x2 w;
-      w[0] = pack2(acc[d][4 * g] * inv, acc[d][4 * g + 1] * inv);
-      w[1] = pack2(acc[d][4 * g + 2] * inv, acc[d][4 * g + 3] * inv);
-      *(u32x2*)(orow + d * 32 + 8 * g + 4 * h) = w;
-    }
-  if (h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
+  // O through a wave-private LDS slot (the ring is free once every wave is past its last tile)
+  __syncthreads();
+  const int q0 = bx * F_QUERIES + wave * 32;
+  store_rows_lds<HD>(smem + wave * 4096, acc, inv, p.o_out + (int64_t)b * p.Nq * p.ldo + hh * HD, p.ldo, q0,
+                     min(32, p.Nq - q0), lane);
+  if (qi < p.Nq && h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
 }
 
 bool fwd_pipe_enabled() {  // LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8> (A/B switch)
