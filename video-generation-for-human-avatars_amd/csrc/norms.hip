@@ -52,33 +52,33 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_fwd_kernel(
   const int m = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
   if (m >= M) return;
   const bf16_t* xr = x + (int64_t)m * D;
+  const int b = m / rows_per_batch;
+  // the row and its batch's shift / (1 + scale) chunks go out together (one memory round trip
+  // per row; loaded after the reduction, each chunk's pair waited on its own)
+  u32x4 raw[MAXP], sraw[MAXP], oraw[MAXP];
+  load_row_raw(xr, D, lane, raw);
+  load_row_raw(shift + (int64_t)b * ld_mod, D, lane, sraw);
+  load_row_raw(onep + (int64_t)b * ld_mod, D, lane, oraw);
   float v[MAXP][8];
   float ss = 0.f;
-  {
-    u32x4 raw[MAXP];
-    load_row_raw(xr, D, lane, raw);
 #pragma unroll
-    for (int p = 0; p < MAXP; ++p) {
-      unpack8(raw[p], v[p]);
-      if (p * 512 + lane * 8 < D) {
+  for (int p = 0; p < MAXP; ++p) {
+    unpack8(raw[p], v[p]);
+    if (p * 512 + lane * 8 < D) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
-      }
+      for (int j = 0; j < 8; ++j) ss += v[p][j] * v[p][j];
     }
   }
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)D + eps);
   if (lane == 0 && rstd_out) rstd_out[m] = r;
-  const int b = m / rows_per_batch;
-  const bf16_t* sh = shift + (int64_t)b * ld_mod;
-  const bf16_t* op = onep + (int64_t)b * ld_mod;
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
     if (e < D) {
       float s8[8], o8[8], out[8];
-      load8(sh + e, s8);
-      load8(op + e, o8);
+      unpack8(sraw[p], s8);
+      unpack8(oraw[p], o8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) out[j] = rbf(rbf(v[p][j] * r) * o8[j]) + s8[j];
       store8(y + (int64_t)m * D + e, out);
