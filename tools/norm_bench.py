@@ -24,3 +24,7 @@ def t(fn, it=50):
 
 y = ops.rmsnorm_modulate_fwd(x, mods[:, 0], mods[:, 1], mods.stride(0), M // B, 1e-6)
 print(f"rmsnorm_mod_fwd {t(lambda: ops.rmsnorm_modulate_fwd(x, mods[:, 0], mods[:, 1], mods.stride(0), M // B, 1e-6)):.1f} us", flush=True)
+dy = torch.randn(M, D, device="cuda").bfloat16()
+rstd = torch.rand(M, device="cuda") + 0.5
+dres = torch.randn(M, D, device="cuda").bfloat16()
+print(f"rmsnorm_mod_bwd {t(lambda: ops.rmsnorm_modulate_bwd(dy, x, rstd, mods[:, 1], mods.stride(0), M // B, dres=dres)):.1f} us", flush=True)

@@ -106,10 +106,14 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_bwd_kernel(
   const bf16_t* op = onep + (int64_t)b * ld_mod;
   u32x4 gpk[MAXP], xpk[MAXP];
   float dr = 0.f;
-  u32x4 dyr[MAXP], opr[MAXP];
+  u32x4 dyr[MAXP], opr[MAXP], rsr[MAXP];
   load_row_raw(dy + (int64_t)m * D, D, lane, dyr);
   load_row_raw(x + (int64_t)m * D, D, lane, xpk);
   load_row_raw(op, D, lane, opr);
+  // the residual gradient row and rstd go out with the other loads (after the reduction each
+  // chunk had its own round trip)
+  if (dres) load_row_raw(dres + (int64_t)m * D, D, lane, rsr);
+  const float r = rstd[m];
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
@@ -127,7 +131,6 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_bwd_kernel(
     }
   }
   dr = wave_sum(dr);
-  const float r = rstd[m];
   const float dvar = (-0.5f * dr) * (r * r * r);
   const float dmean = dvar / (float)D;
 #pragma unroll
@@ -135,7 +138,7 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_bwd_kernel(
     const int e = p * 512 + lane * 8;
     if (e < D) {
       float res[8], out[8];
-      if (dres) load8(dres + (int64_t)m * D + e, res);
+      if (dres) unpack8(rsr[p], res);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float gj = bf2f((bf16_t)(gpk[p][j >> 1] >> ((j & 1) * 16)));
