@@ -180,7 +180,8 @@ def _sdpa_ref(q, k, v, B, H, d, bias=None):
                                                  # split backward without key bias (the pipelined dQ and
                                                  # dK/dV kernels): ragged queries, one and several key tiles
                                                  (2, 3, 1000, 768, 64, False), (1, 2, 70, 320, 64, False),
-                                                 (1, 2, 320, 1792, 64, False)])
+                                                 (1, 2, 320, 1792, 64, False),
+                                                 (1, 2, 50, 512, 64, False)])  # one ragged query tile
 def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
     from ltx_amd import ops
     scale = d ** -0.5
