@@ -254,6 +254,20 @@ __global__ __launch_bounds__(NW * 64, MODE == 1 ? 3 : 2) void attn_q_kernel(cons
     }
   }
 
+  if constexpr (MODE == 0 && HD == 64) {  // O rows in 16-B pieces (store_row_swap)
+    const float l_tot = xor32_sum(l_run);
+    store_row_swap<HD>(acc, 1.0f / l_tot, qi < p.Nq ? p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD : nullptr,
+                       lane);
+    if (qi < p.Nq && h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
+    return;
+  }
+  if constexpr (MODE == 1 && HD == 64) {
+    if (!p.dq_f32) {
+      store_row_swap<HD>(acc, p.scale,
+                         qi < p.Nq ? (bf16_t*)p.dq + ((int64_t)b * p.Nq + qi) * p.lddq + hh * HD : nullptr, lane);
+      return;
+    }
+  }
   if (qi >= p.Nq) return;
   if constexpr (MODE == 0) {
     const float l_tot = xor32_sum(l_run);
@@ -440,6 +454,12 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 1 : 2) void attn_dkdv_kernel(con
       __syncthreads();
     }
   }
+  if constexpr (HD == 64) {  // dK, dV rows in 16-B pieces (store_row_swap)
+    const bool kin = key < p.Nk;
+    store_row_swap<HD>(dka, p.scale, kin ? p.dk + ((int64_t)b * p.Nk + key) * p.lddk + hh * HD : nullptr, lane);
+    store_row_swap<HD>(dva, 1.0f, kin ? p.dv + ((int64_t)b * p.Nk + key) * p.lddv + hh * HD : nullptr, lane);
+    return;
+  }
   if (key >= p.Nk) return;
   bf16_t* krow = p.dk + ((int64_t)b * p.Nk + key) * p.lddk + hh * HD;
   bf16_t* vrow = p.dv + ((int64_t)b * p.Nk + key) * p.lddv + hh * HD;
@@ -605,20 +625,11 @@ __global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BI
     }
     const int qi = sl * 32 + (lane & 31);
     const float l_tot = xor32_sum(l_run);
-    if (qi < p.Nq) {
-      const float inv = 1.0f / l_tot;
-      bf16_t* orow = p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD;
-#pragma unroll
-      for (int d = 0; d < DS; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          u32x2 w;
-          w[0] = pack2(acc[d][4 * g] * inv, acc[d][4 * g + 1] * inv);
-          w[1] = pack2(acc[d][4 * g + 2] * inv, acc[d][4 * g + 3] * inv);
-          *(u32x2*)(orow + d * 32 + 8 * g + 4 * h) = w;
-        }
-      if (h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
-    }
+    const float inv = 1.0f / l_tot;
+    // O rows in 16-B pieces (32 contiguous bytes per row per store instruction; the 8-B pieces of
+    // the per-lane layout took half the kernel's time)
+    store_row_swap<HD>(acc, inv, qi < p.Nq ? p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD : nullptr, lane);
+    if (qi < p.Nq && h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
   }
 }
 
@@ -870,21 +881,10 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   dq_steps(simg0 + ((ntiles - 1) & 1) * SIMG, 0, KSTEPS);
   dq_store((ntiles - 1) * QT);
-  if (kl >= p.Nk) return;
-  bf16_t* krow = p.dk + ((int64_t)b * p.Nk + kl) * p.lddk + hh * HD;
-  bf16_t* vrow = p.dv + ((int64_t)b * p.Nk + kl) * p.lddv + hh * HD;
-#pragma unroll
-  for (int d = 0; d < DS; ++d)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      u32x2 wk, wv;
-      wk[0] = pack2(dka[d][4 * g] * p.scale, dka[d][4 * g + 1] * p.scale);
-      wk[1] = pack2(dka[d][4 * g + 2] * p.scale, dka[d][4 * g + 3] * p.scale);
-      wv[0] = pack2(dva[d][4 * g], dva[d][4 * g + 1]);
-      wv[1] = pack2(dva[d][4 * g + 2], dva[d][4 * g + 3]);
-      *(u32x2*)(krow + d * 32 + 8 * g + 4 * h) = wk;
-      *(u32x2*)(vrow + d * 32 + 8 * g + 4 * h) = wv;
-    }
+  // dK, dV rows in 16-B pieces (store_row_swap: both lane halves take part)
+  const bool kin = kl < p.Nk;
+  store_row_swap<HD>(dka, p.scale, kin ? p.dk + ((int64_t)b * p.Nk + kl) * p.lddk + hh * HD : nullptr, lane);
+  store_row_swap<HD>(dva, 1.0f, kin ? p.dv + ((int64_t)b * p.Nk + kl) * p.lddv + hh * HD : nullptr, lane);
 }
 
 // delta[b,h,q] = sum_d dO*O (f32), one wave per (b, q) row covering all heads

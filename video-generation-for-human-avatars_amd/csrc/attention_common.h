@@ -230,6 +230,36 @@ __device__ __forceinline__ void store_rows_lds(char* stage, const f32x16* acc, f
   }
 }
 
+// The same rows stored from registers with 16-B pieces: lanes l and l ^ 32 hold the two 4-dim
+// halves of every 8-dim chunk, one v_permlane32_swap per dword hands lane l (h = 0) the even
+// chunks and lane l + 32 the odd ones whole (cdna guide T21), so each store instruction writes
+// 32 contiguous bytes of each of 32 rows instead of 8-B pieces. `row` is this lane's output row
+// (null: not stored).
+template <int HD>
+__device__ __forceinline__ void store_row_swap(const f32x16* acc, float scale, bf16_t* row, int lane) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+    for (int gp = 0; gp < 4; gp += 2) {
+      u32x2 w[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int g = gp + e;
+        w[e][0] = pack2(acc[d][4 * g] * scale, acc[d][4 * g + 1] * scale);
+        w[e][1] = pack2(acc[d][4 * g + 2] * scale, acc[d][4 * g + 3] * scale);
+      }
+      u32x4 c;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const auto r = __builtin_amdgcn_permlane32_swap(w[0][j], w[1][j], false, false);
+        c[j] = r[0];      // h = 0: own dims 0-3 of chunk gp; h = 1: partner's dims 0-3 of chunk gp+1
+        c[2 + j] = r[1];  // h = 0: partner's dims 4-7;        h = 1: own dims 4-7
+      }
+      if (row) *(u32x4*)(row + d * 32 + 8 * (gp + h)) = c;
+    }
+}
+
 // the dK/dV kernel with the software-pipelined, LDS-DMA-staged loop (attention_dkdv.hip)
 int launch_dkdv_pipe(const AttnParams& p, hipStream_t s);
 bool dkdv_pipe_enabled();
