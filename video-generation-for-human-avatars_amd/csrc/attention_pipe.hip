@@ -559,6 +559,7 @@ int launch_dq_pipe(const AttnParams& p, hipStream_t s) {
 // (neutral to +3 %).
 // =============================================================================================
 namespace {
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 constexpr int F_KT = 64;
 constexpr int F_TILE = F_KT * PHD * 2;  // 8 KiB
 constexpr int F_BUF = 2 * F_TILE;       // K | V
@@ -622,6 +623,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   sync(0);
 
   f32x16 s[2];
+  s16x8 pk[2][2];  // the tile's probabilities, bf16 (the PV product's B operand)
   float ls[4];
   for (int t = 0; t < ntiles; ++t) {
     const char* kt = smem + (t % P_NBUF) * F_BUF;
@@ -638,18 +640,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(k2, u * 32, ks, lofs), qf[ks], s[u]);
       }
     };
+    // row sums from the bf16 probabilities the PV product consumes (v_dot2c_f32_bf16 against
+    // (1, 1): two values per instruction instead of one f32 add each), so O is normalised by the
+    // sum of exactly the weights it was accumulated with
     auto probs = [&]() {
       const float nm = -m_run;
 #pragma unroll
       for (int i = 0; i < 4; ++i) ls[i] = 0.f;
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < 2; ++u) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = fast_exp2(fmaf(s[u][r], c2, nm));
-          s[u][r] = e;
-          ls[r & 3] += e;
+        for (int r = 0; r < 16; ++r) s[u][r] = fast_exp2(fmaf(s[u][r], c2, nm));
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          pk[u][ss] = acc_frag(s[u], ss);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ls[(2 * u + ss) & 3] = __builtin_amdgcn_fdot2_f32_bf16(
+                __builtin_bit_cast(bf16x2_t, (unsigned)(unsigned short)pk[u][ss][2 * j] |
+                                                 ((unsigned)(unsigned short)pk[u][ss][2 * j + 1] << 16)),
+                __builtin_bit_cast(bf16x2_t, 0x3F803F80u), ls[(2 * u + ss) & 3], false);
         }
+      }
     };
     float alpha = 1.f;
     bool rescale = false;
@@ -684,11 +696,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const s16x8 pb = acc_frag(s[u], ss);
+      for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
-        for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vt, u * 32, ss, d, lofs), pb, acc[d]);
-      }
+        for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(vt, u * 32, ss, d, lofs), pk[u][ss], acc[d]);
     if (t + 1 < ntiles) sync(t + 1);
   }
 
