@@ -659,12 +659,16 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   constexpr int NDB = HD / 16;              // 16-wide head-dim blocks of dQ
   constexpr int QBW = HD / 32;              // 16-query blocks per wave (4 * NDB / 8 waves)
   constexpr int KSTEPS = BWD1_KEYS / 32;    // 32-key steps of the dQ product
-  // Q / dO tiles and their row statistics double-buffered: one barrier per query tile
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE + KIMG + 2 * SIMG];
-  __shared__ __attribute__((aligned(16))) float st_lse[2][QT];
-  __shared__ __attribute__((aligned(16))) float st_dl[2][QT];
-  char* kimg = smem + 4 * TILE;
+  // Q / dO tiles and their lse / delta words arrive by LDS-DMA into a 3-slot ring (two tiles in
+  // flight behind the one being computed); ONE shared array (a second __shared__ object beside the
+  // DMA target makes hipcc wait for the DMA before unrelated LDS reads)
+  constexpr int STAT = QT * 4;
+  constexpr int SLOT = 2 * TILE + 2 * STAT;  // Q | dO | lse | delta
+  constexpr int NSLOT = 3;
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + KIMG + 2 * SIMG + 64];
+  char* kimg = smem + NSLOT * SLOT;
   char* simg0 = kimg + KIMG;
+  unsigned* wact = (unsigned*)(simg0 + 2 * SIMG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const LaneOfs<HD> lofs(lane);
@@ -681,7 +685,6 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   // 32-key blocks (one per wave) whose keys are all padding have P = dS = 0 exactly behind any
   // unmasked key: their S / dP / dK / dV work and their dQ k-steps are skipped (dK = dV = 0 are
   // still stored), which leaves every output bitwise unchanged (see attn_fwd1_kernel).
-  __shared__ unsigned wact[8];
   if (lane == 0) wact[wave] = (BIAS && p.skip_masked) ? (__any(kbias > KEY_MASKED) ? 1u : 0u) : 1u;
   s16x8 kf[KS], vf[KS];
   {
@@ -773,22 +776,43 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
   const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
   const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
-  TileStage<HD, QT, BWD1_THREADS> qs_, os_;
   const int ntiles = (p.Nq + QT - 1) / QT;
-  auto stage_stats = [&](int qb, int buf) {
-    if (tid < QT) {
-      const int q = qb + tid;
-      st_lse[buf][tid] = q < p.Nq ? -lbase[q] : -INFINITY;  // -lse2 (rows past Nq: P = 0)
-      st_dl[buf][tid] = q < p.Nq ? dbase[q] : 0.f;
+  // tile t -> slot t % 3: wave w moves Q rows 8w..8w+7 and dO rows 8w..8w+7 (one 1-KiB piece each,
+  // the chunk swizzle applied on the source address), wave 0 the lse words, wave 1 the delta words.
+  // Rows past Nq re-read the last row; their lse is set to +inf after the DMA lands (P = dS = 0).
+  const int drow = wave * 8 + (lane >> 3), dch = (lane & 7) ^ swz<HD>(drow);
+  uint32_t qoff = (uint32_t)(drow * p.ldq + dch * 8) * 2, ooff = (uint32_t)(drow * p.lddo + dch * 8) * 2;
+  auto dma = [&](int t) {
+    char* base = smem + (t % NSLOT) * SLOT;
+    const int q0 = t * QT;
+    if (q0 + QT > p.Nq) {  // the ragged last tile (its DMA is the last one issued)
+      const int rr = min(drow, p.Nq - q0 - 1);
+      qoff = (uint32_t)(rr * p.ldq + dch * 8) * 2;
+      ooff = (uint32_t)(rr * p.lddo + dch * 8) * 2;
     }
+    dma16s(qoff, qbase + (int64_t)q0 * p.ldq, lds_u32(base + wave * 1024));
+    dma16s(ooff, obase + (int64_t)q0 * p.lddo, lds_u32(base + TILE + wave * 1024));
+    if (wave < 2) dma4((wave == 0 ? lbase : dbase) + min(q0 + lane, p.Nq - 1), lds_u32(base + 2 * TILE + wave * STAT));
   };
-  qs_.load(qbase, p.ldq, 0, p.Nq, tid);
-  os_.load(obase, p.lddo, 0, p.Nq, tid);
-  qs_.store(smem, tid);
-  os_.store(smem + TILE, tid);
-  stage_stats(0, 0);
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0);  // retire the pre-loop loads (see attn_dkdv_kernel)
+  // this wave's DMA of tile t retired (the `later` pieces of tile t+1 may stay in flight) and the
+  // LDS writes done; rows past Nq of tile t get lse = +inf; then the workgroup barrier
+  auto tile_sync = [&](int t, bool later) {
+    if (later) {
+      if (wave < 2) __builtin_amdgcn_s_waitcnt(0x0073);  // vmcnt(3) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0x0072);           // vmcnt(2) lgkmcnt(0)
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0070);
+    }
+    if (wave == 0 && t * QT + QT > p.Nq && t * QT + lane >= p.Nq)
+      ((float*)(smem + (t % NSLOT) * SLOT + 2 * TILE))[lane] = INFINITY;
+    __builtin_amdgcn_s_waitcnt(0x0070);
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  dma(0);
+  if (ntiles > 1) dma(1);
+  tile_sync(0, ntiles > 1);
   kmask = 0u;
 #pragma unroll
   for (int w = 0; w < 8; ++w) kmask |= wact[w] << w;
@@ -796,21 +820,22 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   const bool mine = (kmask >> wave) & 1u;
 
   // Tile t's dQ product runs during tile t+1's S / dP / dK / dV (its dS image is the other
-  // buffer): one barrier interval holds both, so the dQ MFMAs fill the softmax VALU gaps.
+  // buffer): one barrier interval holds both, so the dQ MFMAs fill the softmax VALU gaps. Its
+  // result is stored at the top of iteration t+2, before that iteration's DMA, so the counted
+  // wait at the end of an iteration only has the next tile's pieces behind it.
   for (int t = 0; t < ntiles; ++t) {
-    const int q0 = t * QT;
     char* simg = simg0 + (t & 1) * SIMG;
-    const char* qtile = smem + (t & 1) * 2 * TILE;
+    int soff = (t % NSLOT) * SLOT;
+    asm volatile("" : "+s"(soff));  // opaque: no per-slot copies of the fragment addresses
+    const char* qtile = smem + soff;
     const char* otile = qtile + TILE;
-    const float* sl = st_lse[t & 1];
-    const float* sd = st_dl[t & 1];
+    const float* sl = (const float*)(qtile + 2 * TILE);
+    const float* sd = sl + QT;
     const char* sprev = simg0 + ((t + 1) & 1) * SIMG;
-    if (t + 1 < ntiles) {
-      qs_.load(qbase, p.ldq, q0 + QT, p.Nq, tid);
-      os_.load(obase, p.lddo, q0 + QT, p.Nq, tid);
-    }
+    if (t >= 2) dq_store((t - 2) * QT);
 #pragma unroll
     for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (t + 2 < ntiles) dma(t + 2);  // into tile t-1's slot (last read before the barrier)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (!mine) {  // padding keys: only this wave's share of the dQ product
@@ -837,12 +862,12 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
       if (t > 0) dq_steps(sprev, u * (KSTEPS / 2), (u + 1) * (KSTEPS / 2));
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x4 nl4 = *(const f32x4*)&sl[u * 32 + 8 * g + 4 * h];
+        const f32x4 l4 = *(const f32x4*)&sl[u * 32 + 8 * g + 4 * h];
         const f32x4 dl4 = *(const f32x4*)&sd[u * 32 + 8 * g + 4 * h];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = 4 * g + i;
-          const float pr = fast_exp2(fmaf(s[r], c2, BIAS ? kbias + nl4[i] : nl4[i]));
+          const float pr = fast_exp2(fmaf(s[r], c2, BIAS ? kbias - l4[i] : -l4[i]));
           s[r] = pr;
           dp[r] = pr * (dp[r] - dl4[i]);
         }
@@ -868,15 +893,11 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
         }
       }
     }
-    if (t > 0) dq_store(q0 - QT);
-    if (t + 1 < ntiles) {  // tile t+1 into the other buffers (tile t-1's, free since the last barrier)
-      char* nt = smem + ((t + 1) & 1) * 2 * TILE;
-      qs_.store(nt, tid);
-      os_.store(nt + TILE, tid);
-      stage_stats(q0 + QT, (t + 1) & 1);
-    }
-    __syncthreads();  // dS image t and tile t+1 complete; tile t-1's buffers no longer read
+    // dS image t complete, tile t+1 resident, tile t's slot no longer read
+    if (t + 1 < ntiles) tile_sync(t + 1, t + 2 < ntiles);
+    else __syncthreads();
   }
+  if (ntiles >= 2) dq_store((ntiles - 2) * QT);
 #pragma unroll
   for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   dq_steps(simg0 + ((ntiles - 1) & 1) * SIMG, 0, KSTEPS);

@@ -116,6 +116,30 @@ struct TileStage {
   }
 };
 
+// LDS-DMA pieces in inline asm: hipcc tracks its own global_load_lds builtin as an LDS write
+// and waits vmcnt(0) before the next ds_read, which would drain the tile prefetch every
+// iteration; hidden from it, the DMA is retired only by the kernel's tile barrier's explicit wait + barrier.
+// M0 (the wave-uniform LDS destination) is written in the same statement (compiler-reserved).
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p);
+}
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+// scalar-base form: per-lane 32-bit byte offset + wave-uniform 64-bit base (no per-lane 64-bit math)
+__device__ __forceinline__ void dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds) : "memory");
+}
+__device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
+}
+
 struct AttnParams {
   const bf16_t* q; int64_t ldq;
   const bf16_t* k; int64_t ldk;
