@@ -294,6 +294,19 @@ int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u, int64_t l
                            int accumulate, int64_t groups, int64_t gy, int64_t gu, int64_t gd,
                            void* stream);
 
+/* One pass over dY for a token-sized adapter's backward (replaces the ltx_lora_rows call on dY
+ * plus the ltx_lora_wgrad call for lora_B, transformer3d backward): w[m,j] = alpha * sum_n Y[m,n] *
+ * (w3[j] + w3[RP+j] + w3[2RP+j])[n] (f32, ldw_out) with its K-extension split row [hi|hi|lo|0..]
+ * (bf16 [M, K2], ld_split) and dw[n*on + j*oj] (+)= alpha * sum_m Y[m,n] * U[m,j] (accumulate != 0
+ * adds into the buffer). Y bf16 [M,N] (ldy), U f32 [M,r] (ldu), w3 = ltx_lora_pieces of B^T.
+ * M % 32 == 0, N % 512 == 0, rank 8 or 16. workspace: ltx_lora_dy_workspace floats (f32). */
+int ltx_lora_dy(const void* y, int64_t ldy, const float* u, int64_t ldu, const void* w3, int64_t ldw3,
+                int64_t M, int64_t N, int64_t r, float alpha, float* w, int64_t ldw_out, void* split,
+                int64_t ld_split, int64_t K2, float* dw, int64_t on, int64_t oj, int accumulate,
+                float* workspace, void* stream);
+/* f32 workspace size (in floats) of ltx_lora_dy for an [M, N] dY at rank r */
+int ltx_lora_dy_workspace(int64_t M, int64_t N, int64_t r, int64_t* floats);
+
 /* ---- small ops -------------------------------------------------------------------------------- */
 /* AdaLayerNormSingle sinusoid: out[b,:] = bf16([cos(s*t*f), sin(s*t*f)]) (256 ch), s = scale */
 int ltx_timestep_embedding(const float* t, float scale, void* out, int64_t B, int64_t dim,

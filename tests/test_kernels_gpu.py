@@ -519,6 +519,32 @@ def test_lora_kernels(M, r):
     assert rel(buf, ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,r", [(1792, 2048, 16), (1760, 1024, 16), (4480, 512, 8), (32, 512, 16)])
+def test_lora_dy_one_pass(M, N, r):
+    """ltx_lora_dy = lora_down(dY, B, transposed, split) + lora_wgrad(dY, u, accumulate) in one
+    pass over dY: the same f32 products to summation order (fp32 reference), the split operand
+    exactly lora_split of its own w, dB added into the existing buffer. Ragged row splits (M not a
+    multiple of 224) and a single 32-row group included."""
+    from ltx_amd import ops
+    dy = g(M, N, seed=3)
+    u = torch.randn(M, r, device=DEV)
+    Bm = torch.randn(N, r, device=DEV) * 0.05
+    pieces = ops.lora_pieces(Bm, transposed=True)
+    assert ops.lora_dy_fits(dy, r)
+    buf = torch.randn(N, r, device=DEV)
+    ref_dB = buf + 0.5 * dy.float().t() @ u
+    w, sp = ops.lora_dy(dy, u, pieces, r, 0.5, buf)
+    assert rel(w, 0.5 * dy.float() @ Bm) < 1e-5
+    assert torch.equal(sp, ops.lora_split(w, "act"))
+    assert rel(buf, ref_dB) < 1e-5
+    # against the two-kernel path it replaces
+    w2, sp2 = ops.lora_rows(dy, pieces, r, alpha=0.5, split=True)
+    assert rel(w, w2) < 1e-6
+    buf2 = torch.zeros(N, r, device=DEV)
+    ops.lora_dy(dy, u, pieces, r, 0.5, buf2, accumulate=False)
+    assert rel(buf2, ops.lora_wgrad(dy, u, alpha=0.5)) < 1e-6
+
+
 def test_mse_and_adamw():
     from ltx_amd import ops
     o, v = g(2, 64, 128, seed=1), g(2, 64, 128, seed=2)

@@ -1,0 +1,315 @@
+// One pass over dY for a token-sized LoRA adapter's backward (peft's f32 lora_B, training.py:50-68):
+//   w  = alpha * dY . B        [M, r]  (the input-gradient term, consumed as the dgrad GEMM's
+//                                       K-extension after the hi / lo split)
+//   dB (+)= alpha * dY^T . u   [N, r]  (u = x . A^T, saved by the forward)
+// Until now these were two kernels that each streamed dY from HBM (ltx_lora_rows and
+// ltx_lora_wgrad, ~18.5 us each at M = 14336, N = 2048); here one LDS-DMA stream of dY feeds both
+// products on the bf16 matrix core, and a small second kernel finishes the sums.
+//
+// Block = 8 waves over 512 columns x G row groups of 32 rows (grid: N / 512 column splits x
+// ceil(M / 32G) row splits). Wave w owns columns c0 = 512 bx + 64 w .. +64 and streams its 32 x 64
+// slot of every row group (4 KiB, the attention tiles' chunk swizzle swz<64>) through a private
+// 4-slot ring, so no barrier is needed in the loop. Per slot:
+//   * w:  [32 rows x 16 j] += slot . (B^T pieces)^T: 12 v_mfma_f32_16x16x32_bf16 (2 row halves x
+//         2 k halves x 3 pieces), the B^T pieces (ltx_lora_pieces) in registers for the whole block;
+//   * dB: [16 j x 64 cols] += (u pieces)^T . slot: 12 MFMAs (4 column blocks x 3 pieces), the
+//         slot read transposed (ds_read_b64_tr_b16, the attention dQ product's k-slot order), u
+//         split into exact hi / mid / lo bf16 pieces from an LDS copy of the block's u rows.
+// Exact bf16 products summed in f32, as ltx_lora_rows; the sums run in a different order than
+// ltx_lora_rows / ltx_lora_wgrad (f32 rounding differences only).
+// Partials (deterministic, no atomics): w over the 4 column splits [CS][M][RP], dB over the row
+// splits [RS][N][RP]; lora_dy_finish_kernel sums them in a fixed order, applies alpha, writes w,
+// its [hi | hi | lo | 0..] split operand, and adds dB into the gradient buffer.
+#include <cstdlib>
+
+#include "attention_common.h"
+#include "ltx_hip.h"
+
+namespace ltx {
+
+namespace {
+constexpr int DY_G = 7;      // row groups of 32 per block (14336 = 64 x 7 x 32)
+constexpr int DY_NR = 4;     // ring slots per wave
+constexpr int DY_COLS = 512; // columns per block
+constexpr int DY_UPAD = DY_G * 32 + 4;  // u^T row length in LDS (floats; +4 spreads the banks)
+}  // namespace
+
+template <int R>
+__global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__ y, int64_t ldy,
+                                                      const float* __restrict__ u, int64_t ldu,
+                                                      const bf16_t* __restrict__ w3, int64_t ldw,
+                                                      float* __restrict__ part_w, float* __restrict__ part_b,
+                                                      int M, int N) {
+  constexpr int RP = R >= 16 ? R : 16;
+  constexpr int JT = RP / 16;
+  constexpr int NF = 3 * JT;
+  constexpr int RING = 8 * DY_NR * 4096;
+  constexpr int UT = RP * DY_UPAD * 4;
+  static_assert(R == 8 || R == 16, "rank 8 or 16 (the w partials of rank 32 would not fit the ring)");
+  static_assert(8 * DY_G * 32 * (RP + 1) * 4 <= RING, "w partials fit the ring");
+  // ONE shared array (the DMA target): the ring, then u^T of the block's rows
+  __shared__ __attribute__((aligned(16))) char smem[RING + UT];
+  float* ut = (float*)(smem + RING);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cs = blockIdx.x, rs = blockIdx.y;
+  const int c0 = cs * DY_COLS + wave * 64;
+  const int mb = rs * DY_G * 32;
+
+  // u^T of rows mb .. mb + 32G (zero past M)
+  for (int e = tid; e < DY_G * 32 * RP; e += 512) {
+    const int rr = e / RP, j = e % RP;
+    const int m = mb + rr;
+    ut[j * DY_UPAD + rr] = (m < M && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
+  }
+  // B^T pieces of this wave's 64 columns: [k half][piece x JT] (ltx_lora_rows' fragment layout)
+  s16x8 bp[2][NF];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const bf16_t* src = w3 + (int64_t)(p * RP + t * 16 + (lane & 15)) * ldw + c0 + (lane >> 4) * 8;
+      bp[0][p * JT + t] = *(const s16x8*)src;
+      bp[1][p * JT + t] = *(const s16x8*)(src + 32);
+    }
+  __syncthreads();  // u^T staged; every ordinary load retired before the DMA stream starts
+
+  // DMA: piece i of a slot = rows 8i .. 8i+7; lane -> row 8i + (lane >> 3), physical chunk lane & 7
+  uint32_t yo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * i + (lane >> 3);
+    yo[i] = (uint32_t)(row * ldy + (((lane & 7) ^ swz<64>(row)) * 8)) * 2;
+  }
+  const uint32_t lring = lds_u32(smem + wave * (DY_NR * 4096));
+  auto dma = [&](int g) {
+    const char* sb = (const char*)(y + (int64_t)(mb + 32 * g) * ldy + c0);  // M % 32 == 0
+    const uint32_t l = lring + (g % DY_NR) * 4096;
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %5\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(yo[0]), "v"(yo[1]), "v"(yo[2]), "v"(yo[3]), "s"(sb), "s"(l)
+        : "memory", "scc");
+  };
+  const int ng = min(DY_G, (M - mb + 31) / 32);  // row groups of this block
+
+  // row reads (w product): rows 16q + (lane & 15), logical chunk 4h + (lane >> 4)
+  int roff[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 16 * q + (lane & 15);
+      roff[q][h] = row * 128 + (((4 * h + (lane >> 4)) ^ swz<64>(row)) * 16);
+    }
+  // transposed reads (dB product): k-slot 8g + jj = row 4g + jj (jj < 4) / 16 + 4g + jj - 4
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  int toffs[4];
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb) toffs[nb] = toff<64>(4 * g4 + qq, 2 * nb + (pp >> 1)) + 8 * (pp & 1);
+  auto tr4 = [](const char* a) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
+  };
+
+  f32x4 wacc[DY_G][2][JT];
+  f32x4 bacc[JT][4];
+#pragma unroll
+  for (int t = 0; t < JT; ++t)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) bacc[t][nb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int g = 0; g < DY_NR - 1; ++g)
+    if (g < ng) dma(g);
+#pragma unroll
+  for (int g = 0; g < DY_G; ++g) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int t = 0; t < JT; ++t) wacc[g][q][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (g >= ng) continue;
+    // slot g landed: only the slots issued after it (at most DY_NR - 2) stay in flight
+    const int younger = min(DY_NR - 2, ng - 1 - g);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const char* sl = smem + wave * (DY_NR * 4096) + (g % DY_NR) * 4096;
+    s16x8 xf[2][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) xf[q][h] = *(const s16x8*)(sl + roff[q][h]);
+    s16x8 yb[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const s16x4 b0 = tr4(sl + toffs[nb]), b1 = tr4(sl + toffs[nb] + 16 * 128);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        yb[nb][j] = b0[j];
+        yb[nb][4 + j] = b1[j];
+      }
+    }
+    // u pieces of this group's rows in the k-slot order: [piece][t]
+    s16x8 up[3][JT];
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const float* ur = ut + (16 * t + (lane & 15)) * DY_UPAD + 32 * g + 4 * g4;
+      const f32x4 lo4 = *(const f32x4*)ur, hi4 = *(const f32x4*)(ur + 16);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const float v = jj < 4 ? lo4[jj] : hi4[jj - 4];
+        const bf16_t a = f2bf(v);
+        const float r1 = v - bf2f(a);
+        const bf16_t b = f2bf(r1);
+        const bf16_t c = f2bf(r1 - bf2f(b));
+        up[0][t][jj] = (short)a;
+        up[1][t][jj] = (short)b;
+        up[2][t][jj] = (short)c;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot g read: its ring slot may be refilled
+    if (g + DY_NR - 1 < ng) dma(g + DY_NR - 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int t = 0; t < JT; ++t)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            wacc[g][q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[q][h], bp[h][p * JT + t], wacc[g][q][t], 0, 0, 0);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int t = 0; t < JT; ++t)
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+          bacc[t][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(up[p][t], yb[nb], bacc[t][nb], 0, 0, 0);
+  }
+  // dB partial: C[j][n] -> part_b[rs][n][j], lane: n = c0 + 16 nb + (lane & 15), j = 16t + 4 g4 + 0..3
+#pragma unroll
+  for (int t = 0; t < JT; ++t)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const int n = c0 + 16 * nb + (lane & 15);
+      *(f32x4*)(part_b + ((int64_t)rs * N + n) * RP + 16 * t + 4 * g4) = bacc[t][nb];
+    }
+  // w partial: the 8 waves' [32G rows][RP] sums through LDS (the ring is free once all waves are
+  // past their last slot), then one column-split partial per row
+  __syncthreads();
+  float(*part)[DY_G * 32][RP + 1] = (float(*)[DY_G * 32][RP + 1])smem;
+#pragma unroll
+  for (int g = 0; g < DY_G; ++g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int t = 0; t < JT; ++t)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          part[wave][32 * g + 16 * q + 4 * g4 + rr][16 * t + (lane & 15)] = wacc[g][q][t][rr];
+  __syncthreads();
+  for (int e = tid; e < DY_G * 32 * RP; e += 512) {
+    const int rr = e / RP, j = e % RP;
+    const int m = mb + rr;
+    if (m >= M) continue;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) sum += part[w][rr][j];
+    part_w[((int64_t)cs * M + m) * RP + j] = sum;
+  }
+}
+
+// Blocks [0, nwb): w[m,j] = alpha * sum_c part_w[c][m][j] and the [hi | hi | lo | 0..] split row,
+// one thread per split element. Blocks [nwb, ..): dw[n*on + j*oj] (+)= alpha * sum_s part_b[s][n][j]
+// for 64 (n, j) pairs per block, the row splits dealt to 4 thread groups (strided, independent
+// loads in flight) and the 4 group sums added in a fixed order (deterministic).
+template <int R>
+__global__ __launch_bounds__(256) void lora_dy_finish_kernel(const float* __restrict__ part_w, int CS,
+                                                             const float* __restrict__ part_b, int RS, int M, int N,
+                                                             float alpha, float* __restrict__ w, int64_t ldw_out,
+                                                             bf16_t* __restrict__ split, int64_t lds, int K2,
+                                                             float* __restrict__ dw, int64_t on, int64_t oj,
+                                                             int accumulate, int nwb) {
+  constexpr int RP = R >= 16 ? R : 16;
+  if ((int)blockIdx.x < nwb) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= (int64_t)M * K2) return;
+    const int m = (int)(e / K2), c = (int)(e % K2);
+    if (c >= 3 * R) {
+      split[(int64_t)m * lds + c] = (bf16_t)0;
+      return;
+    }
+    const int j = c % R;
+    float sum = 0.f;
+    for (int s = 0; s < CS; ++s) sum += part_w[((int64_t)s * M + m) * RP + j];
+    const float v = sum * alpha;
+    const bf16_t hi = f2bf(v);
+    if (c < R) w[(int64_t)m * ldw_out + j] = v;
+    split[(int64_t)m * lds + c] = c < 2 * R ? hi : f2bf(v - bf2f(hi));
+    return;
+  }
+  __shared__ float red[4][64];
+  const int pr = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t e = (int64_t)(blockIdx.x - nwb) * 64 + pr;  // pair (n, j), j fastest
+  const bool ok = e < (int64_t)N * R;
+  const int n = ok ? (int)(e / R) : 0, j = ok ? (int)(e % R) : 0;
+  float sum = 0.f;
+#pragma unroll 8
+  for (int s = grp; s < RS; s += 4) sum += part_b[((int64_t)s * N + n) * RP + j];
+  red[grp][pr] = sum;
+  __syncthreads();
+  if (grp == 0 && ok) {
+    const float v = (((red[0][pr] + red[1][pr]) + red[2][pr]) + red[3][pr]) * alpha;
+    float* o = dw + (int64_t)n * on + (int64_t)j * oj;
+    *o = accumulate ? *o + v : v;
+  }
+}
+
+extern "C" int ltx_lora_dy_workspace(int64_t M, int64_t N, int64_t r, int64_t* floats) {
+  LTX_CHECK_ARG(floats && M > 0 && N > 0 && (r == 8 || r == 16), "lora_dy_workspace: bad args");
+  const int64_t RP = r >= 16 ? r : 16;
+  const int64_t CS = N / DY_COLS, RS = (M + DY_G * 32 - 1) / (DY_G * 32);
+  *floats = CS * M * RP + RS * N * RP;
+  return LTX_OK;
+}
+
+extern "C" int ltx_lora_dy(const void* y, int64_t ldy, const float* u, int64_t ldu, const void* w3, int64_t ldw3,
+                           int64_t M, int64_t N, int64_t r, float alpha, float* w, int64_t ldw_out, void* split,
+                           int64_t ld_split, int64_t K2, float* dw, int64_t on, int64_t oj, int accumulate,
+                           float* workspace, void* stream) {
+  LTX_CHECK_ARG(y && u && w3 && w && split && dw && workspace, "lora_dy: null operand");
+  LTX_CHECK_ARG(M >= 32 && M % 32 == 0 && N % DY_COLS == 0 && (r == 8 || r == 16),
+                "lora_dy: M % 32 == 0, N % 512 == 0, rank 8 or 16");
+  LTX_CHECK_ARG(ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 && ldw3 % 8 == 0 && ((uintptr_t)w3 % 16) == 0 && ldw3 >= N,
+                "lora_dy: 16-B aligned rows of dY and of the pieces");
+  LTX_CHECK_ARG(ldy * 2 * 32 < ((int64_t)1 << 32), "lora_dy: 32-bit DMA offsets");
+  LTX_CHECK_ARG(ldw_out >= r && ldu >= r && K2 >= 3 * r && K2 % 64 == 0 && ld_split >= K2, "lora_dy: output strides");
+  LTX_CHECK_ARG((on == r && oj == 1) || (on == 1 && oj == N), "lora_dy: dB must be a dense [N,r] or [r,N]");
+  const int64_t RP = r >= 16 ? r : 16;
+  const int CS = (int)(N / DY_COLS), RS = (int)((M + DY_G * 32 - 1) / (DY_G * 32));
+  float* pw = workspace;
+  float* pb = workspace + (int64_t)CS * M * RP;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)CS, (unsigned)RS);
+  const int nwb = (int)((M * K2 + 255) / 256);
+  const dim3 g2((unsigned)(nwb + (N * r + 63) / 64));
+#define LTX_LORA_DY(RR)                                                                                          \
+  hipLaunchKernelGGL((lora_dy_kernel<RR>), grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu,                \
+                     (const bf16_t*)w3, ldw3, pw, pb, (int)M, (int)N);                                           \
+  LTX_LAUNCH_CHECK();                                                                                            \
+  hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, pw, CS, pb, RS, (int)M, (int)N, alpha, w, \
+                     ldw_out, (bf16_t*)split, ld_split, (int)K2, dw, on, oj, accumulate, nwb);
+  switch (r) {
+    case 8: LTX_LORA_DY(8) break;
+    case 16: LTX_LORA_DY(16) break;
+    default: return fail(LTX_ERR_BAD_ARG, "lora_dy: rank must be 8 or 16");
+  }
+#undef LTX_LORA_DY
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+}  // namespace ltx

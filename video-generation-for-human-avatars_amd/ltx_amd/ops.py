@@ -649,6 +649,36 @@ def lora_wgrad(y, u, alpha=1.0, transpose_out=False, out=None, accumulate=False,
     return out
 
 
+def lora_dy_enabled():
+    """LTX_LORA_DY=0 (read per call): the backward keeps ltx_lora_wgrad + ltx_lora_rows on dY."""
+    return os.environ.get("LTX_LORA_DY", "1") != "0"
+
+
+def lora_dy_fits(y, r):
+    M, N = y.shape
+    return r in (8, 16) and M % 32 == 0 and N % 512 == 0 and y.stride(1) == 1 and y.stride(0) % 8 == 0
+
+
+def lora_dy(y, u, w3, r, alpha, dB_out, accumulate=True, transpose_out=False):
+    """One pass over dY (ltx_lora_dy): returns (w, split) as lora_down(y, B, transposed=True,
+    split=True) does, and adds alpha * y^T . u into dB_out ([N, r], or [r, N] with transpose_out)
+    as lora_wgrad(y, u, alpha, out=dB_out, accumulate=accumulate) does."""
+    M, N = y.shape
+    shape = (r, N) if transpose_out else (N, r)
+    assert tuple(dB_out.shape) == shape and dB_out.dtype == F32 and dB_out.is_contiguous()
+    on, oj = (1, N) if transpose_out else (r, 1)
+    K2 = lora_k2(r)
+    w = torch.empty(M, r, dtype=F32, device=y.device)
+    sp = torch.empty(M, K2, dtype=BF16, device=y.device)
+    n = ctypes.c_int64(0)
+    call("ltx_lora_dy_workspace", M, N, r, ctypes.byref(n))
+    ws = torch.empty(n.value, dtype=F32, device=y.device)
+    call("ltx_lora_dy", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(w3), _rows(w3, "w3"), M, N, r,
+         float(alpha), _p(w), _rows(w, "w"), _p(sp), _rows(sp, "split"), K2, _p(dB_out), on, oj,
+         1 if accumulate else 0, _p(ws), _s())
+    return w, sp
+
+
 # ---------------------------------------------------------------------------------------------
 # small ops
 # ---------------------------------------------------------------------------------------------

@@ -567,9 +567,12 @@ class _BlockFn(torch.autograd.Function):
             if _DELTA_FUSED else {}
         if has_lora:
             lq, lk, lv, lo = lora
-            ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
-            w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True,
-                                     pieces=lo.weight_pieces("Bt"))
+            if ops.lora_dy_enabled() and ops.lora_dy_fits(dh2, r):  # one pass over dY
+                w_o, sw = ops.lora_dy(dh2, u_o, lo.weight_pieces("Bt"), r, s, _grad_buf(lo, "B"))
+            else:
+                ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
+                w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True,
+                                         pieces=lo.weight_pieces("Bt"))
             ops.lora_wgrad(o2, w_o, transpose_out=True, out=_grad_buf(lo, "A"), accumulate=True)
             do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")), **rd)
         else:
@@ -631,9 +634,12 @@ class _BlockFn(torch.autograd.Function):
         d_y1 = torch.empty_like(dh2)
         gated = dict(aux1=mods[:, 2], aux2=d_y1, rows_per_batch=rpm)
         if has_lora:
-            ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
-            w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True,
-                                     pieces=lq.weight_pieces("Bt"))
+            if ops.lora_dy_enabled() and ops.lora_dy_fits(dq2raw, r):
+                w_q, sw = ops.lora_dy(dq2raw, u_q, lq.weight_pieces("Bt"), r, s, _grad_buf(lq, "B"))
+            else:
+                ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
+                w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True,
+                                         pieces=lq.weight_pieces("Bt"))
             ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
                            ext=(sw, lq.weight_split("A")), **gated)
