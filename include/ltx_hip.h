@@ -102,6 +102,13 @@ int ltx_rmsnorm_modulate_fwd(const void* x, const void* shift, const void* onep,
 int ltx_rmsnorm_modulate_bwd(const void* dy, const void* x, const float* rstd, const void* onep,
                              int64_t ld_mod, const void* dres, void* dx, int64_t M, int64_t D,
                              int64_t rows_per_batch, void* stream);
+/* ltx_rmsnorm_modulate_bwd that also writes gout = bf16(bf16(dx) * gate[b]) (gate rows of D bf16,
+ * row stride ld_gate per batch b = m / rows_per_batch): the previous block's FF-output gradient
+ * (ltx_gate_mul_bf16 of this dx, bitwise) from the same pass. gout = null: plain backward. */
+int ltx_rmsnorm_modulate_bwd_gated(const void* dy, const void* x, const float* rstd, const void* onep,
+                                   int64_t ld_mod, const void* dres, void* dx, int64_t M, int64_t D,
+                                   int64_t rows_per_batch, const void* gate, int64_t ld_gate,
+                                   void* gout, void* stream);
 /* modulation rows: out[b,j,:] = bf16(sst[j,:] + tmod[b*ld_tmod + j*ld_j + :]) and, for the
  * rows flagged in scale_mask (bit j), onep = bf16(1 + that) (attention.py:229-239 with ld_j = D;
  * transformer3d.py:554-560 with ld_j = 0, the embedded timestep broadcast). out/onep [B,P,D]. */

@@ -358,6 +358,12 @@ def test_rmsnorm_modulate_fwd_bwd():
     dx = ops.rmsnorm_modulate_bwd(dy, x, rstd, one, mod.stride(0), N, dres=dres)
     ref.backward(dy.view(B, N, D))
     assert rel(dx, xr.grad.view(B * N, D).float() + dres.float()) < 5e-3
+    # the gated form (the previous block's FF-output gradient from the same pass): dx unchanged,
+    # gout bitwise gate_mul(dx, gate)
+    gate = mod[:, 5]
+    dx2, gout = ops.rmsnorm_modulate_bwd(dy, x, rstd, one, mod.stride(0), N, dres=dres, gate=gate)
+    assert torch.equal(dx2, dx)
+    assert torch.equal(gout, ops.gate_mul(dx, gate, N))
 
 
 def test_layernorm_modulate_fwd_bwd():

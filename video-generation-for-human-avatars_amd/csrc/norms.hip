@@ -98,12 +98,13 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_fwd_kernel(
 __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const float* __restrict__ rstd,
     const bf16_t* __restrict__ onep, int64_t ld_mod, const bf16_t* dres, bf16_t* dx, int M, int D,
-    int rows_per_batch) {
+    int rows_per_batch, const bf16_t* __restrict__ gate, int64_t ld_gate, bf16_t* __restrict__ gout) {
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
   if (m >= M) return;
   const int b = m / rows_per_batch;
   const bf16_t* op = onep + (int64_t)b * ld_mod;
+  const bf16_t* gr = gate ? gate + (int64_t)b * ld_gate : nullptr;
   u32x4 gpk[MAXP], xpk[MAXP];
   float dr = 0.f;
   u32x4 dyr[MAXP], opr[MAXP], rsr[MAXP];
@@ -149,6 +150,14 @@ __global__ __launch_bounds__(ROW_THREADS) void rmsnorm_mod_bwd_kernel(
         out[j] = dres ? res[j] + d : d;
       }
       store8(dx + (int64_t)m * D + e, out);
+      if (gout) {  // the previous block's bf16(dx * gate) from the stored bf16 dx (gate_mul, bitwise)
+        const u32x4 gg = *(const u32x4*)(gr + e);
+        float g8[8], o2[8];
+        unpack8(gg, g8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o2[j] = rbf(out[j]) * g8[j];
+        store8(gout + (int64_t)m * D + e, o2);
+      }
     }
   }
 }
@@ -558,16 +567,27 @@ int ltx_rmsnorm_modulate_fwd(const void* x, const void* shift, const void* onep,
   return LTX_OK;
 }
 
+int ltx_rmsnorm_modulate_bwd_gated(const void* dy, const void* x, const float* rstd, const void* onep,
+                                   int64_t ld_mod, const void* dres, void* dx, int64_t M, int64_t D,
+                                   int64_t rows_per_batch, const void* gate, int64_t ld_gate, void* gout,
+                                   void* stream) {
+  LTX_CHECK_ARG(dy && x && rstd && onep && dx && M > 0 && D > 0, "rmsnorm_modulate_bwd: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048 && ld_mod % 8 == 0, "rmsnorm_modulate_bwd: D must be %8 and <= 2048");
+  LTX_CHECK_ARG(!gout || (gate && ld_gate % 8 == 0 && ((uintptr_t)gate % 16) == 0),
+                "rmsnorm_modulate_bwd: gated output needs 16-B aligned gate rows");
+  hipLaunchKernelGGL(rmsnorm_mod_bwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16_t*)dy, (const bf16_t*)x, rstd, (const bf16_t*)onep, ld_mod, (const bf16_t*)dres,
+                     (bf16_t*)dx, (int)M, (int)D, (int)(rows_per_batch > 0 ? rows_per_batch : M),
+                     (const bf16_t*)gate, ld_gate, (bf16_t*)gout);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
 int ltx_rmsnorm_modulate_bwd(const void* dy, const void* x, const float* rstd, const void* onep, int64_t ld_mod,
                              const void* dres, void* dx, int64_t M, int64_t D, int64_t rows_per_batch,
                              void* stream) {
-  LTX_CHECK_ARG(dy && x && rstd && onep && dx && M > 0 && D > 0, "rmsnorm_modulate_bwd: bad args");
-  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048 && ld_mod % 8 == 0, "rmsnorm_modulate_bwd: D must be %8 and <= 2048");
-  hipLaunchKernelGGL(rmsnorm_mod_bwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream,
-                     (const bf16_t*)dy, (const bf16_t*)x, rstd, (const bf16_t*)onep, ld_mod, (const bf16_t*)dres,
-                     (bf16_t*)dx, (int)M, (int)D, (int)(rows_per_batch > 0 ? rows_per_batch : M));
-  LTX_LAUNCH_CHECK();
-  return LTX_OK;
+  return ltx_rmsnorm_modulate_bwd_gated(dy, x, rstd, onep, ld_mod, dres, dx, M, D, rows_per_batch, nullptr, 0,
+                                        nullptr, stream);
 }
 
 int ltx_layernorm_modulate_fwd(const void* x, const void* shift, const void* onep, int64_t ld_mod, void* y,

@@ -31,6 +31,8 @@ _SIGNATURES = {
     "ltx_rf_prepare_tokens": [_p, _p, _p, _p, _p, _p, _p, _p, _i64, _i64, _i64, _i64, _i64, _p],
     "ltx_rmsnorm_modulate_fwd": [_p, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _f32, _p],
     "ltx_rmsnorm_modulate_bwd": [_p, _p, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _p],
+    "ltx_rmsnorm_modulate_bwd_gated": [_p, _p, _p, _p, _i64, _p, _p, _i64, _i64, _i64, _p, _i64, _p,
+                                       _p],
     "ltx_ada_modulation": [_p, _p, _i64, _i64, _p, _p, _i64, _i64, _i64, _i64, _p],
     "ltx_gate_mul_bf16": [_p, _p, _i64, _p, _i64, _i64, _i64, _p],
     "ltx_layernorm_modulate_fwd": [_p, _p, _p, _i64, _p, _p, _p, _i64, _i64, _i64, _f32, _p],

@@ -171,13 +171,21 @@ def rmsnorm_modulate_fwd(x, shift, onep, ld_mod, rows_per_batch, eps, out=None):
     return y, rstd
 
 
-def rmsnorm_modulate_bwd(dy, x, rstd, onep, ld_mod, rows_per_batch, dres=None, out=None):
+def rmsnorm_modulate_bwd(dy, x, rstd, onep, ld_mod, rows_per_batch, dres=None, out=None,
+                         gate=None):
+    """dx (= dres + the norm/modulate backward). gate (a [B, D] row view): also returns
+    gate_mul(dx, gate, rows_per_batch), bitwise, from the same pass (ltx_rmsnorm_modulate_bwd_gated)."""
     M, D = _dense(x, "x").shape
     _dense(dy, "dy")
     dx = torch.empty(M, D, dtype=BF16, device=x.device) if out is None else out
-    call("ltx_rmsnorm_modulate_bwd", _p(dy), _p(x), _p(rstd), _p(onep), ld_mod, _p(dres), _p(dx),
-         M, D, rows_per_batch, _s())
-    return dx
+    if gate is None:
+        call("ltx_rmsnorm_modulate_bwd", _p(dy), _p(x), _p(rstd), _p(onep), ld_mod, _p(dres),
+             _p(dx), M, D, rows_per_batch, _s())
+        return dx
+    gout = torch.empty(M, D, dtype=BF16, device=x.device)
+    call("ltx_rmsnorm_modulate_bwd_gated", _p(dy), _p(x), _p(rstd), _p(onep), ld_mod, _p(dres),
+         _p(dx), M, D, rows_per_batch, _p(gate), _rows(gate, "gate"), _p(gout), _s())
+    return dx, gout
 
 
 def layernorm_modulate_fwd(x, shift, onep, ld_mod, rows_per_batch, eps):

@@ -383,6 +383,11 @@ class _Shared:
         self.text_stack = None
         self.eps = eps
         self.full = False  # train_mode='full': attention / AdaLN weights take gradients
+        # block id -> the previous block's FF gate row view (mods[:, 5]): the block's backward
+        # also writes the previous block's d_ffo = gate_mul(dh, gate) from its last norm pass,
+        # handed over in ffo_pre = (dh, d_ffo) (LTX_FFGATE_FUSED=0: separate gate_mul launches)
+        self.ffgate = {}
+        self.ffo_pre = None
 
 
 _LORA_KEYS = ("q", "k", "v", "o")
@@ -546,7 +551,12 @@ class _BlockFn(torch.autograd.Function):
             r, s = lora[0].r, lora[0].scaling
         # ---- FF: h3 = h2 + g_mlp * ff(x2)
         rpm = sh.rpm
-        d_ffo = ops.gate_mul(dh3, mods[:, 5], rpm)
+        pre, sh.ffo_pre = sh.ffo_pre, None
+        if pre is not None and pre[0].data_ptr() == dh3.data_ptr() and pre[0].shape == dh3.shape:
+            d_ffo = pre[1]  # written by the next block's last norm pass (bitwise gate_mul)
+        else:
+            d_ffo = ops.gate_mul(dh3, mods[:, 5], rpm)
+        del pre
         if full:  # gate_mlp: sum over the batch's rows of bf16(dh3 * y3) (attention.py:305-308)
             ops.colsum_into(dmods[:, 5], dh3, y3, mode=1, rows_per_group=rpm, sum_groups=False,
                             accumulate=False)
@@ -702,7 +712,14 @@ class _BlockFn(torch.autograd.Function):
         dh = None
         if ctx.needs_input_grad[4] or full:  # (blk, sh, keep, skip, h, ...)
             dx1 = ops.gemm(dqkv, W["qkv_wT"])
-            dh = ops.rmsnorm_modulate_bwd(dx1, h, rstd1, onep[:, 1], ldm, rpm, dres=dh1)
+            g_prev = None if full else sh.ffgate.get(id(blk))
+            if g_prev is not None:
+                dh, d_ffo_prev = ops.rmsnorm_modulate_bwd(dx1, h, rstd1, onep[:, 1], ldm, rpm,
+                                                          dres=dh1, gate=g_prev)
+                sh.ffo_pre = (dh, d_ffo_prev)
+                del d_ffo_prev
+            else:
+                dh = ops.rmsnorm_modulate_bwd(dx1, h, rstd1, onep[:, 1], ldm, rpm, dres=dh1)
             if full:  # shift_msa / scale_msa (attention.py:229-236)
                 ops.colsum_into(dmods[:, 0], dx1, rows_per_group=rpm, sum_groups=False,
                                 accumulate=False)
@@ -1389,6 +1406,9 @@ class Transformer3DModel(nn.Module):
             prep(0)
         else:
             prep = None
+        fuse_gate = keep and not ckpt and not full and strat is None and \
+            os.environ.get("LTX_FFGATE_FUSED", "1") != "0"
+        prev_gate = None
         for i, blk in enumerate(self.transformer_blocks):
             if prep is not None and i + 1 < len(blocks):
                 prep(i + 1)
@@ -1401,6 +1421,10 @@ class Transformer3DModel(nn.Module):
                     mods, onep = ops.ada_modulation(blk.scale_shift_table, tmod,
                                                     (1 << 1) | (1 << 4))
             ab = _lora_ab(blk)
+            if fuse_gate:
+                if prev_gate is not None:
+                    sh.ffgate[id(blk)] = prev_gate
+                prev_gate = mods[:, 5]
             if ckpt:
                 h = torch.utils.checkpoint.checkpoint(
                     lambda *a, _b=blk, _s=skip: _BlockFn.apply(_b, sh, True, _s, *a),
