@@ -217,6 +217,7 @@ def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
 
 @pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),  # no key bias
                                                       (8, 4, 1792, 256, True, True),    # bench's attn2
+                                                      (8, 4, 1792, 128, True, True),    # 128 keys: QS
                                                       (1, 2, 300, 200, True, False),    # ragged both
                                                       (2, 2, 64, 33, False, False)])    # < 2 waves
 def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
@@ -259,6 +260,16 @@ def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
         for e1, e0 in zip(errs["1", f32], errs["0", f32]):
             assert e1 < 2e-2 and e0 < 2e-2, errs
             assert e1 <= 1.25 * e0 + 1e-3, errs
+    if Nk <= 128:  # the query-split one-pass kernel (QS) against the 8 x 32-key one: dQ bitwise
+        monkeypatch.setenv("LTX_ATTN_BWD1", "1")
+        outs = {}
+        for qs in ("1", "0"):
+            monkeypatch.setenv("LTX_ATTN_BWD1_QS", qs)
+            outs[qs] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias,
+                                    kv_shared=shared)
+        assert torch.equal(outs["1"][0], outs["0"][0])
+        for a, b_ in zip(outs["1"][1:], outs["0"][1:]):
+            assert rel(a, b_) < 1e-2
 
 
 @pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),
@@ -309,6 +320,7 @@ def test_attention_padding_blocks_skipped_exactly(B, H, Nq, Nk, valid, shared, m
     keep = torch.arange(Nk, device=DEV)[None, :] < (valid + torch.arange(Bk, device=DEV)[:, None])
     bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
     res = {}
+    monkeypatch.setenv("LTX_ATTN_BWD1_QS", "0")  # the 8 x 32-key kernel: bitwise skip invariance
     for mode in ("1", "0"):
         monkeypatch.setenv("LTX_ATTN_SKIP", mode)
         o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias, kv_shared=shared)
@@ -316,7 +328,20 @@ def test_attention_padding_blocks_skipped_exactly(B, H, Nq, Nk, valid, shared, m
         res[mode] = (o, lse, dq, dk, dv)
     for a, b_ in zip(res["1"], res["0"]):
         assert torch.equal(a, b_)
+    # the query-split backward (every unmasked key below 128 here): dQ bitwise, dK / dV to the
+    # order of two partial sums, padding rows exactly 0
+    monkeypatch.setenv("LTX_ATTN_SKIP", "1")
+    monkeypatch.setenv("LTX_ATTN_BWD1_QS", "1")
+    o, lse = res["1"][:2]
+    dq2, dk2, dv2 = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, kv_shared=shared)
+    assert torch.equal(dq2, res["1"][2])
+    assert rel(dk2, res["1"][3]) < 1e-2 and rel(dv2, res["1"][4]) < 1e-2
+    for t in (dk2, dv2):
+        assert torch.isfinite(t.float()).all()
     o, lse, dq, dk, dv = res["1"]
+    pad2 = ~(keep.repeat(B, 1) if shared else keep).reshape(-1)
+    assert float(dk2.view(-1, H * d)[pad2].abs().max()) == 0.0
+    assert float(dv2.view(-1, H * d)[pad2].abs().max()) == 0.0
     kx = k.repeat(B, 1) if shared else k
     vx = v.repeat(B, 1) if shared else v
     bx = bias.repeat(B, 1) if shared else bias

@@ -648,7 +648,11 @@ __global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BI
 // consecutive image rows, which the row swizzle keeps conflict-free.
 // =============================================================================================
 
-template <int HD, bool BIAS>
+// QS (biased key ranges): when every unmasked key lies below 128 (the caption's padded prompt),
+// waves w and w + 4 hold the same 32 keys and take the two 32-query halves of each tile (instead
+// of the padding-key waves idling and the others running both halves); their dK / dV partials
+// are added through LDS at the end.
+template <int HD, bool BIAS, bool QS>
 __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnParams p) {
   constexpr int QT = 64;
   constexpr int KS = HD / 16;
@@ -665,15 +669,31 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   constexpr int STAT = QT * 4;
   constexpr int SLOT = 2 * TILE + 2 * STAT;  // Q | dO | lse | delta
   constexpr int NSLOT = 3;
-  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + KIMG + 2 * SIMG + 64];
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + KIMG + 2 * SIMG];
   char* kimg = smem + NSLOT * SLOT;
   char* simg0 = kimg + KIMG;
-  unsigned* wact = (unsigned*)(simg0 + 2 * SIMG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const LaneOfs<HD> lofs(lane);
   const int hh = blockIdx.x, b = blockIdx.y;
-  const int kl = wave * 32 + (lane & 31);  // this lane's key
+  // active 32-key blocks (bit kb: a key of kb*32 .. +31 above the padding bias), the same in every
+  // wave. 32-key blocks whose keys are all padding have P = dS = 0 exactly behind any unmasked key:
+  // their S / dP / dK / dV work and their dQ k-steps are skipped (dK = dV = 0 are still stored),
+  // which leaves every output bitwise unchanged (see attn_fwd1_kernel).
+  unsigned kact = 0xffu;
+  if (BIAS && p.skip_masked) {
+    kact = 0u;
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int key = kb * 32 + (lane & 31);
+      float kbv = -INFINITY;
+      if (key < p.Nk) kbv = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + key] * LOG2E : 0.f;
+      if (__any(kbv > KEY_MASKED)) kact |= 1u << kb;
+    }
+    if (kact == 0u) kact = 0xffu;  // no unmasked key at all: keep everything
+  }
+  const bool qs = QS && (kact & 0xf0u) == 0u;  // every active key below 128: split the queries
+  const int kl = (qs ? (wave & 3) : wave) * 32 + (lane & 31);  // this lane's key
   const int kc = min(kl, p.Nk - 1);
   const float c2 = p.scale * LOG2E;
   float kbias = 0.f;
@@ -682,10 +702,6 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
     if (kl < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + kl] * LOG2E : 0.f;
   }
   const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
-  // 32-key blocks (one per wave) whose keys are all padding have P = dS = 0 exactly behind any
-  // unmasked key: their S / dP / dK / dV work and their dQ k-steps are skipped (dK = dV = 0 are
-  // still stored), which leaves every output bitwise unchanged (see attn_fwd1_kernel).
-  if (lane == 0) wact[wave] = (BIAS && p.skip_masked) ? (__any(kbias > KEY_MASKED) ? 1u : 0u) : 1u;
   s16x8 kf[KS], vf[KS];
   {
     const bf16_t* kr = kbase + (int64_t)kc * p.ldk;
@@ -813,11 +829,9 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   dma(0);
   if (ntiles > 1) dma(1);
   tile_sync(0, ntiles > 1);
-  kmask = 0u;
-#pragma unroll
-  for (int w = 0; w < 8; ++w) kmask |= wact[w] << w;
-  if (kmask == 0u) kmask = 0xffu;  // no unmasked key at all: keep everything
-  const bool mine = (kmask >> wave) & 1u;
+  kmask = kact;
+  asm volatile("" : "+s"(kmask));  // opaque: the dQ k-step loop keeps its per-step test
+  const bool mine = (kmask >> (kl >> 5)) & 1u;
 
   // Tile t's dQ product runs during tile t+1's S / dP / dK / dV (its dS image is the other
   // buffer): one barrier interval holds both, so the dQ MFMAs fill the softmax VALU gaps. Its
@@ -838,7 +852,7 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
     if (t + 2 < ntiles) dma(t + 2);  // into tile t-1's slot (last read before the barrier)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      if (!mine) {  // padding keys: only this wave's share of the dQ product
+      if (!mine || (qs && u != (wave >> 2))) {  // padding keys / the other wave's half: dQ share only
         if (t > 0) dq_steps(sprev, u * (KSTEPS / 2), (u + 1) * (KSTEPS / 2));
         continue;
       }
@@ -902,6 +916,38 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   dq_steps(simg0 + ((ntiles - 1) & 1) * SIMG, 0, KSTEPS);
   dq_store((ntiles - 1) * QT);
+  if (qs) {  // waves 4-7's dK / dV partials into waves 0-3 (the dS images are free now)
+    static_assert(4 * 2 * DS * 16 * 64 * 4 <= 2 * SIMG, "partials fit the dS images");
+    float* xs = (float*)simg0 + (wave & 3) * (2 * DS * 16 * 64) + lane;
+    __syncthreads();
+    if (wave >= 4) {
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          xs[((2 * d) * 16 + r) * 64] = dka[d][r];
+          xs[((2 * d + 1) * 16 + r) * 64] = dva[d][r];
+        }
+    }
+    __syncthreads();
+    if (wave >= 4) {  // keys 128 + 32 (w - 4) ..: all padding under qs, so dK = dV = 0 exactly
+      const int kz = 128 + kl;
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dka[d][r] = 0.f;
+      store_row_swap<HD>(dka, 1.0f, kz < p.Nk ? p.dk + ((int64_t)b * p.Nk + kz) * p.lddk + hh * HD : nullptr, lane);
+      store_row_swap<HD>(dka, 1.0f, kz < p.Nk ? p.dv + ((int64_t)b * p.Nk + kz) * p.lddv + hh * HD : nullptr, lane);
+      return;
+    }
+#pragma unroll
+    for (int d = 0; d < DS; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dka[d][r] += xs[((2 * d) * 16 + r) * 64];
+        dva[d][r] += xs[((2 * d + 1) * 16 + r) * 64];
+      }
+  }
   // dK, dV rows in 16-B pieces (store_row_swap: both lane halves take part)
   const bool kin = kl < p.Nk;
   store_row_swap<HD>(dka, p.scale, kin ? p.dk + ((int64_t)b * p.Nk + kl) * p.lddk + hh * HD : nullptr, lane);
@@ -976,6 +1022,13 @@ static int fwd1_flag() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
+// LTX_ATTN_BWD1_QS=1: biased key ranges may split the queries (read per call; off by default
+// until measured)
+static int bwd1_qs_flag() {
+  const char* e = std::getenv("LTX_ATTN_BWD1_QS");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
 template <int HD>
 static int launch_fwd(AttnParams p, hipStream_t s) {
   p.xcd_order = xcd_order_flag();
@@ -1027,10 +1080,12 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   if constexpr (HD == 64) {  // (head dim 32, the tiny config, keeps the split kernels)
     if (p.Nk <= BWD1_KEYS && bwd1_flag()) {  // every key in one workgroup: one-pass backward
       const dim3 g1((unsigned)p.H, (unsigned)p.B);
-      if (p.key_bias != nullptr || p.Nk != BWD1_KEYS)
-        hipLaunchKernelGGL((attn_bwd1_kernel<HD, true>), g1, dim3(BWD1_THREADS), 0, s, p);
+      if ((p.key_bias != nullptr || p.Nk != BWD1_KEYS) && bwd1_qs_flag())
+        hipLaunchKernelGGL((attn_bwd1_kernel<HD, true, true>), g1, dim3(BWD1_THREADS), 0, s, p);
+      else if (p.key_bias != nullptr || p.Nk != BWD1_KEYS)
+        hipLaunchKernelGGL((attn_bwd1_kernel<HD, true, false>), g1, dim3(BWD1_THREADS), 0, s, p);
       else
-        hipLaunchKernelGGL((attn_bwd1_kernel<HD, false>), g1, dim3(BWD1_THREADS), 0, s, p);
+        hipLaunchKernelGGL((attn_bwd1_kernel<HD, false, false>), g1, dim3(BWD1_THREADS), 0, s, p);
       LTX_LAUNCH_CHECK();
       return LTX_OK;
     }
