@@ -1022,11 +1022,10 @@ static int fwd1_flag() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
-// LTX_ATTN_BWD1_QS=1: biased key ranges may split the queries (read per call; off by default
-// until measured)
+// LTX_ATTN_BWD1_QS=0: biased key ranges keep the 8 x 32-key one-pass backward (read per call)
 static int bwd1_qs_flag() {
   const char* e = std::getenv("LTX_ATTN_BWD1_QS");
-  return (e && e[0] == '1') ? 1 : 0;
+  return (e && e[0] == '0') ? 0 : 1;
 }
 
 template <int HD>
