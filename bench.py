@@ -33,15 +33,20 @@ import torch.distributed as dist
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, spec)
 HBM_PEAK_GBS = 8000.0
 B_PER_GPU, F_LAT, H_LAT, W_LAT, L_TXT = 8, 7, 16, 16, 256
+N_VALID_TXT = 16  # valid caption tokens of the synthetic prompt (mask below)
 LORA_RANK = 16
 ACCUM = 16
 
 
-def step_flops_per_sample(N, r=LORA_RANK, D=2048, FF=8192, Lyr=28, L=L_TXT, C=128, Cc=4096):
+def step_flops_per_sample(N, r=LORA_RANK, D=2048, FF=8192, Lyr=28, L=L_TXT, C=128, Cc=4096, L_att=None):
     """Algorithmic FLOPs of one fwd+bwd per sample: dgrad-only for frozen
-    weights, wgrad for LoRA and caption_projection, attention bwd = 2x fwd, no recompute."""
+    weights, wgrad for LoRA and caption_projection, attention bwd = 2x fwd, no recompute.
+    L_att: caption keys counted in the cross-attention contractions (default L = 256, SURVEY
+    8d; the valid-token count 16 leaves out the padding keys, whose products are exact zeros that
+    the kernels skip)."""
+    L_att = L if L_att is None else L_att
     lin = 2 * N * D * D * 6 + 4 * L * D * D + 4 * N * D * FF
-    att = 4 * N * N * D + 4 * N * L * D
+    att = 4 * N * N * D + 4 * N * L_att * D
     lora = 8 * r * D * (N + L)
     fwd = Lyr * (lin + att + lora) + 4 * N * C * D + 2 * L * (Cc * D + D * D)
     bwd = Lyr * (lin + 2 * att + 2 * lora) + 2 * N * D * C + 2 * L * (Cc * D + D * D) + 2 * L * D * D
@@ -96,7 +101,7 @@ def synthetic_batch(device, rank):
              "pose_latents": torch.randn(B, 128, F_LAT, H_LAT, W_LAT, generator=g)}
     batch = {k: v.to(device=device, dtype=torch.bfloat16) for k, v in batch.items()}
     prompt = torch.randn(1, L_TXT, 4096, generator=g).to(device=device, dtype=torch.bfloat16)
-    mask = (torch.arange(L_TXT) < 16).long().view(1, L_TXT).to(device)
+    mask = (torch.arange(L_TXT) < N_VALID_TXT).long().view(1, L_TXT).to(device)
     return batch, prompt, mask
 
 
@@ -418,6 +423,10 @@ def main():
     if full:  # + wgrad of every attention projection, adaln_single, proj_out (2*M*K*N each)
         bwd += 28 * (2 * N * 2048 * 2048 * 6 + 4 * L_TXT * 2048 * 2048) + 2 * N * 2048 * 128
     step_tflops = (fwd + bwd) * B_PER_GPU * args.steps / (elapsed * 1e12)  # per GPU
+    # the same without the cross-attention's padding keys (16 of 256 caption tokens valid: the
+    # skipped key blocks' products are exact zeros, VERDICT r03 asks for both figures)
+    fwd_v, bwd_v = step_flops_per_sample(N, r=LORA_RANK, L_att=N_VALID_TXT)
+    step_tflops_valid = step_tflops * (fwd_v + bwd_v) / (fwd + bwd)
     # the dominant kernel = the class with the most HIP-event time in the ranking step (all of them
     # are hand-written); its algorithmic TFLOP/s = its FLOPs / its summed launch durations
     for k in kernels + [dom]:
@@ -459,6 +468,8 @@ def main():
                                             else "skipped, exact")},
         "step_tflops_per_gpu": round(step_tflops, 1),
         "step_mfma_frac": round(step_tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+        "step_tflops_per_gpu_excl_padding_keys": round(step_tflops_valid, 1),
+        "step_mfma_frac_excl_padding_keys": round(step_tflops_valid / MFMA_BF16_PEAK_TFLOPS, 4),
         "roofline": {"bound": "mfma", "kernel": dom["kernel"],
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4),

@@ -1,0 +1,144 @@
+"""Generates video-generation-for-human-avatars_amd/csrc/gemm_ring_body.h: the hand-scheduled K loop of
+gemm_ring_kernel (gemm_ring.hip) as inline-asm strings, one per m-fragment count MF (7: 224-row
+tiles, 8: 256-row tiles).
+
+Geometry (per workgroup): a BMT x 256 output tile (BMT = 16 * MF * 2), 4 waves at one wave per SIMD,
+wave w owns rows (w >> 1) * 16 * MF .. and columns (w & 1) * 128 .. as MF x 8 fragments of
+v_mfma_f32_16x16x32_bf16 (accumulators in AGPRs). K is walked in 32-deep half-steps j = 0 .. H - 1.
+LDS is a ring of S = 4 slots, one half-step each: [X: BMT rows x 64 B][W: 256 rows x 64 B], 16-B
+chunk c of row r stored at c ^ g((r >> 2) & 3), g = {0, 2, 3, 1} (conflict-free fragment reads; the
+LDS-DMA writes lane-linear, so the same XOR is applied to the per-lane SOURCE chunk).
+
+Phase P(j) (56 or 64 MFMAs on the fragments F(j) in registers):
+  s_waitcnt vmcnt(16) lgkmcnt(0); s_barrier     -- every wave's DMA of half-step j + 1 has landed
+                                                   and every wave has finished reading slot j % S
+  MFMAs on F(j); between them: ds_read F(j + 1) from slot (j + 1) % S (first MF + 8 gaps),
+  LDS-DMA of half-step j + S into slot j % S (8 pieces of 1 KiB per wave, one every 5 MFMAs, M0
+  written one MFMA ahead of its piece: the M0 -> LDS-DMA wait state).
+The DMA of half-step j + S therefore has two whole phases (~1800 cycles) to land before the wait at
+the start of P(j + S - 1). F(j) / F(j + 1) alternate between two register sets; the loop body is
+the 4 phases of one ring turn (2 K-tiles), and a last turn without DMA drains the ring with
+vmcnt(16) / (8) / (0). Requires H % 4 == 0 (K % 128 == 0) and H >= 4.
+
+Operands (see gemm_ring.hip): %0 .. : accumulators acc[i * MF + jm] ("+a", i = n-fragment 0..7,
+jm = m-fragment), then the fragment registers ("=&v", set 0 W[0..7] X[0..MF-1], set 1 likewise),
+then named operands.
+"""
+import os
+import sys
+
+S = 4
+G = [0, 2, 3, 1]
+
+
+def body(MF):
+    NA = 8 * MF                  # accumulator tuples
+    NFR = 8 + MF                 # fragment registers per set
+    SLOT = MF * 32 * 64 + 256 * 64
+    XREG = 0                     # X region offset inside a slot
+    WREG = MF * 32 * 64
+    fr = lambda st, k: "%" + str(NA + st * NFR + k)   # k < 8: W frag k; k >= 8: X frag k - 8
+    acc = lambda i, jm: "%" + str(i * MF + jm)
+    L = []
+    a = L.append
+
+    def reads(st, slot):
+        # 8 W fragments then MF X fragments of the half-step in `slot` into register set st
+        out = []
+        wb = "%[wr0]" if slot < 2 else "%[wr2]"
+        xb = "%[xr0]" if slot < 2 else "%[xr2]"
+        so = (slot % 2) * SLOT
+        for i in range(8):
+            out.append(f"ds_read_b128 {fr(st, i)}, {wb} offset:{so + WREG + i * 1024}")
+        for jm in range(MF):
+            out.append(f"ds_read_b128 {fr(st, 8 + jm)}, {xb} offset:{so + XREG + jm * 1024}")
+        return out
+
+    def dmas(slot):
+        # 8 pieces of this wave into `slot`: X piece p (p even: X, p odd: W), M0 then the load
+        out = []
+        for p in range(8):
+            srd = "%[xsrd]" if p % 2 == 0 else "%[wsrd]"
+            m0 = f"s_add_u32 m0, %[d{p}], {slot * SLOT}"
+            ld = f"buffer_load_dwordx4 %[o{p}], {srd}, %[koff] offen lds"
+            out.append((m0, ld))
+        return out
+
+    def advance():
+        return ["s_add_u32 %[koff], %[koff], 64"]
+
+    def phase(p, vm, with_dma, last):
+        # ring position p (0..3): computes set p % 2, reads slot (p + 1) % S into the other set
+        st = p % 2
+        a(f"s_waitcnt vmcnt({vm}) lgkmcnt(0)")
+        a("s_barrier")
+        rd = [] if last else reads(1 - st, (p + 1) % S)
+        dm = dmas(p) if with_dma else []
+        mf = [(i, jm) for i in range(8) for jm in range(MF)]
+        nm = len(mf)
+        # slot plan after MFMA q: the fragment reads in every second gap from the start, the DMA
+        # pieces spread evenly over the phase (odd gaps), M0 one gap ahead of its piece
+        after = {q: [] for q in range(nm)}
+        for k, r in enumerate(rd):
+            after[2 * k].append(r)
+        if dm:
+            step = (nm - 6) // 8
+            for k, (m0, ld) in enumerate(dm):
+                q = 3 + k * step
+                after[q - 1].append(m0)
+                after[q].append(ld)
+            after[3 + 7 * step + 1].extend(advance())
+        for q, (i, jm) in enumerate(mf):
+            a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
+            L.extend(after[q])
+
+    a("s_nop 4")  # SGPR operands fresh from v_readfirstlane -> buffer descriptor / soffset reads
+    a("s_mov_b32 %[keep], m0")
+    # prologue: half-steps 0..3 into slots 0..3, then F(0)
+    for slot in range(S):
+        for m0, ld in dmas(slot):
+            a(m0)
+            a("s_nop 0")
+            a(ld)
+        L.extend(advance())
+    a("s_waitcnt vmcnt(24)")
+    a("s_barrier")
+    L.extend(reads(0, 0))
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc1 L_tail_%=")
+    a("L_loop_%=:")
+    for p in range(S):
+        phase(p, 16, True, False)
+    a("s_sub_u32 %[iters], %[iters], 1")
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc0 L_loop_%=")
+    a("L_tail_%=:")
+    for p, vm in enumerate([16, 8, 0, 0]):
+        phase(p, vm, False, p == S - 1)
+    a("s_mov_b32 m0, %[keep]")
+    a("s_nop 15")
+    a("s_nop 15")
+    return L
+
+
+def emit(MF):
+    lines = body(MF)
+    s = "\n".join(f'  "{l}\\n\\t"' for l in lines)
+    return f"#define LTX_RING_BODY_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n"
+
+
+def main():
+    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+        "video-generation-for-human-avatars_amd", "csrc", "gemm_ring_body.h")
+    txt = ["// GENERATED by tools/gen_gemm_ring.py -- do not edit by hand.",
+           "// The hand-scheduled K loop of gemm_ring_kernel (gemm_ring.hip); see the generator's docstring.",
+           "#pragma once", ""]
+    for MF in (7, 8):
+        txt.append(emit(MF))
+    open(out, "w").write("\n".join(txt))
+    print(out)
+
+
+if __name__ == "__main__":
+    main()

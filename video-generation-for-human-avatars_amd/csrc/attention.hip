@@ -1022,10 +1022,12 @@ static int fwd1_flag() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 
-// LTX_ATTN_BWD1_QS=0: biased key ranges keep the 8 x 32-key one-pass backward (read per call)
+// LTX_ATTN_BWD1_QS=1: biased key ranges take the query-split one-pass backward (read per call).
+// Off by default: its step A/B was neutral, and with it dK / dV of the unmasked keys are the sum
+// of two partials (f32 rounding away from the 8 x 32-key kernel; dQ stays bitwise)
 static int bwd1_qs_flag() {
   const char* e = std::getenv("LTX_ATTN_BWD1_QS");
-  return (e && e[0] == '0') ? 0 : 1;
+  return (e && e[0] == '1') ? 1 : 0;
 }
 
 template <int HD>

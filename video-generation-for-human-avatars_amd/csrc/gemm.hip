@@ -21,6 +21,7 @@
 #include "common.h"
 #include "ltx_hip.h"
 #include "gemm_common.h"
+#include "gemm_ring.h"
 
 namespace ltx {
 
@@ -591,6 +592,13 @@ static int g_variant = [] {
   const char* e = getenv("LTX_GEMM_VARIANT");
   return e ? atoi(e) : 0;
 }();
+// LTX_GEMM_RING=1 (or variant 20): the large-tile calls that gemm_ring_kernel supports run it
+// (gemm_ring.h: hand-scheduled K loop, 4 waves at one wave per SIMD)
+static int g_ring = [] {
+  const char* e = getenv("LTX_GEMM_RING");
+  return (e && e[0] == '1') ? 1 : 0;
+}();
+static bool ring_applies(const GemmParams& p) { return p.K2 == 0 && p.K % 128 == 0 && p.K >= 128; }
 // LTX_GEMM_DMA_BATCH=0: the large-tile kernel issues each LDS-DMA piece in its own asm block
 // (M0 saved / set / restored per piece) instead of one block per wave's piece set
 static int g_dma_batch = [] {
@@ -605,7 +613,7 @@ static int g_epi_batch = [] {
 
 // The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can
 // attribute its per-launch timings to the kernel rocprof will name).
-enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_SMALL = 3 };
+enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_SMALL = 3, PATH_RING = 4 };
 struct GemmPlan {
   GemmPath path;
   int bmt;     // PATH_T: tile height (256 or 224)
@@ -646,7 +654,8 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
     auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
     // the tile height that fills the last round best; variant 13 forces BMT 256, 14 forces 224
     const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
-    return GemmPlan{PATH_T, use224 ? 224 : 256, 1, 2};
+    const bool ring = (g_ring || g_variant == 20) && ring_applies(p);
+    return GemmPlan{ring ? PATH_RING : PATH_T, use224 ? 224 : 256, 1, 2};
   }
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int tiles = ntm * ntn;
@@ -676,6 +685,9 @@ static void describe_plan(const GemmPlan& pl, int epi, int R, char* buf, size_t 
       snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, %d, %d, 0>(ltx::GemmParams)", epi, R, pl.bmt,
                pl.bmt == 224 ? 4 : 8);
       break;
+    case PATH_RING:
+      snprintf(buf, len, "ltx::gemm_ring_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt / 32);
+      break;
     default:
       snprintf(buf, len, "ltx::gemm_nt_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.nst);
       break;
@@ -704,7 +716,11 @@ static int launch(const GemmParams& p, hipStream_t s) {
     LTX_LAUNCH_CHECK();
     return LTX_OK;
   }
-  if (pl.path == PATH_T) {
+  if (pl.path == PATH_RING && launch_ring<EPI, R>(p, pl.bmt, s)) {
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+  if (pl.path == PATH_T || pl.path == PATH_RING) {
     static bool t_set = false;
     if (!t_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
@@ -774,7 +790,8 @@ static int launch_lora(const GemmParams& p, hipStream_t s) {
 using namespace ltx;
 
 extern "C" int ltx_gemm_set_variant(int variant) {
-  LTX_CHECK_ARG(variant == 0 || variant == 13 || variant == 14, "gemm_set_variant: 0, 13 or 14");
+  LTX_CHECK_ARG(variant == 0 || variant == 13 || variant == 14 || variant == 20,
+                "gemm_set_variant: 0, 13, 14 or 20 (ring kernel)");
   g_variant = variant;
   return LTX_OK;
 }
@@ -885,6 +902,8 @@ extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, 
     case LTX_EPI_GELU: return launch<LTX_EPI_GELU>(p, s);
     case LTX_EPI_GATED_RESIDUAL:
       LTX_CHECK_ARG(aux0 && aux1, "gemm gated residual: needs residual (aux0) and gate (aux1)");
+      LTX_CHECK_ARG(ld1 % 8 == 0 && ((uintptr_t)aux1 % 16) == 0 && (!aux2 || (ld2 % 8 == 0 && ((uintptr_t)aux2 % 16) == 0)),
+                    "gemm gated residual: gate rows (aux1) and the pre-gate store (aux2) must be 16-B aligned rows");
       return launch<LTX_EPI_GATED_RESIDUAL>(p, s);
     case LTX_EPI_LORA:
     case LTX_EPI_LORA_RESIDUAL:
@@ -897,8 +916,9 @@ extern "C" int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, 
       return launch<LTX_EPI_GELU_BWD>(p, s);
     case LTX_EPI_ACCUM:
       LTX_CHECK_ARG(aux0, "gemm accum: needs the accumulator input (aux0)");
-      LTX_CHECK_ARG(!aux1 == !aux2 && (!aux1 || (ld1 % 8 == 0 && ld2 % 8 == 0 && ld2 >= N && M % p.rows_per_batch == 0)),
-                    "gemm accum: the gated copy needs both the gate rows (aux1) and its output (aux2), 16-B rows");
+      LTX_CHECK_ARG(!aux1 == !aux2 && (!aux1 || (ld1 % 8 == 0 && ld2 % 8 == 0 && ld2 >= N && M % p.rows_per_batch == 0 &&
+                                                 ((uintptr_t)aux1 | (uintptr_t)aux2) % 16 == 0)),
+                    "gemm accum: the gated copy needs both the gate rows (aux1) and its output (aux2), 16-B aligned rows");
       return launch<LTX_EPI_ACCUM>(p, s);
     case LTX_EPI_LORA_DGRAD_ACCUM:
       LTX_CHECK_ARG(aux1 && aux2, "gemm lora dgrad: needs Wd (aux1) and A (aux2)");

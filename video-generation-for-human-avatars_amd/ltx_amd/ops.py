@@ -365,8 +365,11 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
     bias = "true" if key_bias is not None else "false"
     if d == 64 and Nk <= 256 and os.environ.get("LTX_ATTN_BWD1", "1") != "0":
         # every key in one workgroup: the one-pass kernel (attention.hip attn_bwd1_kernel)
-        b1 = "true" if (key_bias is not None or Nk != 256) else "false"
-        kern = f"ltx::attn_bwd1_kernel<{d}, {b1}>"
+        # the name rocprofv3 prints: <d, biased, query-split>, the split read from the same switch
+        # the library reads (attention.hip bwd1_qs_flag: on only with LTX_ATTN_BWD1_QS=1)
+        biased = key_bias is not None or Nk != 256
+        qs = "true" if (biased and os.environ.get("LTX_ATTN_BWD1_QS", "0") == "1") else "false"
+        kern = f"ltx::attn_bwd1_kernel<{d}, {'true' if biased else 'false'}, {qs}>"
     elif d == 64 and _env_on("LTX_ATTN_DKDV_PIPE"):  # the pipelined kernels (attention_pipe.hip)
         kb = "true" if (key_bias is not None or Nk % 64) else "false"
         dqk = ("ltx::attn_dq_pipe_kernel" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
@@ -547,9 +550,11 @@ def lora_down(x, wr, alpha=1.0, transposed=False, out=None, split=False, split_o
     kernel. groups > 1 runs `groups` adapters in one launch (ltx_lora_down_grouped): wr is the
     first adapter, group_strides = element offsets per group of (x, wr, out, split); the caller
     passes out (and split_out) covering every group. pieces = lora_pieces(wr, transposed) (the
-    caller's cache) routes token-sized calls to the bf16-matrix-core kernel (ltx_lora_rows)."""
+    caller's cache) routes token-sized calls to the bf16-matrix-core kernel (ltx_lora_rows); a
+    callable is invoked only when that route is taken (the pieces are built lazily)."""
     M, K = x.shape
     if pieces is not None and _LORA_ROWS and groups == 1 and M >= 8192 and K % 256 == 0:
+        pieces = pieces() if callable(pieces) else pieces
         return lora_rows(x, pieces, wr.shape[1] if transposed else wr.shape[0], alpha=alpha,
                          out=out, split=split, split_out=split_out)
     if transposed:

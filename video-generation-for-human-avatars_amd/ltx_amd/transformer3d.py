@@ -482,7 +482,7 @@ class _BlockFn(torch.autograd.Function):
         if has_lora:
             # peft LoRA fused into the K loop: [x | split(x.A^T)] . [W | split(s*B)]^T
             Aq, Bq, Ak, Bk, Av, Bv, Ao, Bo = lora_ab
-            u_q, su = ops.lora_down(h1, Aq, split=True, pieces=lora[0].weight_pieces("A"))
+            u_q, su = ops.lora_down(h1, Aq, split=True, pieces=lambda: lora[0].weight_pieces("A"))
             q2raw = ops.gemm(h1, wq, bias=bq, ext=(su, lora[0].weight_split("B")))
             del su
         else:
@@ -499,7 +499,7 @@ class _BlockFn(torch.autograd.Function):
         o2, lse2 = ops.attn_fwd(q2, k2, v2, B, H, d, a2.scale, key_bias=sh.enc_bias,
                                 kv_shared=sh.text_shared)
         if has_lora:
-            u_o, su = ops.lora_down(o2, Ao, split=True, pieces=lora[3].weight_pieces("A"))
+            u_o, su = ops.lora_down(o2, Ao, split=True, pieces=lambda: lora[3].weight_pieces("A"))
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1,
                           ext=(su, lora[3].weight_split("B")))
             del su
@@ -552,6 +552,9 @@ class _BlockFn(torch.autograd.Function):
         # ---- FF: h3 = h2 + g_mlp * ff(x2)
         rpm = sh.rpm
         pre, sh.ffo_pre = sh.ffo_pre, None
+        # accepted only for the very dh buffer the next block's norm pass wrote. Safe because
+        # ffo_pre holds a reference to that dh: while it is alive autograd cannot accumulate
+        # another gradient into the buffer in place, so d_ffo = bf16(dh * g_mlp) still matches it
         if pre is not None and pre[0].data_ptr() == dh3.data_ptr() and pre[0].shape == dh3.shape:
             d_ffo = pre[1]  # written by the next block's last norm pass (bitwise gate_mul)
         else:
@@ -582,7 +585,7 @@ class _BlockFn(torch.autograd.Function):
             else:
                 ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
                 w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True,
-                                         pieces=lo.weight_pieces("Bt"))
+                                         pieces=lambda: lo.weight_pieces("Bt"))
             ops.lora_wgrad(o2, w_o, transpose_out=True, out=_grad_buf(lo, "A"), accumulate=True)
             do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")), **rd)
         else:
@@ -649,7 +652,7 @@ class _BlockFn(torch.autograd.Function):
             else:
                 ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
                 w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True,
-                                         pieces=lq.weight_pieces("Bt"))
+                                         pieces=lambda: lq.weight_pieces("Bt"))
             ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
                            ext=(sw, lq.weight_split("A")), **gated)
