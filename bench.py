@@ -355,7 +355,10 @@ def main():
     trainable = [p for p in model.parameters() if p.requires_grad]
     if full:
         from ltx_amd.zero import Zero2AdamW
-        opt = Zero2AdamW(trainable, lr=cfg.learning_rate, gradient_clipping=1.0)
+        # ds_config_zero2.json: reduce_scatter of f32 grads in 5e8-element buckets, overlap_comm:
+        # buckets in the backward's completion order, launched from its hooks on the last micro-step
+        opt = Zero2AdamW(trainable, lr=cfg.learning_rate, gradient_clipping=1.0,
+                         order=model.grad_ready_order()).install(model)
         reducer = lambda: None  # noqa: E731  (the reduce-scatter is inside Zero2AdamW.step)
     else:
         opt = FusedAdamW(trainable, lr=cfg.learning_rate)
@@ -370,8 +373,8 @@ def main():
 
     def one_step(i):
         last = (i + 1) % ACCUM == 0
-        if last and not full:
-            reducer.arm()
+        if last:
+            (opt if full else reducer).arm()
         train_step(model, batch, sched, model.patchifier, cfg, prompt, mask, device)
         if last:
             reducer()

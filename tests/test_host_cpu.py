@@ -423,7 +423,7 @@ def test_grad_allreduce_overlapped_with_backward_gloo_world2(full):
             assert torch.equal(res[r]["overlap"]["grads"][i], exp), (r, i)
 
 
-# ------------------------------------------------------------------ ZeRO-2 (gloo, world size 2)
+# ------------------------------------------------------------------ ZeRO-2 (gloo, world 2 / 3 / 8)
 ZSHAPES = [(16, 64), (64,), (300,), (7, 5), (1001,)]
 Z_LR, Z_CLIP, Z_STEPS = 1e-2, 0.5, 3
 
@@ -436,6 +436,14 @@ def _ref_adamw(master, g, m, v, step, lr, b1=0.9, b2=0.999, eps=1e-8, wd=1e-2):
     bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
     denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
     master.addcdiv_(m, denom, value=-lr / bc1)
+
+
+def _clip_coef(sumsq, world, clip):
+    """ltx_clip_scale_f32's factor: the averaged grads' global norm -> min(1, clip / (norm + 1e-6)),
+    applied with the 1/world average as one f32 multiplier"""
+    norm = math.sqrt(sumsq) / world
+    c = min(1.0, clip / (norm + 1e-6)) if clip > 0 else 1.0
+    return torch.tensor(c / world, dtype=torch.float32)
 
 
 def _zero_cpu_cls():
@@ -454,42 +462,111 @@ def _zero_cpu_cls():
             out.fill_(float((x.double() ** 2).sum()))
 
         def _clip_scale(self, x, sumsq, coef):
-            norm = math.sqrt(float(sumsq)) / self.world
-            c = min(1.0, self.clip / (norm + 1e-6)) if self.clip > 0 else 1.0
-            coef.fill_(c / self.world)
-            x.mul_(float(coef))
+            coef.copy_(_clip_coef(float(sumsq), self.world, self.clip))
+            x.mul_(coef)
 
         def _adamw(self, master, g, m, v, step):
             _ref_adamw(master, g, m, v, step, self.lr)
     return CpuZero2
 
 
+def _exact_grad(shape, g):
+    """grads whose f32 sums over up to 8 ranks are exact in any order (multiples of 2^-6 in
+    [-2, 2], exact in bf16), so a reduce-scatter matches the sequential sum bit for bit"""
+    return (torch.randint(-128, 129, shape, generator=g).float() / 64).to(torch.bfloat16)
+
+
+class _FakeBlockBf16(torch.nn.Module):
+    def __init__(self, g):
+        super().__init__()
+        self.attn2 = torch.nn.Module()
+        self.attn2.w = torch.nn.Parameter((torch.randn(8, 8, generator=g) * 0.3).to(torch.bfloat16))
+        self.scale_shift_table = torch.nn.Parameter((torch.randn(1, 8, generator=g) * 0.1).to(torch.bfloat16))
+
+
+class _FakeZeroModel(torch.nn.Module):
+    """bf16 twin of _FakeModel for ZeRO-2 (train_mode='full'): caption + 3 blocks whose attn2
+    weight gradient is written by the 'kernel' (block hook) and whose scale_shift_table gradient
+    autograd accumulates after the block's backward (post-accumulate-grad hook)."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(3)
+        self.cap = torch.nn.Parameter(torch.randn(8, 8, generator=g).to(torch.bfloat16))
+        self.transformer_blocks = torch.nn.ModuleList([_FakeBlockBf16(g) for _ in range(3)])
+
+    def forward(self, x):
+        h = x.to(torch.bfloat16) @ self.cap
+        for b in self.transformer_blocks:
+            h = _FakeBlockFn.apply(b, h, b.scale_shift_table * 1.0)
+        return h
+
+    def grad_ready_order(self):
+        order = []
+        for b in reversed(self.transformer_blocks):
+            order += [p for p in b.parameters() if p.requires_grad]
+        return order + [self.cap]
+
+
 def _zero_worker(rank, world, port, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        res = {}
+        # (a) the partition / bucket / clip bookkeeping against single-process math
         g0 = torch.Generator().manual_seed(7)
-        params = [torch.nn.Parameter(torch.randn(s, generator=g0).to(torch.bfloat16))
-                  for s in ZSHAPES]
+        params = [torch.nn.Parameter(torch.randn(s, generator=g0).to(torch.bfloat16)) for s in ZSHAPES]
         opt = _zero_cpu_cls()(params, lr=Z_LR, gradient_clipping=Z_CLIP, bucket_elems=512)
+        assert len(opt.buckets) > 2 and all(b["n"] % world == 0 for b in opt.buckets)
         g = torch.Generator().manual_seed(100 + rank)
         for _ in range(Z_STEPS):
             for p in params:  # accumulate into the flat-buffer views, as the kernels do
-                p.grad.add_(torch.randn(p.shape, generator=g).to(torch.bfloat16))
+                p.grad.add_(_exact_grad(p.shape, g))
             opt.step()
             opt.zero_grad()
-        torch.save([p.detach().clone() for p in params], os.path.join(out_dir, f"z{rank}.pt"))
+        res["math"] = [p.detach().clone() for p in params]
+        # (b) overlap_comm: the armed path (reduce-scatters launched from the backward's hooks)
+        # against the post-hoc one, and the bf16 reduction next to the f32 one
+        for mode in ("armed", "posthoc", "bf16"):
+            m = _FakeZeroModel()
+            launched_at_cap, box = [], []
+            m.cap.register_post_accumulate_grad_hook(lambda p: launched_at_cap.append(box[0]._launched))
+            kw = dict(lr=Z_LR, gradient_clipping=Z_CLIP, bucket_elems=72, order=m.grad_ready_order())
+            if mode == "bf16":
+                kw["reduce_dtype"] = torch.bfloat16
+            opt = _zero_cpu_cls()(list(m.parameters()), **kw)
+            if mode == "armed":
+                opt.install(m)
+            box.append(opt)
+            g = torch.Generator().manual_seed(200 + rank)
+            for step in range(2):
+                for micro in range(3):
+                    if mode == "armed" and micro == 2:
+                        opt.arm()
+                    x = (torch.randint(-4, 5, (4, 8), generator=g).float() / 4)
+                    m(x).float().square().sum().backward()
+                opt.step()
+                opt.zero_grad()
+            res[mode] = {"params": [p.detach().clone() for p in m.parameters()],
+                         "launched_at_cap": launched_at_cap[2] if launched_at_cap else -1,
+                         "buckets": len(opt.buckets)}
+        torch.save(res, os.path.join(out_dir, f"z{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
 
-def test_zero2_gloo_world2_matches_single_process_math():
-    world = 2
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_zero2_gloo_matches_single_process_math(world):
+    """Zero2AdamW at world 2, 3 (padded buckets) and 8 over gloo: the final weights of every rank
+    are BITWISE those of one process keeping an f32 master of all parameters and applying the
+    averaged, globally clipped gradients with torch AdamW's math (the grads are exact under any
+    summation order); the overlapped (armed) reduce-scatter path is bitwise the post-hoc one and
+    launches the block buckets during the backward; the bf16 reduction stays within bf16 rounding."""
     with tempfile.TemporaryDirectory() as td:
         mp.start_processes(_zero_worker, args=(world, _free_port(), td), nprocs=world,
                            start_method="spawn", join=True)
         res = [torch.load(os.path.join(td, f"z{r}.pt"), weights_only=True) for r in range(world)]
-    # reference: one process, f32 master of all params, averaged + globally clipped grads
+    # (a) reference: one process, f32 master of all params, averaged + globally clipped grads
     g0 = torch.Generator().manual_seed(7)
     params = [torch.randn(s, generator=g0).to(torch.bfloat16) for s in ZSHAPES]
     master = [p.float() for p in params]
@@ -497,22 +574,29 @@ def test_zero2_gloo_world2_matches_single_process_math():
     v = [torch.zeros_like(x) for x in master]
     gens = [torch.Generator().manual_seed(100 + r) for r in range(world)]
     for step in range(1, Z_STEPS + 1):
-        grads = [torch.zeros_like(x) for x in master]
+        sums = [torch.zeros_like(x) for x in master]
         for r in range(world):
             for i, s in enumerate(ZSHAPES):
-                grads[i] += torch.randn(s, generator=gens[r]).to(torch.bfloat16).float()
-        grads = [x / world for x in grads]
-        norm = math.sqrt(sum(float((x.double() ** 2).sum()) for x in grads))
-        c = min(1.0, Z_CLIP / (norm + 1e-6))
+                sums[i] += _exact_grad(s, gens[r]).float()
+        sumsq = sum(float((x.double() ** 2).sum()) for x in sums)
+        coef = _clip_coef(sumsq, world, Z_CLIP)
         for i in range(len(master)):
-            _ref_adamw(master[i], grads[i] * c, m[i], v[i], step, Z_LR)
+            _ref_adamw(master[i], sums[i] * coef, m[i], v[i], step, Z_LR)
     expect = [x.to(torch.bfloat16) for x in master]
     for r in range(world):
         for i, e in enumerate(expect):
-            assert torch.allclose(res[r][i].float(), e.float(), rtol=0, atol=1e-2), (r, i)
-            assert (res[r][i] != e).float().mean() < 0.02, (r, i)  # bf16 ulp flips only
-    for i in range(len(expect)):
-        assert torch.equal(res[0][i], res[1][i])  # every rank holds the same weights
+            assert torch.equal(res[r]["math"][i], e), (world, r, i)
+    # (b) overlap_comm
+    for r in range(world):
+        armed, post, b16 = res[r]["armed"], res[r]["posthoc"], res[r]["bf16"]
+        assert armed["buckets"] > 2
+        assert armed["launched_at_cap"] >= 1, "block buckets reduce-scatter during the backward"
+        assert post["launched_at_cap"] == 0
+        for a, b_, c in zip(armed["params"], post["params"], b16["params"]):
+            assert torch.equal(a, b_)
+            assert torch.allclose(c.float(), a.float(), rtol=0, atol=2e-2)
+        for i, a in enumerate(armed["params"]):
+            assert torch.equal(a, res[0]["armed"]["params"][i])  # every rank holds the same weights
 
 
 def test_sample_timesteps_is_the_lognormal_draw_bitwise():

@@ -163,12 +163,12 @@ def test_gemm_store_rowdot(M, N, K, hd, ext):
 
 
 # ------------------------------------------------------------------------------------- attention
-def _sdpa_ref(q, k, v, B, H, d, bias=None):
+def _sdpa_ref(q, k, v, B, H, d, bias=None, dtype=torch.float32):
     Nq, Nk = q.shape[0] // B, k.shape[0] // B
-    qh = q.float().view(B, Nq, H, d).transpose(1, 2)
-    kh = k.float().view(B, Nk, H, d).transpose(1, 2)
-    vh = v.float().view(B, Nk, H, d).transpose(1, 2)
-    mask = None if bias is None else bias.view(B, 1, 1, Nk)
+    qh = q.to(dtype).view(B, Nq, H, d).transpose(1, 2)
+    kh = k.to(dtype).view(B, Nk, H, d).transpose(1, 2)
+    vh = v.to(dtype).view(B, Nk, H, d).transpose(1, 2)
+    mask = None if bias is None else bias.view(B, 1, 1, Nk).to(dtype)
     o = F.scaled_dot_product_attention(qh, kh, vh, attn_mask=mask)
     return o.transpose(1, 2).reshape(B * Nq, H * d)
 
@@ -194,7 +194,9 @@ def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
         bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
     o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias)
     ref = _sdpa_ref(q, k, v, B, H, d, bias)
-    assert rel(o, ref) < 1e-2
+    # SURVEY 8(c)(4) noise criterion against fp32: within 1.25x torch's own bf16 SDPA error (+1e-3)
+    ref16 = _sdpa_ref(q, k, v, B, H, d, bias, dtype=torch.bfloat16)
+    assert rel(o, ref) <= 1.25 * rel(ref16, ref) + 1e-3, (rel(o, ref), rel(ref16, ref))
     # lse (log2 units) vs logsumexp of the scaled scores
     qh = q.float().view(B, Nq, H, d).transpose(1, 2)
     kh = k.float().view(B, Nk, H, d).transpose(1, 2)
@@ -208,19 +210,21 @@ def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
     qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (q, k, v))
     _sdpa_ref(qf, kf, vf, B, H, d, bias).backward(do.float())
     dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias)
-    assert rel(dq, qf.grad) < 2e-2
-    assert rel(dk, kf.grad) < 2e-2
-    assert rel(dv, vf.grad) < 2e-2
+    qh, kh, vh = (t.clone().requires_grad_(True) for t in (q, k, v))  # torch's bf16 SDPA backward
+    _sdpa_ref(qh, kh, vh, B, H, d, bias, dtype=torch.bfloat16).backward(do)
+    for ours, r32, r16 in ((dq, qf.grad, qh.grad), (dk, kf.grad, kh.grad), (dv, vf.grad, vh.grad)):
+        assert rel(ours, r32) <= 1.25 * rel(r16, r32) + 1e-3, (rel(ours, r32), rel(r16, r32))
     dq32, _, _ = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, dq_f32=True)
-    assert rel(dq32, qf.grad) < 2e-2
+    assert rel(dq32, qf.grad) <= 1.25 * rel(qh.grad, qf.grad) + 1e-3
 
 
 @pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),  # no key bias
                                                       (8, 4, 1792, 256, True, True),    # bench's attn2
                                                       (8, 4, 1792, 128, True, True),    # 128 keys: QS
                                                       (1, 2, 300, 200, True, False),    # ragged both
-                                                      (2, 2, 64, 33, False, False)])    # < 2 waves
-def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
+                                                      (2, 2, 64, 33, False, False),     # < 2 waves
+                                                      (1, 32, 7488, 256, True, False)])  # config X, B=1:
+def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):        # query split
     """Nk <= 256 runs the one-pass backward (attn_bwd1_kernel: S/dP once, dQ from the dS image);
     LTX_ATTN_BWD1=0 forces the split dQ + dK/dV kernels. Both against fp32 autograd: rel-Frobenius
     <= 2e-2, and the one-pass error within 1.25x the split path's (+1e-3)."""
@@ -260,6 +264,16 @@ def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
         for e1, e0 in zip(errs["1", f32], errs["0", f32]):
             assert e1 < 2e-2 and e0 < 2e-2, errs
             assert e1 <= 1.25 * e0 + 1e-3, errs
+    if H * B < 128 and (Nq + 63) // 64 >= 4:  # the one-pass kernel split over the queries
+        monkeypatch.setenv("LTX_ATTN_BWD1", "1")
+        ops._gemm_workspace(q.device)  # its dK / dV partials live in the stream's workspace
+        outs = {}
+        for qsplit in ("1", "0"):
+            monkeypatch.setenv("LTX_ATTN_QSPLIT", qsplit)
+            outs[qsplit] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, kv_shared=shared)
+        assert torch.equal(outs["1"][0], outs["0"][0])  # dQ: per query tile, unaffected
+        for a, b_ in zip(outs["1"][1:], outs["0"][1:]):  # dK / dV: f32 partials summed in order
+            assert rel(a, b_) < 1e-3
     if Nk <= 128:  # the query-split one-pass kernel (QS) against the 8 x 32-key one: dQ bitwise
         monkeypatch.setenv("LTX_ATTN_BWD1", "1")
         outs = {}
@@ -275,7 +289,8 @@ def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
 @pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),
                                                       (8, 4, 1792, 256, True, True),
                                                       (1, 2, 300, 200, True, False),
-                                                      (2, 2, 40, 64, False, False)])
+                                                      (2, 2, 40, 64, False, False),
+                                                      (1, 32, 7488, 256, True, False)])  # 8 WGs per head
 def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
     """Nk <= 256 runs attn_fwd1_kernel (K/V staged once per (batch, head)); its per-slice
     arithmetic is the tiled kernel's, so O and lse are bitwise those of LTX_ATTN_FWD1=0."""

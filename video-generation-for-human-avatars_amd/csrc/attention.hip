@@ -792,7 +792,11 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
   const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
   const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
-  const int ntiles = (p.Nq + QT - 1) / QT;
+  // this workgroup's query tiles [tq0, tq0 + ntiles) (all of them unless the queries are split over
+  // gridDim.z = p.qsplit workgroups); t below is the tile index within the range
+  const int ntot = (p.Nq + QT - 1) / QT;
+  const int tq0 = (int)((int64_t)ntot * blockIdx.z / p.qsplit);
+  const int ntiles = (int)((int64_t)ntot * (blockIdx.z + 1) / p.qsplit) - tq0;
   // tile t -> slot t % 3: wave w moves Q rows 8w..8w+7 and dO rows 8w..8w+7 (one 1-KiB piece each,
   // the chunk swizzle applied on the source address), wave 0 the lse words, wave 1 the delta words.
   // Rows past Nq re-read the last row; their lse is set to +inf after the DMA lands (P = dS = 0).
@@ -800,7 +804,7 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   uint32_t qoff = (uint32_t)(drow * p.ldq + dch * 8) * 2, ooff = (uint32_t)(drow * p.lddo + dch * 8) * 2;
   auto dma = [&](int t) {
     char* base = smem + (t % NSLOT) * SLOT;
-    const int q0 = t * QT;
+    const int q0 = (tq0 + t) * QT;
     if (q0 + QT > p.Nq) {  // the ragged last tile (its DMA is the last one issued)
       const int rr = min(drow, p.Nq - q0 - 1);
       qoff = (uint32_t)(rr * p.ldq + dch * 8) * 2;
@@ -819,7 +823,7 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
     } else {
       __builtin_amdgcn_s_waitcnt(0x0070);
     }
-    if (wave == 0 && t * QT + QT > p.Nq && t * QT + lane >= p.Nq)
+    if (wave == 0 && (tq0 + t) * QT + QT > p.Nq && (tq0 + t) * QT + lane >= p.Nq)
       ((float*)(smem + (t % NSLOT) * SLOT + 2 * TILE))[lane] = INFINITY;
     __builtin_amdgcn_s_waitcnt(0x0070);
     asm volatile("" ::: "memory");
@@ -846,7 +850,7 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
     const float* sl = (const float*)(qtile + 2 * TILE);
     const float* sd = sl + QT;
     const char* sprev = simg0 + ((t + 1) & 1) * SIMG;
-    if (t >= 2) dq_store((t - 2) * QT);
+    if (t >= 2) dq_store((tq0 + t - 2) * QT);
 #pragma unroll
     for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
     if (t + 2 < ntiles) dma(t + 2);  // into tile t-1's slot (last read before the barrier)
@@ -911,11 +915,26 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
     if (t + 1 < ntiles) tile_sync(t + 1, t + 2 < ntiles);
     else __syncthreads();
   }
-  if (ntiles >= 2) dq_store((ntiles - 2) * QT);
+  if (ntiles >= 2) dq_store((tq0 + ntiles - 2) * QT);
 #pragma unroll
   for (int i = 0; i < QBW; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   dq_steps(simg0 + ((ntiles - 1) & 1) * SIMG, 0, KSTEPS);
-  dq_store((ntiles - 1) * QT);
+  dq_store((tq0 + ntiles - 1) * QT);
+  if (p.qsplit > 1) {  // f32 partial rows (dK unscaled): lane h holds dims 32d + 8g + 4h .. +3
+    if (kl < p.Nk) {
+      const int64_t plane = (int64_t)p.qsplit * p.B * p.Nk * p.H * HD;
+      float* pk = p.part + (((int64_t)blockIdx.z * p.B + b) * p.Nk + kl) * (p.H * HD) + hh * HD + 4 * h;
+#pragma unroll
+      for (int d = 0; d < DS; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          *(f32x4*)(pk + d * 32 + 8 * g) = (f32x4){dka[d][4 * g], dka[d][4 * g + 1], dka[d][4 * g + 2], dka[d][4 * g + 3]};
+          *(f32x4*)(pk + plane + d * 32 + 8 * g) =
+              (f32x4){dva[d][4 * g], dva[d][4 * g + 1], dva[d][4 * g + 2], dva[d][4 * g + 3]};
+        }
+    }
+    return;
+  }
   if (qs) {  // waves 4-7's dK / dV partials into waves 0-3 (the dS images are free now)
     static_assert(4 * 2 * DS * 16 * 64 * 4 <= 2 * SIMG, "partials fit the dS images");
     float* xs = (float*)simg0 + (wave & 3) * (2 * DS * 16 * 64) + lane;
@@ -952,6 +971,40 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   const bool kin = kl < p.Nk;
   store_row_swap<HD>(dka, p.scale, kin ? p.dk + ((int64_t)b * p.Nk + kl) * p.lddk + hh * HD : nullptr, lane);
   store_row_swap<HD>(dva, 1.0f, kin ? p.dv + ((int64_t)b * p.Nk + kl) * p.lddv + hh * HD : nullptr, lane);
+}
+
+// sum of the query-split one-pass backward's dK / dV partials in split order (deterministic):
+// dK = bf16(scale * sum), dV = bf16(sum); 8 columns per thread
+template <int HD>
+__global__ __launch_bounds__(256) void attn_bwd1_finish_kernel(const AttnParams p) {
+  const int cols = p.H * HD;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t rows = (int64_t)p.B * p.Nk;
+  if (idx >= rows * (cols / 8)) return;
+  const int64_t row = idx / (cols / 8);
+  const int c = (int)(idx % (cols / 8)) * 8;
+  const int64_t plane = (int64_t)p.qsplit * rows * cols;
+  float k8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, v8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < p.qsplit; ++z) {
+    const float* src = p.part + ((int64_t)z * rows + row) * cols + c;
+    const f32x4 a0 = *(const f32x4*)src, a1 = *(const f32x4*)(src + 4);
+    const f32x4 b0 = *(const f32x4*)(src + plane), b1 = *(const f32x4*)(src + plane + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      k8[i] += a0[i];
+      k8[4 + i] += a1[i];
+      v8[i] += b0[i];
+      v8[4 + i] += b1[i];
+    }
+  }
+  u32x4 wk, wv;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    wk[j] = pack2(k8[2 * j] * p.scale, k8[2 * j + 1] * p.scale);
+    wv[j] = pack2(v8[2 * j], v8[2 * j + 1]);
+  }
+  *(u32x4*)(p.dk + row * p.lddk + c) = wk;
+  *(u32x4*)(p.dv + row * p.lddv + c) = wv;
 }
 
 // delta[b,h,q] = sum_d dO*O (f32), one wave per (b, q) row covering all heads
@@ -1030,6 +1083,13 @@ static int bwd1_qs_flag() {
   return (e && e[0] == '1') ? 1 : 0;
 }
 
+// LTX_ATTN_QSPLIT=0: the one-pass cross backward keeps one workgroup per (batch, head) at any
+// H * B (read per call)
+static int qsplit_flag() {
+  const char* e = std::getenv("LTX_ATTN_QSPLIT");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 template <int HD>
 static int launch_fwd(AttnParams p, hipStream_t s) {
   p.xcd_order = xcd_order_flag();
@@ -1037,8 +1097,11 @@ static int launch_fwd(AttnParams p, hipStream_t s) {
   if constexpr (HD == 64) {
     if (p.Nk <= BWD1_KEYS && fwd1_flag()) {  // every key staged once per (batch, head)
       // two workgroups per (batch, head) when that still leaves >= 8 slices each: 2 per CU
+      // (more when H * B leaves the chip short of 256 workgroups: inference, config X at B = 1)
       const int nsl = (p.Nq + 31) / 32;
-      const dim3 g1((unsigned)p.H, (unsigned)p.B, nsl >= 16 ? 2u : 1u);
+      int z = nsl >= 16 ? 2 : 1;
+      if (z == 2 && p.H * p.B < 128) z = std::max(2, std::min(nsl / 8, (256 + p.H * p.B - 1) / (p.H * p.B)));
+      const dim3 g1((unsigned)p.H, (unsigned)p.B, (unsigned)z);
       if (needs_bias(p))
         hipLaunchKernelGGL((attn_fwd1_kernel<HD, true>), g1, dim3(BWD1_THREADS), 0, s, p);
       else
@@ -1080,6 +1143,30 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   p.skip_masked = skip_flag();
   if constexpr (HD == 64) {  // (head dim 32, the tiny config, keeps the split kernels)
     if (p.Nk <= BWD1_KEYS && bwd1_flag()) {  // every key in one workgroup: one-pass backward
+      // under 128 (batch, head) pairs the queries are split over S workgroups each (f32 dK / dV
+      // partials in the stream's workspace, summed in order by attn_bwd1_finish_kernel)
+      p.qsplit = 1;
+      const int ntot = (p.Nq + 63) / 64;
+      if (p.H * p.B < 128 && ntot >= 4 && qsplit_flag()) {
+        int S = std::min(ntot / 2, (256 + p.H * p.B - 1) / (p.H * p.B));
+        size_t ws = 0;
+        float* part = stream_workspace(s, &ws);
+        while (S > 1 && (size_t)2 * S * p.B * p.Nk * p.H * HD * sizeof(float) > ws) --S;
+        if (S > 1) {
+          p.qsplit = S;
+          p.part = part;
+          const dim3 gs((unsigned)p.H, (unsigned)p.B, (unsigned)S);
+          if (p.key_bias != nullptr || p.Nk != BWD1_KEYS)
+            hipLaunchKernelGGL((attn_bwd1_kernel<HD, true, false>), gs, dim3(BWD1_THREADS), 0, s, p);
+          else
+            hipLaunchKernelGGL((attn_bwd1_kernel<HD, false, false>), gs, dim3(BWD1_THREADS), 0, s, p);
+          LTX_LAUNCH_CHECK();
+          const int64_t n8 = (int64_t)p.B * p.Nk * p.H * HD / 8;
+          hipLaunchKernelGGL((attn_bwd1_finish_kernel<HD>), dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, s, p);
+          LTX_LAUNCH_CHECK();
+          return LTX_OK;
+        }
+      }
       const dim3 g1((unsigned)p.H, (unsigned)p.B);
       if ((p.key_bias != nullptr || p.Nk != BWD1_KEYS) && bwd1_qs_flag())
         hipLaunchKernelGGL((attn_bwd1_kernel<HD, true, true>), g1, dim3(BWD1_THREADS), 0, s, p);
@@ -1153,6 +1240,7 @@ extern "C" int ltx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t l
   p.q = (const bf16_t*)q; p.ldq = ldq; p.k = (const bf16_t*)k; p.ldk = ldk; p.v = (const bf16_t*)v; p.ldv = ldv;
   p.o_out = (bf16_t*)o; p.ldo = ldo; p.lse = lse; p.key_bias = key_bias;
   p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.kvb = (int)kv_batch_rows; p.scale = scale;
+  p.qsplit = 1;
   return d == 64 ? launch_fwd<64>(p, (hipStream_t)stream) : launch_fwd<32>(p, (hipStream_t)stream);
 }
 
@@ -1174,6 +1262,7 @@ extern "C" int ltx_attn_bwd_ex(const void* q, int64_t ldq, const void* k, int64_
   p.dq = dq; p.lddq = lddq; p.dq_f32 = dq_is_f32;
   p.dk = (bf16_t*)dk; p.lddk = lddk; p.dv = (bf16_t*)dv; p.lddv = lddv;
   p.B = (int)B; p.H = (int)H; p.Nq = (int)Nq; p.Nk = (int)Nk; p.kvb = (int)kv_batch_rows; p.scale = scale;
+  p.qsplit = 1;
   return d == 64 ? launch_bwd<64>(p, delta_ws, delta_ready, (hipStream_t)stream)
                  : launch_bwd<32>(p, delta_ws, delta_ready, (hipStream_t)stream);
 }

@@ -158,6 +158,11 @@ struct AttnParams {
   float scale;
   int xcd_order;                       // 1: XCD-aware block order (xcd_block), 0: hardware order
   int skip_masked;                     // 1: skip all-padding key blocks (one-pass kernels), 0: keep
+  // one-pass cross backward split over the queries (attn_bwd1_kernel, qsplit > 1): gridDim.z
+  // workgroups per (batch, head) each take a contiguous range of query tiles and write f32 dK / dV
+  // partials [2][qsplit][B][Nk][H*HD] to `part`, summed in order by attn_bwd1_finish_kernel
+  int qsplit;
+  float* part;
 };
 
 // per-key additive term in log2 units for keys key0..key0+63 -> LDS

@@ -118,6 +118,10 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
 namespace ltx {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
+// the caller-owned f32 scratch of stream s (gemm.hip: ltx_gemm_set_workspace /
+// ltx_gemm_set_stream_workspace); kernels on one stream run in order, so any launcher on that
+// stream may use it between its own launches. bytes = 0 when none was set.
+float* stream_workspace(hipStream_t s, size_t* bytes);
 }  // namespace ltx
 
 #define LTX_CHECK_ARG(cond, msg)                                   \

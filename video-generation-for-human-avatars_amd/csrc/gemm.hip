@@ -584,6 +584,11 @@ static SplitWs ws_for(hipStream_t s) {
   auto it = g_ws_stream.find(s);
   return it != g_ws_stream.end() ? it->second : g_ws_default;
 }
+float* stream_workspace(hipStream_t s, size_t* bytes) {
+  const SplitWs w = ws_for(s);
+  *bytes = w.bytes;
+  return w.ptr;
+}
 // tuning knob (ltx_gemm_set_variant, or LTX_GEMM_VARIANT at load for whole-step A/B runs): 0 default,
 // 13 / 14 large-tile kernel forced to 256 / 224-row tiles. (The not-adopted schedules -- one wave
 // per SIMD, 4-slot ring, three-tile X ring, persistent four-wave kernel -- live in

@@ -165,111 +165,35 @@ class FusedAdamW(torch.optim.Optimizer):
                  float(group["weight_decay"]), int(step), ops._s())
 
 
-class GradAllReduce:
-    """Data-parallel averaging of the trainable gradients (LoRA f32 + caption projection bf16)
-    over torch.distributed (RCCL on ROCm, gloo in the CPU tests), overlapped with the backward.
+class OverlapHooks:
+    """Readiness tracking shared by the reducers that overlap their collectives with the last
+    micro-step's backward (GradAllReduce here, zero.Zero2AdamW): ``self.buckets`` is a list of
+    dicts with a "params" list, ``self._where`` maps id(param) -> (bucket, index), and the subclass
+    implements ``_launch(bi)`` (start bucket bi's collective, set ``self._launched = bi + 1``).
 
-    * The gradients ARE views of per-dtype flat bucket buffers (``zero_grad`` installs them), so
-      the backward's kernels accumulate straight into what gets reduced: no pack, no copy-back.
-      f32 buckets are reduced in place; bf16 buckets (caption projection) through an f32 staging
-      copy (one cast each way), so the sum is f32 and rounds to bf16 once.
-    * Buckets (~bucket_mb of f32 each) follow ``order``: the order the backward completes the
-      grads (``Transformer3DModel.grad_ready_order``: last block first).
-    * ``arm()`` before the LAST micro-step's backward of an accumulation cycle: from then on a
-      bucket's async all-reduce (SUM) is launched as soon as all of its grads are final -- the
-      blocks' LoRA grads via the block hook at the end of each ``_BlockFn.backward``, autograd-
-      accumulated grads via post-accumulate-grad hooks -- while the remaining blocks' backward
-      runs. Buckets always launch in index order on every rank (a ready bucket waits for its
-      predecessors), so the collectives match across ranks.
-    * ``__call__()`` (before the optimizer step) launches whatever has not been launched, waits
-      (a stream wait, no host sync) and divides by the world size. Unarmed, it is the plain
-      post-backward reduction of the same buckets: the two paths are bitwise equal.
-    """
+    ``install(model)`` hooks the model: each block reports, at the end of its backward, the grads
+    its own kernels wrote into .grad (the attn1 / attn2 parameters: LoRA adapters, and in
+    train_mode='full' the attention weights, biases and q/k norm weights); every other trainable
+    parameter -- including a block's scale_shift_table, whose gradient autograd accumulates AFTER
+    the block's backward returns (through _AdaModFn) -- reports through a post-accumulate-grad
+    hook. ``arm()`` before the last backward of an accumulation cycle; from then on a bucket
+    launches as soon as all of its grads are final, always in index order on every rank (a ready
+    bucket waits for its predecessors), so the collectives match across ranks."""
 
-    def __init__(self, params, bucket_mb=25.0, group=None, order=None):
-        params = [p for p in params if p.requires_grad]
-        if order is not None:
-            ids = {id(p) for p in params}
-            ordered = [p for p in order if id(p) in ids]
-            rest = [p for p in reversed(params) if id(p) not in {id(q) for q in ordered}]
-            params = ordered + rest
-        else:
-            params = list(reversed(params))  # registration order reversed
-        self.params = params
-        self.group = group
-        self.buckets = []  # each: {"dtype", "params", "offsets", "n", "flat", "stage"}
-        open_b = {}
-        for p in params:
-            b = open_b.get(p.dtype)
-            if b is None:
-                b = {"dtype": p.dtype, "params": [], "offsets": [], "n": 0, "flat": None,
-                     "stage": None}
-                open_b[p.dtype] = b
-                self.buckets.append(b)
-            b["params"].append(p)
-            b["offsets"].append(b["n"])
-            b["n"] += p.numel()
-            if b["n"] * 4 >= bucket_mb * 1e6:
-                del open_b[p.dtype]
-        self._where = {id(p): (bi, j) for bi, b in enumerate(self.buckets)
-                       for j, p in enumerate(b["params"])}
+    def _init_hooks(self):
         self._armed = False
         self._pending = None   # per bucket: grads not yet final
-        self._launched = 0     # buckets [0, _launched) have their all-reduce in flight
+        self._launched = 0     # buckets [0, _launched) have their collective in flight
         self._works = []
         self._hooks = []
         self._block_cbs = []  # (weakref to block, callback) appended to its _grad_ready_hooks
 
-    # ---- buffers -------------------------------------------------------------------------
     def _world(self):
         if not (dist.is_available() and dist.is_initialized()):
             return 1
         return dist.get_world_size(self.group)
 
-    def _alloc(self, b):
-        if b["flat"] is None:
-            dev = b["params"][0].device
-            b["flat"] = torch.zeros(b["n"], dtype=b["dtype"], device=dev)
-            if b["dtype"] != torch.float32:
-                b["stage"] = torch.empty(b["n"], dtype=torch.float32, device=dev)
-
-    def _view(self, b, j):
-        p, off = b["params"][j], b["offsets"][j]
-        return b["flat"][off:off + p.numel()].view_as(p)
-
-    @torch.no_grad()
-    def zero_grad(self):
-        """Zero every bucket (one fill each) and make each p.grad the view of its slice (in place
-        of optimizer.zero_grad(set_to_none=True), which would detach the grads from the buckets)."""
-        for b in self.buckets:
-            self._alloc(b)
-            b["flat"].zero_()
-            for j, p in enumerate(b["params"]):
-                p.grad = self._view(b, j)
-
-    @torch.no_grad()
-    def _adopt_grads(self, b):
-        """Make the bucket's grads views again if something replaced them (copy them in)."""
-        self._alloc(b)
-        for j, p in enumerate(b["params"]):
-            v = self._view(b, j)
-            g = p.grad
-            if g is not None and g.data_ptr() == v.data_ptr() and g.dtype == v.dtype:
-                continue
-            if g is None:
-                v.zero_()
-            else:
-                v.copy_(g)
-            p.grad = v
-
-    # ---- overlap with the backward -----------------------------------------------------------
     def install(self, model):
-        """Hook the model: each block reports, at the end of its backward, the grads its own
-        kernels wrote into .grad (the attn1 / attn2 parameters: LoRA adapters, and in
-        train_mode='full' the attention weights, biases and q/k norm weights); every other
-        trainable parameter -- including a block's scale_shift_table, whose gradient autograd
-        accumulates AFTER the block's backward returns (through _AdaModFn) -- reports through a
-        post-accumulate-grad hook. ``uninstall()`` removes both kinds of hook."""
         import weakref
         self.uninstall()
         me = weakref.ref(self)
@@ -308,12 +232,14 @@ class GradAllReduce:
                 hooks[:] = [h for h in hooks if h is not cb]
         self._block_cbs = []
 
+    def _prepare_arm(self):
+        """subclass hook: make the grads views of the buckets before an armed backward"""
+
     def arm(self):
         """The next backward is the last of the accumulation cycle: reduce during it."""
         if self._world() == 1:
             return
-        for b in self.buckets:
-            self._adopt_grads(b)
+        self._prepare_arm()
         self._armed = True
         self._pending = [set(id(p) for p in b["params"]) for b in self.buckets]
         self._launched = 0
@@ -327,6 +253,95 @@ class GradAllReduce:
             self._pending[bi].discard(id(p))
         while self._launched < len(self.buckets) and not self._pending[self._launched]:
             self._launch(self._launched)
+
+
+class GradAllReduce(OverlapHooks):
+    """Data-parallel averaging of the trainable gradients (LoRA f32 + caption projection bf16)
+    over torch.distributed (RCCL on ROCm, gloo in the CPU tests), overlapped with the backward.
+
+    * The gradients ARE views of per-dtype flat bucket buffers (``zero_grad`` installs them), so
+      the backward's kernels accumulate straight into what gets reduced: no pack, no copy-back.
+      f32 buckets are reduced in place; bf16 buckets (caption projection) through an f32 staging
+      copy (one cast each way), so the sum is f32 and rounds to bf16 once.
+    * Buckets (~bucket_mb of f32 each) follow ``order``: the order the backward completes the
+      grads (``Transformer3DModel.grad_ready_order``: last block first).
+    * ``arm()`` before the LAST micro-step's backward of an accumulation cycle: a bucket's async
+      all-reduce (SUM) is launched as soon as all of its grads are final (OverlapHooks) while the
+      remaining blocks' backward runs.
+    * ``__call__()`` (before the optimizer step) launches whatever has not been launched, waits
+      (a stream wait, no host sync) and divides by the world size. Unarmed, it is the plain
+      post-backward reduction of the same buckets: the two paths are bitwise equal.
+    """
+
+    def __init__(self, params, bucket_mb=25.0, group=None, order=None):
+        params = [p for p in params if p.requires_grad]
+        if order is not None:
+            ids = {id(p) for p in params}
+            ordered = [p for p in order if id(p) in ids]
+            rest = [p for p in reversed(params) if id(p) not in {id(q) for q in ordered}]
+            params = ordered + rest
+        else:
+            params = list(reversed(params))  # registration order reversed
+        self.params = params
+        self.group = group
+        self.buckets = []  # each: {"dtype", "params", "offsets", "n", "flat", "stage"}
+        open_b = {}
+        for p in params:
+            b = open_b.get(p.dtype)
+            if b is None:
+                b = {"dtype": p.dtype, "params": [], "offsets": [], "n": 0, "flat": None,
+                     "stage": None}
+                open_b[p.dtype] = b
+                self.buckets.append(b)
+            b["params"].append(p)
+            b["offsets"].append(b["n"])
+            b["n"] += p.numel()
+            if b["n"] * 4 >= bucket_mb * 1e6:
+                del open_b[p.dtype]
+        self._where = {id(p): (bi, j) for bi, b in enumerate(self.buckets)
+                       for j, p in enumerate(b["params"])}
+        self._init_hooks()
+
+    # ---- buffers -------------------------------------------------------------------------
+    def _alloc(self, b):
+        if b["flat"] is None:
+            dev = b["params"][0].device
+            b["flat"] = torch.zeros(b["n"], dtype=b["dtype"], device=dev)
+            if b["dtype"] != torch.float32:
+                b["stage"] = torch.empty(b["n"], dtype=torch.float32, device=dev)
+
+    def _view(self, b, j):
+        p, off = b["params"][j], b["offsets"][j]
+        return b["flat"][off:off + p.numel()].view_as(p)
+
+    @torch.no_grad()
+    def zero_grad(self):
+        """Zero every bucket (one fill each) and make each p.grad the view of its slice (in place
+        of optimizer.zero_grad(set_to_none=True), which would detach the grads from the buckets)."""
+        for b in self.buckets:
+            self._alloc(b)
+            b["flat"].zero_()
+            for j, p in enumerate(b["params"]):
+                p.grad = self._view(b, j)
+
+    @torch.no_grad()
+    def _adopt_grads(self, b):
+        """Make the bucket's grads views again if something replaced them (copy them in)."""
+        self._alloc(b)
+        for j, p in enumerate(b["params"]):
+            v = self._view(b, j)
+            g = p.grad
+            if g is not None and g.data_ptr() == v.data_ptr() and g.dtype == v.dtype:
+                continue
+            if g is None:
+                v.zero_()
+            else:
+                v.copy_(g)
+            p.grad = v
+
+    def _prepare_arm(self):
+        for b in self.buckets:
+            self._adopt_grads(b)
 
     @torch.no_grad()
     def _launch(self, bi):
