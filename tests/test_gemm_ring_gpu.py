@@ -101,3 +101,34 @@ def test_gemm_ring_epilogues_bitwise(M, N, K):
         _set(0)
         torch.cuda.synchronize()
         assert torch.equal(s0, s1) and torch.equal(dl0, dl1)
+
+
+@pytest.mark.parametrize("M,N,K,K2", [(14336, 2048, 2048, 64), (14336, 2048, 2048, 128), (7000, 2056, 384, 64)])
+def test_gemm_ring_k_extension_bitwise(M, N, K, K2):
+    """The fused LoRA K-extension (attn2 q / out projections and their dgrads): the ring kernel runs
+    the extension tiles after the main loop, in gemm_nt_kernel_t's order -- bitwise, for the plain
+    store and the accumulate epilogue (<6>)."""
+    g = torch.Generator(device="cuda").manual_seed(K2 + M)
+    a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
+    a2 = torch.randn(M, K2 + 8, device="cuda", generator=g).bfloat16()[:, :K2]  # strided view
+    w2 = torch.randn(N, K2, device="cuda", generator=g).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g).bfloat16()
+    _set(20)
+    ops._GEMM_NAMES.clear()
+    try:
+        assert "gemm_ring_kernel" in ops.gemm_kernel_name(M, N, K, K2, "store")
+    finally:
+        _set(0)
+        ops._GEMM_NAMES.clear()
+    r0, r1 = _both(lambda: ops.gemm(a, w, bias=b, ext=(a2, w2)))
+    assert torch.equal(r0, r1)
+    R = torch.randn(M, N, device="cuda", generator=g).bfloat16()
+    c0, c1 = R.clone(), R.clone()
+    _set(0)
+    ops.gemm(a, w, epilogue="accum", aux0=c0, out=c0, ext=(a2, w2))
+    _set(20)
+    ops.gemm(a, w, epilogue="accum", aux0=c1, out=c1, ext=(a2, w2))
+    _set(0)
+    torch.cuda.synchronize()
+    assert torch.equal(c0, c1)

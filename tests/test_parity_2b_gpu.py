@@ -186,6 +186,55 @@ def test_ltx2b_loss_curve_shared_prompt():
         _loss_crit(f"step {i}", curves["build"][i], curves[torch.bfloat16][i], curves[torch.float32][i])
 
 
+@pytest.mark.timeout(900)
+def test_ltx2b_28_layers_loss_curve_50_steps():
+    """SURVEY 8(c)-5 at depth: K = 50 optimizer steps of the full 28-layer LTX-2B (LoRA r=16 on
+    attn2, trainable caption projection, lr 1e-4) at B = 1, N = 1792 (7x16x16), one prompt of 256
+    tokens (16 valid): train_step + FusedAdamW (training.py:159-166, 199-207, 270-271) against the
+    oracle + torch AdamW in fp32 and in bf16 on the GPU, from the same weights and the same per-step
+    (latents, t, noise); every step's f32 loss within max(1e-3, 1.25 x the oracle's own bf16
+    distance to fp32 + 1e-4) of the fp32 curve. Progress goes to gpurun_out/ (one line a step)."""
+    import os
+    from ltx_amd.training import FusedAdamW
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    cfg = dict(OURS_TRANSFORMER_CONFIG)  # 28 layers
+    assert cfg["num_layers"] == 28
+    params = O.make_params(cfg, 41, lora_rank=16, requires_grad=False)
+    model = build_model(cfg, params, 16, device=DEV)
+    model.train()
+    opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+    refs = {}
+    for dt in (torch.bfloat16, torch.float32):
+        q = {k: v.detach().to(DEV).to(torch.float32 if ("lora_" in k or dt == torch.float32) else dt)
+             .requires_grad_(("lora_" in k) or ("caption_projection" in k)) for k, v in params.items()}
+        refs[dt] = (q, torch.optim.AdamW([v for v in q.values() if v.requires_grad], lr=1e-4, foreach=False))
+    del params
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    log = open(os.path.join(root, "gpurun_out", "loss_curve_28l_progress.txt"), "w")
+    curves = {"build": [], torch.bfloat16: [], torch.float32: []}
+    for step in range(50):
+        d = _inputs(1, 7, 16, 16, 256, 16, seed=5000 + step)
+        curves["build"].append(_build_step(model, d))
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        for dt, (q, ropt) in refs.items():
+            r = O.train_step(q, cfg, d["in.latents"], d["in.ref_image_latents"], d["in.pose_latents"],
+                             d["in.prompt_embeds"], d["in.prompt_attention_mask"], t=d["out.t"],
+                             noise=d["out.noise"].to(dt))
+            r["loss"].backward()
+            ropt.step()
+            ropt.zero_grad(set_to_none=True)
+            curves[dt].append(float(((r["sample"].float() - r["v_target"].float()) ** 2).mean()))
+            del r
+        log.write(f"step {step}: build {curves['build'][-1]:.6f} bf16 {curves[torch.bfloat16][-1]:.6f} "
+                  f"fp32 {curves[torch.float32][-1]:.6f}\n")
+        log.flush()
+    log.close()
+    for i in range(50):
+        _loss_crit(f"28-layer step {i}", curves["build"][i], curves[torch.bfloat16][i], curves[torch.float32][i])
+
+
 def test_text_stack_matches_per_block():
     """The batched text side (_TextStack: all blocks' text K/V as one grouped-extension GEMM, the
     2n adapters' lora_down / lora_wgrad as grouped launches, one encoder-gradient GEMM over

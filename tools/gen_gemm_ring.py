@@ -121,6 +121,58 @@ def body(MF):
     return L
 
 
+def ext_body(MF, H2):
+    """The K extension (the fused LoRA tiles, K2 = 32 * H2 <= 128) after the main loop: its H2
+    half-steps go into ring slots 0 .. H2 - 1 in one burst (the main loop's last barrier already
+    retired every read of the ring), then fragments + MFMAs per half-step in order -- the same
+    accumulation order as gemm_nt_kernel_t, whose extension tiles also come last."""
+    NA = 8 * MF
+    NFR = 8 + MF
+    SLOT = MF * 32 * 64 + 256 * 64
+    WREG = MF * 32 * 64
+    fr = lambda st, k: "%" + str(NA + st * NFR + k)
+    acc = lambda i, jm: "%" + str(i * MF + jm)
+    L = []
+    a = L.append
+
+    def reads(st, slot):
+        out = []
+        so = slot * SLOT if slot < 2 else (slot - 2) * SLOT
+        wb = "%[wr0]" if slot < 2 else "%[wr2]"
+        xb = "%[xr0]" if slot < 2 else "%[xr2]"
+        for i in range(8):
+            out.append(f"ds_read_b128 {fr(st, i)}, {wb} offset:{so + WREG + i * 1024}")
+        for jm in range(MF):
+            out.append(f"ds_read_b128 {fr(st, 8 + jm)}, {xb} offset:{so + jm * 1024}")
+        return out
+
+    a("s_nop 4")
+    a("s_mov_b32 %[keep], m0")
+    for h in range(H2):
+        for p in range(8):
+            srd = "%[xsrd]" if p % 2 == 0 else "%[wsrd]"
+            a(f"s_add_u32 m0, %[d{p}], {h * SLOT}")
+            a("s_nop 0")
+            a(f"buffer_load_dwordx4 %[o{p}], {srd}, %[koff] offen lds")
+        a("s_add_u32 %[koff], %[koff], 64")
+    a("s_waitcnt vmcnt(0)")
+    a("s_barrier")
+    L.extend(reads(0, 0))
+    for h in range(H2):
+        st = h % 2
+        a("s_waitcnt lgkmcnt(0)")
+        rd = reads(1 - st, h + 1) if h + 1 < H2 else []
+        mf = [(i, jm) for i in range(8) for jm in range(MF)]
+        for q, (i, jm) in enumerate(mf):
+            a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
+            if q % 2 == 0 and q // 2 < len(rd):
+                a(rd[q // 2])
+    a("s_mov_b32 m0, %[keep]")
+    a("s_nop 15")
+    a("s_nop 15")
+    return L
+
+
 def emit(MF):
     lines = body(MF)
     s = "\n".join(f'  "{l}\\n\\t"' for l in lines)
@@ -136,6 +188,9 @@ def main():
            "#pragma once", ""]
     for MF in (7, 8):
         txt.append(emit(MF))
+        for H2 in (2, 4):
+            lines = ext_body(MF, H2)
+            txt.append(f"#define LTX_RING_EXT{H2}_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
     open(out, "w").write("\n".join(txt))
     print(out)
 

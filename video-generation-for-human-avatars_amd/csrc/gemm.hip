@@ -603,7 +603,9 @@ static int g_ring = [] {
   const char* e = getenv("LTX_GEMM_RING");
   return (e && e[0] == '1') ? 1 : 0;
 }();
-static bool ring_applies(const GemmParams& p) { return p.K2 == 0 && p.K % 128 == 0 && p.K >= 128; }
+static bool ring_applies(const GemmParams& p) {
+  return (p.K2 == 0 || p.K2 == 64 || p.K2 == 128) && p.K % 128 == 0 && p.K >= 128;
+}
 // LTX_GEMM_DMA_BATCH=0: the large-tile kernel issues each LDS-DMA piece in its own asm block
 // (M0 saved / set / restored per piece) instead of one block per wave's piece set
 static int g_dma_batch = [] {
