@@ -16,11 +16,11 @@ def _set(v):
     _lib.load().ltx_gemm_set_variant(v)
 
 
-def _both(fn):
+def _both(fn, variant=20):
     _set(0)
     a = fn()
     torch.cuda.synchronize()
-    _set(20)
+    _set(variant)
     try:
         b = fn()
         torch.cuda.synchronize()
@@ -29,8 +29,8 @@ def _both(fn):
     return a, b
 
 
-def _name(M, N, K, epi):
-    _set(20)
+def _name(M, N, K, epi, variant=20):
+    _set(variant)
     ops._GEMM_NAMES.clear()  # the name cache does not key on the variant
     try:
         return ops.gemm_kernel_name(M, N, K, 0, epi)
@@ -43,14 +43,15 @@ SHAPES = [(14336, 2048, 2048), (14336, 6144, 2048), (14336, 2048, 8192), (14336,
           (14336, 2048, 128), (14336, 2048, 256), (7000, 6152, 384), (5376, 2048, 2048), (8192, 4096, 640)]
 
 
+@pytest.mark.parametrize("variant", [20, 21], ids=["ring", "ring2"])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_gemm_ring_store_bitwise(M, N, K):
+def test_gemm_ring_store_bitwise(M, N, K, variant):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     b = torch.randn(N, device="cuda", generator=g).bfloat16()
-    assert "gemm_ring_kernel" in _name(M, N, K, "store")
-    r0, r1 = _both(lambda: ops.gemm(a, w, bias=b))
+    assert ("gemm_ring2_kernel" if variant == 21 else "gemm_ring_kernel") in _name(M, N, K, "store", variant)
+    r0, r1 = _both(lambda: ops.gemm(a, w, bias=b), variant)
     assert torch.equal(r0, r1)
     if (M, N, K) == (5376, 2048, 2048):
         ref = (a.float() @ w.float().t() + b.float())
@@ -58,8 +59,9 @@ def test_gemm_ring_store_bitwise(M, N, K):
         assert err <= 0.02 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("variant", [20, 21], ids=["ring", "ring2"])
 @pytest.mark.parametrize("M,N,K", [(14336, 2048, 2048), (14336, 8192, 2048), (7000, 6152, 384)])
-def test_gemm_ring_epilogues_bitwise(M, N, K):
+def test_gemm_ring_epilogues_bitwise(M, N, K, variant):
     g = torch.Generator(device="cuda").manual_seed(7 + M + N + K)
     B = 8 if M % 8 == 0 else 1
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
@@ -71,21 +73,21 @@ def test_gemm_ring_epilogues_bitwise(M, N, K):
     # GELU with the pre-activation store (two separate aux buffers)
     _set(0)
     o0 = ops.gemm(a, w, bias=b, epilogue="gelu", aux0=pre0)
-    _set(20)
+    _set(variant)
     o1 = ops.gemm(a, w, bias=b, epilogue="gelu", aux0=pre1)
     _set(0)
     torch.cuda.synchronize()
     assert torch.equal(o0, o1) and torch.equal(pre0, pre1)
     r0, r1 = _both(lambda: ops.gemm(a, w, bias=b, epilogue="gated_residual", aux0=R, aux1=gate,
-                                    rows_per_batch=M // B))
+                                    rows_per_batch=M // B), variant)
     assert torch.equal(r0, r1)
-    r0, r1 = _both(lambda: ops.gemm(a, w, epilogue="gelu_bwd", aux0=R))
+    r0, r1 = _both(lambda: ops.gemm(a, w, epilogue="gelu_bwd", aux0=R), variant)
     assert torch.equal(r0, r1)
     acc0, acc1 = R.clone(), R.clone()
     d0, d1 = torch.empty_like(R), torch.empty_like(R)
     _set(0)
     ops.gemm(a, w, epilogue="accum", aux0=acc0, out=acc0, aux1=gate, aux2=d0, rows_per_batch=M // B)
-    _set(20)
+    _set(variant)
     ops.gemm(a, w, epilogue="accum", aux0=acc1, out=acc1, aux1=gate, aux2=d1, rows_per_batch=M // B)
     _set(0)
     torch.cuda.synchronize()
@@ -96,7 +98,7 @@ def test_gemm_ring_epilogues_bitwise(M, N, K):
         dl1 = torch.empty_like(dl0)
         _set(0)
         s0 = ops.gemm(a, w, epilogue="store_rowdot", aux0=o, aux1=dl0, rank=64, rows_per_batch=M // B)
-        _set(20)
+        _set(variant)
         s1 = ops.gemm(a, w, epilogue="store_rowdot", aux0=o, aux1=dl1, rank=64, rows_per_batch=M // B)
         _set(0)
         torch.cuda.synchronize()

@@ -173,6 +173,105 @@ def ext_body(MF, H2):
     return L
 
 
+def body2(MF):
+    """Variant 2 of the K loop (gemm_ring2_kernel): LDS stages of whole 64-deep K-tiles in 128-B
+    rows (2 stages, 120 / 128 KiB), so every LDS-DMA instruction moves 8 full 128-B lines (the ring's
+    32-deep slots split every line over two instructions). K-tile t (stage t % 2) is two phases:
+      P0(t): MFMAs on F0 = (t, k-half 0); ds_read (t, k-half 1) -> F1;
+      s_waitcnt vmcnt(0) lgkmcnt(0); s_barrier   -- tile t+1 landed (its DMA ran during P1(t-1)),
+                                                    every wave done reading stage t % 2
+      P1(t): MFMAs on F1; ds_read (t+1, k-half 0) -> F0; LDS-DMA of tile t+2 into stage t % 2,
+             one piece per ~3.6 MFMAs.
+    One barrier per K-tile; the DMA of tile t+2 has P0(t+1) (~900 cycles) behind its last piece.
+    Chunk c of row r at c ^ (r & 7) (gemm_nt_kernel_t's swizzle, conflict-free fragment reads)."""
+    NA = 8 * MF
+    NFR = 8 + MF
+    XT = MF * 32 * 128            # X region of a stage
+    ST = XT + 256 * 128           # stage bytes
+    NP = MF + 8                   # DMA pieces per wave per K-tile (X: MF, W: 8)
+    fr = lambda st, k: "%" + str(NA + st * NFR + k)
+    acc = lambda i, jm: "%" + str(i * MF + jm)
+    L = []
+    a = L.append
+
+    def reads(st, stage, kh):
+        out = []
+        for i in range(8):
+            out.append(f"ds_read_b128 {fr(st, i)}, %[wr{stage}{kh}] offset:{i * 2048}")
+        for jm in range(MF):
+            out.append(f"ds_read_b128 {fr(st, 8 + jm)}, %[xr{stage}{kh}] offset:{jm * 2048}")
+        return out
+
+    def dmas(stage):
+        out = []
+        for i in range(MF):  # X piece i of this wave: rows (w + 4i) * 8 ..
+            out.append((f"s_add_u32 m0, %[mx], {stage * ST + i * 4096}",
+                        f"buffer_load_dwordx4 %[ox{i}], %[xsrd], %[koff] offen lds"))
+        for i in range(8):
+            out.append((f"s_add_u32 m0, %[mw], {stage * ST + i * 4096}",
+                        f"buffer_load_dwordx4 %[ow{i}], %[wsrd], %[koff] offen lds"))
+        # interleave X / W pieces
+        xs, ws = out[:MF], out[MF:]
+        mixed = []
+        for k in range(max(len(xs), len(ws))):
+            if k < len(ws):
+                mixed.append(ws[k])
+            if k < len(xs):
+                mixed.append(xs[k])
+        return mixed
+
+    mf = [(i, jm) for i in range(8) for jm in range(MF)]
+    nm = len(mf)
+
+    def phase(st, rd, dm):
+        after = {q: [] for q in range(nm)}
+        for k, r in enumerate(rd):
+            after[2 * k].append(r)
+        if dm:
+            qs = [1 + (k * (nm - 3)) // len(dm) for k in range(len(dm))]
+            for (m0, ld), q in zip(dm, qs):
+                after[q - 1].append(m0)
+                after[q].append(ld)
+            after[min(qs[-1] + 1, nm - 1)].append("s_add_u32 %[koff], %[koff], 128")
+        for q, (i, jm) in enumerate(mf):
+            a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
+            L.extend(after[q])
+
+    def tile(stage, with_dma, last):
+        a("s_waitcnt lgkmcnt(0)")
+        phase(0, reads(1, stage, 1), [])
+        a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+        a("s_barrier")
+        phase(1, [] if last else reads(0, 1 - stage, 0), dmas(stage) if with_dma else [])
+
+    a("s_nop 4")
+    a("s_mov_b32 %[keep], m0")
+    for stage in range(2):  # tiles 0 and 1
+        for m0, ld in dmas(stage):
+            a(m0)
+            a("s_nop 0")
+            a(ld)
+        a("s_add_u32 %[koff], %[koff], 128")
+    a(f"s_waitcnt vmcnt({NP})")
+    a("s_barrier")
+    L.extend(reads(0, 0, 0))
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc1 L_tail_%=")
+    a("L_loop_%=:")
+    tile(0, True, False)
+    tile(1, True, False)
+    a("s_sub_u32 %[iters], %[iters], 1")
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc0 L_loop_%=")
+    a("L_tail_%=:")
+    tile(0, False, False)
+    tile(1, False, True)
+    a("s_mov_b32 m0, %[keep]")
+    a("s_nop 15")
+    a("s_nop 15")
+    return L
+
+
 def emit(MF):
     lines = body(MF)
     s = "\n".join(f'  "{l}\\n\\t"' for l in lines)
@@ -188,6 +287,8 @@ def main():
            "#pragma once", ""]
     for MF in (7, 8):
         txt.append(emit(MF))
+        lines = body2(MF)
+        txt.append(f"#define LTX_RING2_BODY_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
         for H2 in (2, 4):
             lines = ext_body(MF, H2)
             txt.append(f"#define LTX_RING_EXT{H2}_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
