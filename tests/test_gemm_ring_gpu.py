@@ -43,14 +43,14 @@ SHAPES = [(14336, 2048, 2048), (14336, 6144, 2048), (14336, 2048, 8192), (14336,
           (14336, 2048, 128), (14336, 2048, 256), (7000, 6152, 384), (5376, 2048, 2048), (8192, 4096, 640)]
 
 
-@pytest.mark.parametrize("variant", [20, 21], ids=["ring", "ring2"])
+@pytest.mark.parametrize("variant", [20, 21, 22], ids=["ring", "ring2", "ring3"])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_ring_store_bitwise(M, N, K, variant):
     g = torch.Generator(device="cuda").manual_seed(M + N + K)
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     b = torch.randn(N, device="cuda", generator=g).bfloat16()
-    assert ("gemm_ring2_kernel" if variant == 21 else "gemm_ring_kernel") in _name(M, N, K, "store", variant)
+    assert ("gemm_ring2_kernel" if variant >= 21 else "gemm_ring_kernel") in _name(M, N, K, "store", variant)
     r0, r1 = _both(lambda: ops.gemm(a, w, bias=b), variant)
     assert torch.equal(r0, r1)
     if (M, N, K) == (5376, 2048, 2048):
@@ -59,7 +59,7 @@ def test_gemm_ring_store_bitwise(M, N, K, variant):
         assert err <= 0.02 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("variant", [20, 21], ids=["ring", "ring2"])
+@pytest.mark.parametrize("variant", [20, 21, 22], ids=["ring", "ring2", "ring3"])
 @pytest.mark.parametrize("M,N,K", [(14336, 2048, 2048), (14336, 8192, 2048), (7000, 6152, 384)])
 def test_gemm_ring_epilogues_bitwise(M, N, K, variant):
     g = torch.Generator(device="cuda").manual_seed(7 + M + N + K)
@@ -105,8 +105,10 @@ def test_gemm_ring_epilogues_bitwise(M, N, K, variant):
         assert torch.equal(s0, s1) and torch.equal(dl0, dl1)
 
 
-@pytest.mark.parametrize("M,N,K,K2", [(14336, 2048, 2048, 64), (14336, 2048, 2048, 128), (7000, 2056, 384, 64)])
-def test_gemm_ring_k_extension_bitwise(M, N, K, K2):
+@pytest.mark.parametrize("variant", [20, 22], ids=["ring", "ring3"])
+@pytest.mark.parametrize("M,N,K,K2", [(14336, 2048, 2048, 64), (14336, 2048, 2048, 128), (7000, 2056, 384, 64),
+                                      (14336, 8192, 2048, 64)])
+def test_gemm_ring_k_extension_bitwise(M, N, K, K2, variant):
     """The fused LoRA K-extension (attn2 q / out projections and their dgrads): the ring kernel runs
     the extension tiles after the main loop, in gemm_nt_kernel_t's order -- bitwise, for the plain
     store and the accumulate epilogue (<6>)."""
@@ -116,20 +118,20 @@ def test_gemm_ring_k_extension_bitwise(M, N, K, K2):
     a2 = torch.randn(M, K2 + 8, device="cuda", generator=g).bfloat16()[:, :K2]  # strided view
     w2 = torch.randn(N, K2, device="cuda", generator=g).bfloat16()
     b = torch.randn(N, device="cuda", generator=g).bfloat16()
-    _set(20)
+    _set(variant)
     ops._GEMM_NAMES.clear()
     try:
-        assert "gemm_ring_kernel" in ops.gemm_kernel_name(M, N, K, K2, "store")
+        assert ("gemm_ring2_kernel" if variant >= 21 else "gemm_ring_kernel") in ops.gemm_kernel_name(M, N, K, K2, "store")
     finally:
         _set(0)
         ops._GEMM_NAMES.clear()
-    r0, r1 = _both(lambda: ops.gemm(a, w, bias=b, ext=(a2, w2)))
+    r0, r1 = _both(lambda: ops.gemm(a, w, bias=b, ext=(a2, w2)), variant)
     assert torch.equal(r0, r1)
     R = torch.randn(M, N, device="cuda", generator=g).bfloat16()
     c0, c1 = R.clone(), R.clone()
     _set(0)
     ops.gemm(a, w, epilogue="accum", aux0=c0, out=c0, ext=(a2, w2))
-    _set(20)
+    _set(variant)
     ops.gemm(a, w, epilogue="accum", aux0=c1, out=c1, ext=(a2, w2))
     _set(0)
     torch.cuda.synchronize()

@@ -272,6 +272,160 @@ def body2(MF):
     return L
 
 
+def body3(MF):
+    """Variant 3 (gemm_ring2_kernel's LDS layout and operands, LTX_GEMM_RING=3): the DMA of the
+    tile after next gets ~1.5x the latency slack. Each K-tile t (stage s = t % 2) is three segments:
+      S1 (k-half 0, all MFMAs): ds_read (t, k-half 1) -> F1;
+         s_waitcnt lgkmcnt(0); s_barrier     -- M1: every wave done reading stage s
+      S2 (first half of k-half 1): the W pieces of tile t+2 into stage s (weights: L2 / HBM, first);
+         s_waitcnt vmcnt(8); s_barrier       -- M2: tile t+1 landed (only the 8 W pieces just
+                                                issued may be in flight)
+      S3 (second half of k-half 1): ds_read (t+1, k-half 0) -> F0 beside the X pieces of tile t+2.
+    A piece issued in S2(t) / S3(t) is waited for at M2(t+1): >= S1 + S2 of the next tile
+    (~84 MFMAs, ~1350 cycles) behind it, against ~56 MFMAs in variant 2."""
+    NA = 8 * MF
+    NFR = 8 + MF
+    XT = MF * 32 * 128
+    ST = XT + 256 * 128
+    NP = MF + 8
+    fr = lambda st, k: "%" + str(NA + st * NFR + k)
+    acc = lambda i, jm: "%" + str(i * MF + jm)
+    L = []
+    a = L.append
+
+    def reads(st, stage, kh):
+        out = []
+        for i in range(8):
+            out.append(f"ds_read_b128 {fr(st, i)}, %[wr{stage}{kh}] offset:{i * 2048}")
+        for jm in range(MF):
+            out.append(f"ds_read_b128 {fr(st, 8 + jm)}, %[xr{stage}{kh}] offset:{jm * 2048}")
+        return out
+
+    def wdma(stage):
+        return [(f"s_add_u32 m0, %[mw], {stage * ST + i * 4096}",
+                 f"buffer_load_dwordx4 %[ow{i}], %[wsrd], %[koff] offen lds") for i in range(8)]
+
+    def xdma(stage):
+        return [(f"s_add_u32 m0, %[mx], {stage * ST + i * 4096}",
+                 f"buffer_load_dwordx4 %[ox{i}], %[xsrd], %[koff] offen lds") for i in range(MF)]
+
+    mf = [(i, jm) for i in range(8) for jm in range(MF)]
+    nm = len(mf)
+    half = nm // 2
+
+    def run(st, qs, rd, dm, koff_after=False):
+        """MFMAs qs (indices into mf) on set st; reads rd in even gaps from the first, DMA pieces dm
+        in the odd gaps spread over the segment (M0 one gap ahead)"""
+        n = len(qs)
+        after = {q: [] for q in range(n)}
+        for k, r in enumerate(rd):
+            g = 2 * k if 2 * k < n else n - 1 - (2 * k - n)
+            after[g].append(r)
+        if dm:
+            step = max(2, (n - 2) // len(dm))
+            for k, (m0, ld) in enumerate(dm):
+                q = min(1 + k * step, n - 1)
+                after[q - 1].append(m0)
+                after[q].append(ld)
+        if koff_after:
+            after[n - 1].append("s_add_u32 %[koff], %[koff], 128")
+        for g, q in enumerate(qs):
+            i, jm = mf[q]
+            a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
+            L.extend(after[g])
+
+    def tile(stage, with_dma, last):
+        a("s_waitcnt lgkmcnt(0)")
+        run(0, range(nm), reads(1, stage, 1), [])
+        a("s_waitcnt lgkmcnt(0)")
+        a("s_barrier")
+        run(1, range(half), [], wdma(stage) if with_dma else [])
+        a("s_waitcnt vmcnt(8)" if with_dma else "s_waitcnt vmcnt(0)")
+        a("s_barrier")
+        run(1, range(half, nm), [] if last else reads(0, 1 - stage, 0), xdma(stage) if with_dma else [],
+            koff_after=with_dma)
+
+    a("s_nop 4")
+    a("s_mov_b32 %[keep], m0")
+    for stage in range(2):  # tiles 0 and 1
+        for m0, ld in wdma(stage) + xdma(stage):
+            a(m0)
+            a("s_nop 0")
+            a(ld)
+        a("s_add_u32 %[koff], %[koff], 128")
+    a(f"s_waitcnt vmcnt({NP})")
+    a("s_barrier")
+    L.extend(reads(0, 0, 0))
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc1 L_tail_%=")
+    a("L_loop_%=:")
+    tile(0, True, False)
+    tile(1, True, False)
+    a("s_sub_u32 %[iters], %[iters], 1")
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc0 L_loop_%=")
+    a("L_tail_%=:")
+    tile(0, False, False)
+    tile(1, False, True)
+    a("s_mov_b32 m0, %[keep]")
+    a("s_nop 15")
+    a("s_nop 15")
+    return L
+
+
+def ext_body2(MF, T2):
+    """The K extension (LoRA tiles, K2 = 64 * T2, T2 <= 2) for gemm_ring2_kernel's layout, after its
+    main loop: every read of both stages retired at the loop's last barrier, so the T2 extension
+    tiles go into stages 0 .. T2 - 1 in one burst, then k-half by k-half as the main loop (the
+    accumulation order of gemm_nt_kernel_t, whose extension tiles also come last)."""
+    NA = 8 * MF
+    NFR = 8 + MF
+    XT = MF * 32 * 128
+    ST = XT + 256 * 128
+    fr = lambda st, k: "%" + str(NA + st * NFR + k)
+    acc = lambda i, jm: "%" + str(i * MF + jm)
+    L = []
+    a = L.append
+
+    def reads(st, stage, kh):
+        out = []
+        for i in range(8):
+            out.append(f"ds_read_b128 {fr(st, i)}, %[wr{stage}{kh}] offset:{i * 2048}")
+        for jm in range(MF):
+            out.append(f"ds_read_b128 {fr(st, 8 + jm)}, %[xr{stage}{kh}] offset:{jm * 2048}")
+        return out
+
+    a("s_nop 4")
+    a("s_mov_b32 %[keep], m0")
+    for stage in range(T2):
+        for i in range(8):
+            a(f"s_add_u32 m0, %[mw], {stage * ST + i * 4096}")
+            a("s_nop 0")
+            a(f"buffer_load_dwordx4 %[ow{i}], %[wsrd], %[koff] offen lds")
+        for i in range(MF):
+            a(f"s_add_u32 m0, %[mx], {stage * ST + i * 4096}")
+            a("s_nop 0")
+            a(f"buffer_load_dwordx4 %[ox{i}], %[xsrd], %[koff] offen lds")
+        a("s_add_u32 %[koff], %[koff], 128")
+    a("s_waitcnt vmcnt(0)")
+    a("s_barrier")
+    L.extend(reads(0, 0, 0))
+    halves = [(stage, kh) for stage in range(T2) for kh in range(2)]
+    mf = [(i, jm) for i in range(8) for jm in range(MF)]
+    for h, (stage, kh) in enumerate(halves):
+        st = h % 2
+        a("s_waitcnt lgkmcnt(0)")
+        rd = reads(1 - st, *halves[h + 1]) if h + 1 < len(halves) else []
+        for q, (i, jm) in enumerate(mf):
+            a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
+            if q % 2 == 0 and q // 2 < len(rd):
+                a(rd[q // 2])
+    a("s_mov_b32 m0, %[keep]")
+    a("s_nop 15")
+    a("s_nop 15")
+    return L
+
+
 def emit(MF):
     lines = body(MF)
     s = "\n".join(f'  "{l}\\n\\t"' for l in lines)
@@ -289,6 +443,11 @@ def main():
         txt.append(emit(MF))
         lines = body2(MF)
         txt.append(f"#define LTX_RING2_BODY_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
+        lines = body3(MF)
+        txt.append(f"#define LTX_RING3_BODY_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
+        for T2 in (1, 2):
+            lines = ext_body2(MF, T2)
+            txt.append(f"#define LTX_RING2_EXT{T2}_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
         for H2 in (2, 4):
             lines = ext_body(MF, H2)
             txt.append(f"#define LTX_RING_EXT{H2}_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")

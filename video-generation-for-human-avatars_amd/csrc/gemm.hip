@@ -620,7 +620,7 @@ static int g_epi_batch = [] {
 
 // The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can
 // attribute its per-launch timings to the kernel rocprof will name).
-enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_SMALL = 3, PATH_RING = 4, PATH_RING2 = 5 };
+enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_SMALL = 3, PATH_RING = 4, PATH_RING2 = 5, PATH_RING3 = 6 };
 struct GemmPlan {
   GemmPath path;
   int bmt;     // PATH_T: tile height (256 or 224)
@@ -655,7 +655,7 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
     }
   }
   if (!g_force_small && p.M >= BM2 &&
-      (big_tiles >= 256 || ((g_variant == 0 || g_variant == 20 || g_variant == 21) && tiles224 >= 160))) {
+      (big_tiles >= 256 || ((g_variant == 0 || (g_variant >= 20 && g_variant <= 22)) && tiles224 >= 160))) {
     const int64_t ntn = (p.N + BN2 - 1) / BN2;
     const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
     // fraction of the last round of 256 CUs that has work, per tile height
@@ -663,8 +663,9 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
     // the tile height that fills the last round best; variant 13 forces BMT 256, 14 forces 224
     const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
     const bool ring = (g_ring == 1 || g_variant == 20) && ring_applies(p);
-    const bool ring2 = (g_ring == 2 || g_variant == 21) && p.K2 == 0 && ring_applies(p);
-    return GemmPlan{ring2 ? PATH_RING2 : ring ? PATH_RING : PATH_T, use224 ? 224 : 256, 1, 2};
+    const bool ring2 = (g_ring == 2 || g_variant == 21) && ring_applies(p);
+    const bool ring3 = (g_ring == 3 || g_variant == 22) && ring_applies(p);
+    return GemmPlan{ring3 ? PATH_RING3 : ring2 ? PATH_RING2 : ring ? PATH_RING : PATH_T, use224 ? 224 : 256, 1, 2};
   }
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int tiles = ntm * ntn;
@@ -698,7 +699,9 @@ static void describe_plan(const GemmPlan& pl, int epi, int R, char* buf, size_t 
       snprintf(buf, len, "ltx::gemm_ring_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt / 32);
       break;
     case PATH_RING2:
-      snprintf(buf, len, "ltx::gemm_ring2_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt / 32);
+    case PATH_RING3:
+      snprintf(buf, len, "ltx::gemm_ring2_kernel<%d, %d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt / 32,
+               pl.path == PATH_RING3 ? 3 : 2);
       break;
     default:
       snprintf(buf, len, "ltx::gemm_nt_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.nst);
@@ -732,11 +735,15 @@ static int launch(const GemmParams& p, hipStream_t s) {
     LTX_LAUNCH_CHECK();
     return LTX_OK;
   }
-  if (pl.path == PATH_RING2 && launch_ring2<EPI, R>(p, pl.bmt, s)) {
+  if (pl.path == PATH_RING2 && launch_ring2<EPI, R, 2>(p, pl.bmt, s)) {
     LTX_LAUNCH_CHECK();
     return LTX_OK;
   }
-  if (pl.path == PATH_T || pl.path == PATH_RING || pl.path == PATH_RING2) {
+  if (pl.path == PATH_RING3 && launch_ring2<EPI, R, 3>(p, pl.bmt, s)) {
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+  if (pl.path == PATH_T || pl.path == PATH_RING || pl.path == PATH_RING2 || pl.path == PATH_RING3) {
     static bool t_set = false;
     if (!t_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
@@ -806,8 +813,8 @@ static int launch_lora(const GemmParams& p, hipStream_t s) {
 using namespace ltx;
 
 extern "C" int ltx_gemm_set_variant(int variant) {
-  LTX_CHECK_ARG(variant == 0 || variant == 13 || variant == 14 || variant == 20 || variant == 21,
-                "gemm_set_variant: 0, 13, 14, 20 (ring kernel) or 21 (ring kernel, 64-deep stages)");
+  LTX_CHECK_ARG(variant == 0 || variant == 13 || variant == 14 || (variant >= 20 && variant <= 22),
+                "gemm_set_variant: 0, 13, 14, 20 (ring kernel), 21 / 22 (ring kernel variants 2 / 3)");
   g_variant = variant;
   return LTX_OK;
 }
