@@ -227,8 +227,10 @@ int ltx_gemm_bf16_nt_gext(const void* A, int64_t lda, const void* W, int64_t ldw
                           const void* aux2, int64_t ld2, float alpha, int64_t rank,
                           int64_t rows_per_batch, void* stream);
 
-/* Tuning knob for A/B measurements (process-global): 0 = the dispatcher's own tile-height choice,
- * 13 / 14 = force 256 / 224-row tiles on the large-tile kernel. Any other value is LTX_ERR_BAD_ARG. */
+/* Tuning knob for A/B measurements (process-global): 0 = the dispatcher's own choice (the ring
+ * kernel where it applies), 15 = gemm_nt_kernel_t at the dispatcher's tile height, 13 / 14 =
+ * gemm_nt_kernel_t forced to 256 / 224-row tiles, 20 = the ring kernel (bitwise equal to 15).
+ * Any other value is LTX_ERR_BAD_ARG. */
 int ltx_gemm_set_variant(int variant);
 /* The demangled name (as rocprofv3 prints it) of the main kernel ltx_gemm_bf16_nt_ext would launch
  * for this call on `stream` (the dispatcher's tile / split-K choice); bench.py groups its

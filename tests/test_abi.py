@@ -51,21 +51,32 @@ def test_gemm_describe_names_the_dispatched_kernel():
         assert lib.ltx_gemm_describe(M, N, K, K2, _lib.EPI[epi], rank, None, buf, 256) == 0
         return buf.value.decode()
     M = 8 * 1792
-    # N = 2048 tiles: 64 x 8 = 512 of 224 rows fill two rounds exactly
-    assert name(M, 2048, 8192) == "ltx::gemm_nt_kernel_t<0, 0, 224, 4, 0>(ltx::GemmParams)"
-    assert name(M, 8192, 2048, epi="gelu") == "ltx::gemm_nt_kernel_t<1, 0, 256, 8, 0>(ltx::GemmParams)"
+    # N = 2048 tiles: 64 x 8 = 512 of 224 rows fill two rounds exactly; the ring kernel by default
+    assert name(M, 2048, 8192) == "ltx::gemm_ring_kernel<0, 0, 7, 0>(ltx::GemmParams)"
+    assert name(M, 8192, 2048, epi="gelu") == "ltx::gemm_ring_kernel<1, 0, 8, 0>(ltx::GemmParams)"
+    assert name(M, 2048, 2048, K2=64) == "ltx::gemm_ring_kernel<0, 0, 7, 1>(ltx::GemmParams)"
+    # K % 128 != 0 keeps gemm_nt_kernel_t; variant 15 selects it everywhere
+    assert name(M, 2048, 2112) == "ltx::gemm_nt_kernel_t<0, 0, 224, 4, 0>(ltx::GemmParams)"
+    assert lib.ltx_gemm_set_variant(15) == 0
+    try:
+        assert name(M, 2048, 8192) == "ltx::gemm_nt_kernel_t<0, 0, 224, 4, 0>(ltx::GemmParams)"
+        assert name(M, 8192, 2048, epi="gelu") == "ltx::gemm_nt_kernel_t<1, 0, 256, 8, 0>(ltx::GemmParams)"
+    finally:
+        lib.ltx_gemm_set_variant(0)
     # the text side (M = 256 rows) runs the 128x128 kernel with three LDS stages
     assert name(256, 4096, 2048, K2=128).startswith("ltx::gemm_nt_kernel<0, 0, 3>")
 
 
 def test_gemm_set_variant_rejects_removed_schedules():
-    """Only the tile-height knobs remain (0 / 13 / 14); the not-adopted schedules are no longer
-    in the library (tools/experiments/)."""
+    """Only the kernel / tile-height knobs remain (0 / 13 / 14 / 15 / 20); the not-adopted
+    schedules are no longer in the library (tools/experiments/)."""
     from ltx_amd import _lib
     lib = _lib.load()
     assert lib.ltx_gemm_set_variant(13) == 0
     assert lib.ltx_gemm_set_variant(0) == 0
-    for v in (30, 40, 50, 60):
+    assert lib.ltx_gemm_set_variant(15) == 0
+    assert lib.ltx_gemm_set_variant(20) == 0
+    for v in (21, 22, 30, 40, 50, 60):
         assert lib.ltx_gemm_set_variant(v) != 0
     assert lib.ltx_gemm_set_variant(0) == 0
 
@@ -86,7 +97,7 @@ def test_bench_traffic_lookup_reads_newest_profile():
         "ltx::gemm_nt_kernel_t<0,0,224,4>"
     newest = sorted(glob.glob(os.path.join(repo, "profiles", "r*_traffic.json")))[-1]
     table = json.load(open(newest))["bytes_per_launch"]
-    name, val = max(((k, v) for k, v in table.items() if k.startswith("ltx::gemm_nt_kernel_t")),
+    name, val = max(((k, v) for k, v in table.items() if k.startswith("ltx::gemm_")),
                     key=lambda kv: kv[1])
     got, src = bench.load_traffic(name + "(ltx::GemmParams)")
     assert src == os.path.basename(newest) and got == val

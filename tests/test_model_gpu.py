@@ -242,3 +242,25 @@ def test_gradient_checkpointing_matches_plain_backward():
     assert float(l1) == float(l2)
     for k in g1:
         assert rel(g2[k], g1[k]) < 1e-5, k
+
+
+def test_ffgate_fused_handoff_matches_separate_gate_mul(monkeypatch):
+    """The block backward's last RMSNorm pass hands the previous block its FF-output gradient
+    gate * dh (ltx_rmsnorm_modulate_bwd_gated, LTX_FFGATE_FUSED=1, transformer3d.py _BlockFn) instead
+    of a separate ltx_gate_mul_bf16 launch per block (LTX_FFGATE_FUSED=0): the same bf16(gate * dh)
+    per element, so the loss is equal and every gradient agrees up to the f32-atomic summation
+    order of the LoRA weight gradients."""
+    d, meta = _load("tiny_train_step")
+    cfg = meta["config"]
+    params = {k[2:]: v for k, v in d.items() if k.startswith("w.")}
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("LTX_FFGATE_FUSED", flag)
+        m = build_model(cfg, params, meta["lora_rank"])
+        m.train()
+        runs.append((_build_run(m, d, cfg)[3], grads_by_canonical(m)))
+    (l1, g1), (l0, g0) = runs
+    assert l1 == l0, (l1, l0)
+    assert g1.keys() == g0.keys()
+    for k in g1:
+        assert rel(g1[k], g0[k]) < 1e-5, k

@@ -1,6 +1,9 @@
 """Generates video-generation-for-human-avatars_amd/csrc/gemm_ring_body.h: the hand-scheduled K loop of
-gemm_ring_kernel (gemm_ring.hip) as inline-asm strings, one per m-fragment count MF (7: 224-row
-tiles, 8: 256-row tiles).
+gemm_ring_kernel (gemm_ring.h) as inline-asm strings, one per m-fragment count MF (7: 224-row
+tiles, 8: 256-row tiles). The emitted loop is body3() (+ ext_body2() for the K extension); body()
+below (a 4-slot ring of 32-deep half-tiles, 64-B LDS rows) and body2() (2 x 64-deep stages, one
+mid-tile barrier) are the variants measured before it and kept for reference: the docstrings of
+body2() / body3() describe the adopted layout and schedule, this one the first variant.
 
 Geometry (per workgroup): a BMT x 256 output tile (BMT = 16 * MF * 2), 4 waves at one wave per SIMD,
 wave w owns rows (w >> 1) * 16 * MF .. and columns (w & 1) * 128 .. as MF x 8 fragments of
@@ -374,10 +377,14 @@ def body3(MF):
 
 
 def ext_body2(MF, T2):
-    """The K extension (LoRA tiles, K2 = 64 * T2, T2 <= 2) for gemm_ring2_kernel's layout, after its
-    main loop: every read of both stages retired at the loop's last barrier, so the T2 extension
-    tiles go into stages 0 .. T2 - 1 in one burst, then k-half by k-half as the main loop (the
-    accumulation order of gemm_nt_kernel_t, whose extension tiles also come last)."""
+    """The K extension (LoRA tiles, K2 = 64 * T2, T2 <= 2) for gemm_ring_kernel's layout, appended
+    to body3() in the SAME asm statement (one asm statement per kernel: a second one with the same
+    accumulator operands made hipcc copy and spill the 224 / 256 AGPRs around it). Every read of both
+    stages retired at the main loop's last barrier, so the T2 extension tiles go into stages
+    0 .. T2 - 1 in one burst (operands ex*/ew*/x2srd/w2srd: the extension's own offsets and
+    buffers), then k-half by k-half as the main loop (the accumulation order of gemm_nt_kernel_t,
+    whose extension tiles also come last). A closing barrier keeps the epilogue's C image (which
+    overlays stage 0) from landing while a slower wave still reads the last k-half."""
     NA = 8 * MF
     NFR = 8 + MF
     XT = MF * 32 * 128
@@ -395,17 +402,16 @@ def ext_body2(MF, T2):
             out.append(f"ds_read_b128 {fr(st, 8 + jm)}, %[xr{stage}{kh}] offset:{jm * 2048}")
         return out
 
-    a("s_nop 4")
-    a("s_mov_b32 %[keep], m0")
+    a("s_mov_b32 %[koff], 0")
     for stage in range(T2):
         for i in range(8):
             a(f"s_add_u32 m0, %[mw], {stage * ST + i * 4096}")
             a("s_nop 0")
-            a(f"buffer_load_dwordx4 %[ow{i}], %[wsrd], %[koff] offen lds")
+            a(f"buffer_load_dwordx4 %[ew{i}], %[w2srd], %[koff] offen lds")
         for i in range(MF):
             a(f"s_add_u32 m0, %[mx], {stage * ST + i * 4096}")
             a("s_nop 0")
-            a(f"buffer_load_dwordx4 %[ox{i}], %[xsrd], %[koff] offen lds")
+            a(f"buffer_load_dwordx4 %[ex{i}], %[x2srd], %[koff] offen lds")
         a("s_add_u32 %[koff], %[koff], 128")
     a("s_waitcnt vmcnt(0)")
     a("s_barrier")
@@ -420,16 +426,11 @@ def ext_body2(MF, T2):
             a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
             if q % 2 == 0 and q // 2 < len(rd):
                 a(rd[q // 2])
+    a("s_barrier")
     a("s_mov_b32 m0, %[keep]")
     a("s_nop 15")
     a("s_nop 15")
     return L
-
-
-def emit(MF):
-    lines = body(MF)
-    s = "\n".join(f'  "{l}\\n\\t"' for l in lines)
-    return f"#define LTX_RING_BODY_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n"
 
 
 def main():
@@ -437,20 +438,18 @@ def main():
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
         "video-generation-for-human-avatars_amd", "csrc", "gemm_ring_body.h")
     txt = ["// GENERATED by tools/gen_gemm_ring.py -- do not edit by hand.",
-           "// The hand-scheduled K loop of gemm_ring_kernel (gemm_ring.hip); see the generator's docstring.",
+           "// The hand-scheduled K loop of gemm_ring_kernel (gemm_ring.h): body3() and ext_body2() of the",
+           "// generator (body() / body2() are the measured-and-not-adopted variants, DESIGN.md §7).",
            "#pragma once", ""]
+
+    def define(name, lines):
+        txt.append(f"#define {name} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
     for MF in (7, 8):
-        txt.append(emit(MF))
-        lines = body2(MF)
-        txt.append(f"#define LTX_RING2_BODY_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
-        lines = body3(MF)
-        txt.append(f"#define LTX_RING3_BODY_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
+        define(f"LTX_RING_BODY_MF{MF}", body3(MF))
+        main = body3(MF)
+        assert main[-3:] == ["s_mov_b32 m0, %[keep]", "s_nop 15", "s_nop 15"]
         for T2 in (1, 2):
-            lines = ext_body2(MF, T2)
-            txt.append(f"#define LTX_RING2_EXT{T2}_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
-        for H2 in (2, 4):
-            lines = ext_body(MF, H2)
-            txt.append(f"#define LTX_RING_EXT{H2}_MF{MF} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
+            define(f"LTX_RING_BODY_EXT{T2}_MF{MF}", main[:-3] + ext_body2(MF, T2))
     open(out, "w").write("\n".join(txt))
     print(out)
 

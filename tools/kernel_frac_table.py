@@ -48,7 +48,7 @@ def main(prefix):
     for k in bench["kernels"]:
         name = k["kernel"]
         # the rocprof / counter rows of the first kernel the class names
-        m = re.search(r"(gemm_nt_kernel_t<[^>]*>|attn_\w+_kernel<[^>]*>)", name)
+        m = re.search(r"(gemm_(?:nt_kernel_t|ring_kernel)<[^>]*>|attn_\w+_kernel<[^>]*>)", name)
         key = short(m.group(1)).replace(">", "") if m else short(name)
         key = key.split("<")[0] + "<" + key.split("<")[1] if "<" in key else key
         avg = find(stats, key, 3)

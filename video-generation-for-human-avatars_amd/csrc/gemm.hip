@@ -589,23 +589,27 @@ float* stream_workspace(hipStream_t s, size_t* bytes) {
   *bytes = w.bytes;
   return w.ptr;
 }
-// tuning knob (ltx_gemm_set_variant, or LTX_GEMM_VARIANT at load for whole-step A/B runs): 0 default,
-// 13 / 14 large-tile kernel forced to 256 / 224-row tiles. (The not-adopted schedules -- one wave
-// per SIMD, 4-slot ring, three-tile X ring, persistent four-wave kernel -- live in
-// tools/experiments/ and are not part of the library.)
+// tuning knob (ltx_gemm_set_variant, or LTX_GEMM_VARIANT at load for whole-step A/B runs): 0 default
+// (the ring kernel where it applies, else gemm_nt_kernel_t), 15 gemm_nt_kernel_t at the dispatcher's
+// tile height, 13 / 14 gemm_nt_kernel_t forced to 256 / 224-row tiles, 20 the ring kernel. (The
+// not-adopted schedules -- one wave per SIMD, 4-slot ring, three-tile X ring, persistent four-wave
+// kernel -- live in tools/experiments/ and are not part of the library.)
 static int g_variant = [] {
   const char* e = getenv("LTX_GEMM_VARIANT");
   return e ? atoi(e) : 0;
 }();
-// LTX_GEMM_RING=1 (or variant 20): the large-tile calls that gemm_ring_kernel supports run it
-// (gemm_ring.h: hand-scheduled K loop, 4 waves at one wave per SIMD)
-static int g_ring = [] {  // 1: gemm_ring_kernel, 2: gemm_ring2_kernel
+// LTX_GEMM_RING=0 at load: variant 0 runs gemm_nt_kernel_t everywhere (the round-3 default)
+static int g_ring = [] {
   const char* e = getenv("LTX_GEMM_RING");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 1;
 }();
-static bool ring_applies(const GemmParams& p) {
-  return (p.K2 == 0 || p.K2 == 64 || p.K2 == 128) && p.K % 128 == 0 && p.K >= 128;
+#ifdef LTX_GEMM_STAMPS
+static float* g_stamps = nullptr;  // diagnostic build: 8 x u64 per workgroup of the ring kernel
+extern "C" int ltx_gemm_set_stamps(void* ptr) {
+  g_stamps = (float*)ptr;
+  return 0;
 }
+#endif
 // LTX_GEMM_DMA_BATCH=0: the large-tile kernel issues each LDS-DMA piece in its own asm block
 // (M0 saved / set / restored per piece) instead of one block per wave's piece set
 static int g_dma_batch = [] {
@@ -620,7 +624,7 @@ static int g_epi_batch = [] {
 
 // The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can
 // attribute its per-launch timings to the kernel rocprof will name).
-enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_SMALL = 3, PATH_RING = 4, PATH_RING2 = 5, PATH_RING3 = 6 };
+enum GemmPath { PATH_SPLIT_T = 0, PATH_T = 1, PATH_SMALL = 3, PATH_RING = 4 };
 struct GemmPlan {
   GemmPath path;
   int bmt;     // PATH_T: tile height (256 or 224)
@@ -655,17 +659,15 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
     }
   }
   if (!g_force_small && p.M >= BM2 &&
-      (big_tiles >= 256 || ((g_variant == 0 || (g_variant >= 20 && g_variant <= 22)) && tiles224 >= 160))) {
+      (big_tiles >= 256 || ((g_variant == 0 || g_variant == 15 || g_variant == 20) && tiles224 >= 160))) {
     const int64_t ntn = (p.N + BN2 - 1) / BN2;
     const int64_t t256 = (int64_t)((p.M + 255) / 256) * ntn, t224 = (int64_t)((p.M + 223) / 224) * ntn;
     // fraction of the last round of 256 CUs that has work, per tile height
     auto fill = [](int64_t t) { return (double)t / (double)(((t + 255) / 256) * 256); };
     // the tile height that fills the last round best; variant 13 forces BMT 256, 14 forces 224
     const bool use224 = g_variant == 14 || (g_variant != 13 && fill(t224) > fill(t256) + 0.02);
-    const bool ring = (g_ring == 1 || g_variant == 20) && ring_applies(p);
-    const bool ring2 = (g_ring == 2 || g_variant == 21) && ring_applies(p);
-    const bool ring3 = (g_ring == 3 || g_variant == 22) && ring_applies(p);
-    return GemmPlan{ring3 ? PATH_RING3 : ring2 ? PATH_RING2 : ring ? PATH_RING : PATH_T, use224 ? 224 : 256, 1, 2};
+    const bool ring = ((g_ring == 1 && g_variant == 0) || g_variant == 20) && ring_applies(p);
+    return GemmPlan{ring ? PATH_RING : PATH_T, use224 ? 224 : 256, 1, 2};
   }
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int tiles = ntm * ntn;
@@ -686,7 +688,7 @@ static GemmPlan plan_gemm(const GemmParams& p, int epi, int R, hipStream_t s) {
 
 // rocprof's demangled name of the main kernel plan_gemm picks (the split-K tail kernel, when
 // there is one, is not named)
-static void describe_plan(const GemmPlan& pl, int epi, int R, char* buf, size_t len) {
+static void describe_plan(const GemmPlan& pl, int epi, int R, int t2, char* buf, size_t len) {
   switch (pl.path) {
     case PATH_SPLIT_T:
       snprintf(buf, len, "ltx::gemm_nt_kernel_t<%d, %d, 256, 8, 1>(ltx::GemmParams)", epi, R);
@@ -696,12 +698,7 @@ static void describe_plan(const GemmPlan& pl, int epi, int R, char* buf, size_t 
                pl.bmt == 224 ? 4 : 8);
       break;
     case PATH_RING:
-      snprintf(buf, len, "ltx::gemm_ring_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt / 32);
-      break;
-    case PATH_RING2:
-    case PATH_RING3:
-      snprintf(buf, len, "ltx::gemm_ring2_kernel<%d, %d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt / 32,
-               pl.path == PATH_RING3 ? 3 : 2);
+      snprintf(buf, len, "ltx::gemm_ring_kernel<%d, %d, %d, %d>(ltx::GemmParams)", epi, R, pl.bmt / 32, t2);
       break;
     default:
       snprintf(buf, len, "ltx::gemm_nt_kernel<%d, %d, %d>(ltx::GemmParams)", epi, R, pl.nst);
@@ -731,19 +728,17 @@ static int launch(const GemmParams& p, hipStream_t s) {
     LTX_LAUNCH_CHECK();
     return LTX_OK;
   }
+#ifdef LTX_GEMM_STAMPS
+  GemmParams ps = p;
+  ps.ws = g_stamps;
+  if (pl.path == PATH_RING && launch_ring<EPI, R>(ps, pl.bmt, s)) {
+#else
   if (pl.path == PATH_RING && launch_ring<EPI, R>(p, pl.bmt, s)) {
+#endif
     LTX_LAUNCH_CHECK();
     return LTX_OK;
   }
-  if (pl.path == PATH_RING2 && launch_ring2<EPI, R, 2>(p, pl.bmt, s)) {
-    LTX_LAUNCH_CHECK();
-    return LTX_OK;
-  }
-  if (pl.path == PATH_RING3 && launch_ring2<EPI, R, 3>(p, pl.bmt, s)) {
-    LTX_LAUNCH_CHECK();
-    return LTX_OK;
-  }
-  if (pl.path == PATH_T || pl.path == PATH_RING || pl.path == PATH_RING2 || pl.path == PATH_RING3) {
+  if (pl.path == PATH_T || pl.path == PATH_RING) {
     static bool t_set = false;
     if (!t_set) {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel_t<EPI, R, 256, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS2);
@@ -813,8 +808,8 @@ static int launch_lora(const GemmParams& p, hipStream_t s) {
 using namespace ltx;
 
 extern "C" int ltx_gemm_set_variant(int variant) {
-  LTX_CHECK_ARG(variant == 0 || variant == 13 || variant == 14 || (variant >= 20 && variant <= 22),
-                "gemm_set_variant: 0, 13, 14, 20 (ring kernel), 21 / 22 (ring kernel variants 2 / 3)");
+  LTX_CHECK_ARG(variant == 0 || variant == 13 || variant == 14 || variant == 15 || variant == 20,
+                "gemm_set_variant: 0, 13, 14, 15 or 20");
   g_variant = variant;
   return LTX_OK;
 }
@@ -827,7 +822,7 @@ extern "C" int ltx_gemm_describe(int64_t M, int64_t N, int64_t K, int64_t K2, in
   p.M = (int)M; p.N = (int)N; p.K = (int)K; p.K2 = (int)K2;
   const int R = (epilogue == LTX_EPI_LORA || epilogue == LTX_EPI_LORA_RESIDUAL ||
                  epilogue == LTX_EPI_LORA_DGRAD_ACCUM) ? (int)rank : 0;
-  describe_plan(plan_gemm(p, epilogue, R, (hipStream_t)stream), epilogue, R, buf, (size_t)len);
+  describe_plan(plan_gemm(p, epilogue, R, (hipStream_t)stream), epilogue, R, p.K2 / 64, buf, (size_t)len);
   return LTX_OK;
 }
 
