@@ -65,6 +65,8 @@ for name, n, k, epi in SHAPES:
     span = (max(r[3] for r in s) - t0) / 100.0
     loop = [(r[1] - r[0]) / 100 for r in s]
     epil = [(r[3] - r[1]) / 100 for r in s]
+    clk = [(r[4] - r[2]) / max(1, r[1] - r[0]) * 0.1 for r in s]  # GHz: cycles / (ticks of 10 ns)
+    kt = k // 64
     starts = sorted((r[0] - t0) / 100 for r in s)
     by_xcc = collections.defaultdict(list)
     for r, l in zip(s, loop):
@@ -74,6 +76,9 @@ for name, n, k, epi in SHAPES:
     print(f"   loop   med {st.median(loop):6.1f}  p10 {pct(loop, .1):6.1f}  p90 {pct(loop, .9):6.1f} us  "
           f"(MFMA-bound ideal at 2.0 GHz: {k / 64 * 8 * (bmt // 32) * 16 * 2 / 2.0e3 / 1.0:.1f} us)")
     print(f"   epilog med {st.median(epil):6.1f}  p10 {pct(epil, .1):6.1f}  p90 {pct(epil, .9):6.1f} us")
+    cyc = [(r[4] - r[2]) / kt for r in s]
+    print(f"   loop clock med {st.median(clk):.3f} GHz; cycles per 64-deep K-tile med {st.median(cyc):.0f} "
+          f"(MFMA floor {8 * (bmt // 32) * 2 * 16})")
     nr = min(256, tiles)
     print(f"   starts: first round {starts[0]:.1f}..{starts[nr - 1]:.1f} us, later rounds from "
           f"{starts[nr] if tiles > nr else float('nan'):.1f} us")

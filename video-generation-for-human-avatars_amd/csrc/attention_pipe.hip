@@ -410,18 +410,17 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
 #pragma unroll
       for (int d = 0; d < DS; ++d) acc[d] = mfma32(tr_frag<HD>(kt, u * 32, ss, d, lofs), sbf[ss], acc[d]);
   };
-  // steady-state iteration j, hand-placed: C(j-1) from half uc of buffer bc, B(j) on (sj, dj),
-  // A(j+1) into (sn, dn) from half ua of buffer ba
-  auto iteration = [&](int bc, int uc, f32x16& sj, f32x16& dj, int ba, int ua, f32x16& sn, f32x16& dn) {
-    const char* ck = smem + bc * D_BUF;
+  // steady-state iteration j, hand-placed: C(j-1) from half uc of buffer bc (its transposed K
+  // fragments tk read one iteration ahead), B(j) on (sj, dj), A(j+1) into (sn, dn) from half ua of
+  // buffer ba; the last four slots read the NEXT iteration's tk (half un of buffer bn) into tkn, so
+  // no iteration opens on an exposed LDS latency
+  auto iteration = [&](int bc, int uc, f32x16& sj, f32x16& dj, int ba, int ua, f32x16& sn, f32x16& dn,
+                       s16x8 (&tk)[2][DS], int bn, int un, s16x8 (&tkn)[2][DS]) {
+    (void)bc;
+    (void)uc;
     const char* ak = smem + ba * D_BUF;
     const char* av = ak + D_TILE;
-    s16x8 tk[2][DS];
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-      for (int d = 0; d < DS; ++d) tk[ss][d] = tr_frag<HD>(ck, uc * 32, ss, d, lofs);
-    __builtin_amdgcn_sched_barrier(0);
+    const char* nk = smem + bn * D_BUF;
     s16x8 ka[KS], va[KS];
     u32x4 sw[2];
 #pragma unroll
@@ -434,6 +433,7 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
         const int ks = (m - 4) >> 1;
         if (m & 1) dn = mfma32(va[ks], of[ks], ks == 0 ? ndl : dn);
         else sn = mfma32(ka[ks], qf[ks], ks == 0 ? f32x16{} : sn);
+        if (m >= 8) tkn[(m - 8) >> 1][(m - 8) & 1] = tr_frag<HD>(nk, un * 32, (m - 8) >> 1, (m - 8) & 1, lofs);
       }
       if (m < 8) {
 #pragma unroll
@@ -466,11 +466,16 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
   stage_A(0, 1, s1, d1);                // iteration 0: A(1), B(0)
   stage_B(s0, d0);
   int b0 = 0, b1 = 1, b2 = 2;
+  s16x8 tka[2][DS], tkb[2][DS];         // C's transposed K fragments, current / next
+#pragma unroll
+  for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+    for (int d = 0; d < DS; ++d) tka[ss][d] = tr_frag<HD>(smem, 0, ss, d, lofs);  // C(0): buffer 0, half 0
   for (int t = 0; t + 1 < ntiles; ++t) {
     tile_sync();
     if (t + 2 < ntiles) dma(t + 2, b2);
-    iteration(b0, 0, s1, d1, b1, 0, s0, d0);  // C(2t), B(2t+1), A(2t+2)
-    iteration(b0, 1, s0, d0, b1, 1, s1, d1);  // C(2t+1), B(2t+2), A(2t+3)
+    iteration(b0, 0, s1, d1, b1, 0, s0, d0, tka, b0, 1, tkb);  // C(2t), B(2t+1), A(2t+2)
+    iteration(b0, 1, s0, d0, b1, 1, s1, d1, tkb, b1, 0, tka);  // C(2t+1), B(2t+2), A(2t+3)
     const int bt = b0;
     b0 = b1;
     b1 = b2;

@@ -23,8 +23,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;
   return __builtin_bit_cast(bf16_t, b);
 }
+// two floats -> packed bf16 pair (one v_cvt_pk_bf16_f32; the scalar form made hipcc pair values
+// from different calls and shuffle them back with and / shift / or)
+typedef __bf16 bf16x2_cvt_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_cvt_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pack2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_cvt_t){lo, hi}, bf16x2_cvt_t));
 }
 // value rounded through bf16 and back (mirrors an eager bf16 op boundary)
 __device__ __forceinline__ float rbf(float f) { return bf2f(f2bf(f)); }
