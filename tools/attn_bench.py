@@ -10,6 +10,8 @@ from ltx_amd import ops
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--which", default="self,cross")
+ap.add_argument("--env-ab", default=None, help="NAME: time each kernel with NAME=0 and NAME=1, interleaved")
+ap.add_argument("--rounds", type=int, default=3)
 args = ap.parse_args()
 B, N, L, H, d = 8, 1792, 256, 32, 64
 D = H * d
@@ -43,8 +45,17 @@ for which in args.which.split(","):
     scale = d ** -0.5
     o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias)
     do = torch.randn(B * N, D, device=dev).bfloat16()
-    tf = timeit(lambda: ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias), args.iters)
-    tb = timeit(lambda: ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias), args.iters)
+    fwd = lambda: ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias)
+    bwd = lambda: ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias)
     prod = 2.0 * B * H * N * Nk * d
+    if args.env_ab:
+        for rd in range(args.rounds):
+            for val in ("0", "1"):
+                os.environ[args.env_ab] = val
+                tf, tb = timeit(fwd, args.iters), timeit(bwd, args.iters)
+                print(f"{which} {args.env_ab}={val} round {rd}: fwd {tf * 1e3:.1f} us  bwd {tb * 1e3:.1f} us", flush=True)
+        continue
+    tf = timeit(fwd, args.iters)
+    tb = timeit(bwd, args.iters)
     print(f"{which}: fwd {tf * 1e3:.1f} us ({2 * prod / tf / 1e9:.0f} TF)  bwd {tb * 1e3:.1f} us "
           f"(alg {4 * prod / tb / 1e9:.0f} TF, executed {7 * prod / tb / 1e9:.0f} TF)", flush=True)

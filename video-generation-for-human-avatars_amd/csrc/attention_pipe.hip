@@ -547,6 +547,11 @@ constexpr int F_BUF = 2 * F_TILE;       // K | V
 constexpr int F_QUERIES = 256;          // 8 waves x 32
 }  // namespace
 
+// F32SUM: the row sums are f32 adds of the probabilities (4 independent chains) instead of
+// v_dot2c_f32_bf16 over their bf16 packs: 32 four-cycle adds per tile against 16 dot2c that each
+// cost ~10 cycles beyond their issue slot beside MFMAs (MI355X_MICROARCH.md, filler prices). The
+// sum is then the f32 one (as flash attention's), not the sum of the bf16-rounded weights.
+template <bool F32SUM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) void attn_fwd_pipe_kernel(const AttnParams p) {
   constexpr int HD = PHD, KS = HD / 16, DS = HD / 32;
   __shared__ __attribute__((aligned(16))) char smem[P_NBUF * F_BUF];
@@ -621,9 +626,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
         for (int ks = 0; ks < KS; ++ks) s[u] = mfma32(row_frag<HD>(k2, u * 32, ks, lofs), qf[ks], s[u]);
       }
     };
-    // row sums from the bf16 probabilities the PV product consumes (v_dot2c_f32_bf16 against
-    // (1, 1): two values per instruction instead of one f32 add each), so O is normalised by the
-    // sum of exactly the weights it was accumulated with
+    // row sums: F32SUM = f32 adds of the probabilities; else from the bf16 probabilities the PV
+    // product consumes (v_dot2c_f32_bf16 against (1, 1)), O then normalised by the sum of exactly
+    // the weights it was accumulated with
     auto probs = [&]() {
       const float nm = -m_run;
 #pragma unroll
@@ -632,15 +637,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int u = 0; u < 2; ++u) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[u][r] = fast_exp2(fmaf(s[u][r], c2, nm));
+        if constexpr (F32SUM) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ls[r & 3] += s[u][r];
+        }
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
           pk[u][ss] = acc_frag(s[u], ss);
+          if constexpr (!F32SUM) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            ls[(2 * u + ss) & 3] = __builtin_amdgcn_fdot2_f32_bf16(
-                __builtin_bit_cast(bf16x2_t, (unsigned)(unsigned short)pk[u][ss][2 * j] |
-                                                 ((unsigned)(unsigned short)pk[u][ss][2 * j + 1] << 16)),
-                __builtin_bit_cast(bf16x2_t, 0x3F803F80u), ls[(2 * u + ss) & 3], false);
+            for (int j = 0; j < 4; ++j)
+              ls[(2 * u + ss) & 3] = __builtin_amdgcn_fdot2_f32_bf16(
+                  __builtin_bit_cast(bf16x2_t, (unsigned)(unsigned short)pk[u][ss][2 * j] |
+                                                   ((unsigned)(unsigned short)pk[u][ss][2 * j + 1] << 16)),
+                  __builtin_bit_cast(bf16x2_t, 0x3F803F80u), ls[(2 * u + ss) & 3], false);
+          }
         }
       }
     };
@@ -699,9 +710,17 @@ bool fwd_pipe_enabled() {  // LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8
   return v != 0;
 }
 
+static bool fwd_f32sum() {  // LTX_ATTN_FWD_F32SUM=0: row sums by v_dot2c over the bf16 weights
+  const char* e = std::getenv("LTX_ATTN_FWD_F32SUM");  // read per call: tests compare paths in one process
+  return !(e && e[0] == '0');
+}
+
 int launch_fwd_pipe(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nq + F_QUERIES - 1) / F_QUERIES), (unsigned)p.H, (unsigned)p.B);
-  hipLaunchKernelGGL(attn_fwd_pipe_kernel, g, dim3(512), 0, s, p);
+  if (fwd_f32sum())
+    hipLaunchKernelGGL(attn_fwd_pipe_kernel<true>, g, dim3(512), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_fwd_pipe_kernel<false>, g, dim3(512), 0, s, p);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
