@@ -41,12 +41,14 @@ __device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-template <bool BIAS>
+// NB: LDS tile buffers (as attn_dq_pipe_kernel): 4 = each tile's DMA two tiles ahead, the tile
+// barrier waiting only for the tile it opens
+template <bool BIAS, int NB>
 __global__ __launch_bounds__(256, 2) void attn_dkdv_pipe_kernel(const AttnParams p) {
   constexpr int HD = PHD, KS = HD / 16, DS = HD / 32;
   // ONE shared array: a second __shared__ object beside the DMA target makes hipcc wait for the
   // DMA before unrelated LDS reads
-  __shared__ __attribute__((aligned(16))) char smem[P_NBUF * P_BUF];
+  __shared__ __attribute__((aligned(16))) char smem[NB * P_BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -271,24 +273,41 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_pipe_kernel(const AttnParams
 
   dma(0, 0);
   if (ntiles > 1) dma(1, 1);
+  if (NB == 4 && ntiles > 2) dma(2, 2);
   __builtin_amdgcn_s_waitcnt(0);
   if (ntiles > 1) fix_stats(1, 1);
+  if (NB == 4 && ntiles > 2) fix_stats(2, 2);
   tile_sync(0, 0);
 
   stage_A(0, 0, s0, d0);                // A(0)
   stage_A(0, 1, s1, d1);                // iteration 0: A(1), B(0)
   stage_B(0, 0, s0, d0, pb, sb);
-  int b0 = 0, b1 = 1, b2 = 2;           // buffers of tiles t, t+1, t+2
+  int b0 = 0, b1 = 1;                   // buffers of tiles t, t+1
   for (int t = 0; t + 1 < ntiles; ++t) {
-    // iteration 2t+1: tile t+1 resident, tile t-1's buffer free for tile t+2
-    tile_sync(t + 1, b1);
-    if (t + 2 < ntiles) dma(t + 2, b2);
+    // iteration 2t+1: tile t+1 resident, tile t-1's buffer free for tile t+2 (NB 3) / t+3 (NB 4)
+    if constexpr (NB == 4) {
+      // tile t+1 landed: tile t+2's pieces (4 per wave, + the lse / delta words of waves 0, 1)
+      // may stay in flight; this wave's reads of tile t-1 done
+      if (t + 2 < ntiles) {
+        if (wave < 2) __builtin_amdgcn_s_waitcnt(0x0075);  // vmcnt(5) lgkmcnt(0)
+        else __builtin_amdgcn_s_waitcnt(0x0074);           // vmcnt(4) lgkmcnt(0)
+      } else {
+        __builtin_amdgcn_s_waitcnt(0);
+      }
+      fix_stats(t + 1, b1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the fix-up store
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + 3 < ntiles) dma(t + 3, (t + 3) & 3);  // into tile t-1's buffer
+    } else {
+      tile_sync(t + 1, b1);
+      if (t + 2 < ntiles) dma(t + 2, (t + 2) % 3);
+    }
     iteration(b0, 0, b0, 1, s1, d1, b1, 0, s0, d0);  // C(2t), B(2t+1), A(2t+2)
     iteration(b0, 1, b1, 0, s0, d0, b1, 1, s1, d1);  // C(2t+1), B(2t+2), A(2t+3)
-    const int bt = b0;
     b0 = b1;
-    b1 = b2;
-    b2 = bt;
+    b1 = NB == 4 ? (b1 + 1) & 3 : (b1 + 1) % 3;
   }
   // iteration J-1 (J = 2 ntiles): C(J-2), B(J-1); then C(J-1)
   stage_C(b0, 0, pb, sb);
@@ -323,9 +342,13 @@ constexpr int D_BUF = 2 * D_TILE;               // K | V
 constexpr int D_QUERIES = 128;                  // queries per workgroup (4 waves x 32)
 }  // namespace
 
+// NB: LDS tile buffers. 3: a tile's DMA is issued one tile-pair ahead and the tile barrier waits for
+// every outstanding piece; 4: issued two ahead, the barrier waits only for the tile it opens
+// (vmcnt(4): the next tile's 4 pieces per wave stay in flight)
+template <int NB>
 __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p) {
   constexpr int HD = PHD, KS = HD / 16, DS = HD / 32;
-  __shared__ __attribute__((aligned(16))) char smem[P_NBUF * D_BUF];
+  __shared__ __attribute__((aligned(16))) char smem[NB * D_BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -460,26 +483,35 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
 
   dma(0, 0);
   if (ntiles > 1) dma(1, 1);
+  if (NB == 4 && ntiles > 2) dma(2, 2);
   tile_sync();
   f32x16 s0, d0, s1, d1;
   stage_A(0, 0, s0, d0);                // A(0)
   stage_A(0, 1, s1, d1);                // iteration 0: A(1), B(0)
   stage_B(s0, d0);
-  int b0 = 0, b1 = 1, b2 = 2;
+  int b0 = 0, b1 = 1;
   s16x8 tka[2][DS], tkb[2][DS];         // C's transposed K fragments, current / next
 #pragma unroll
   for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
     for (int d = 0; d < DS; ++d) tka[ss][d] = tr_frag<HD>(smem, 0, ss, d, lofs);  // C(0): buffer 0, half 0
   for (int t = 0; t + 1 < ntiles; ++t) {
-    tile_sync();
-    if (t + 2 < ntiles) dma(t + 2, b2);
+    if constexpr (NB == 4) {
+      // tile t+1 landed (tile t+2's pieces may stay in flight), this wave's reads of tile t-1 done
+      if (t + 2 < ntiles) __builtin_amdgcn_s_waitcnt(0x0074);  // vmcnt(4) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + 3 < ntiles) dma(t + 3, (t + 3) & 3);  // into tile t-1's buffer
+    } else {
+      tile_sync();
+      if (t + 2 < ntiles) dma(t + 2, (t + 2) % 3);
+    }
     iteration(b0, 0, s1, d1, b1, 0, s0, d0, tka, b0, 1, tkb);  // C(2t), B(2t+1), A(2t+2)
     iteration(b0, 1, s0, d0, b1, 1, s1, d1, tkb, b1, 0, tka);  // C(2t+1), B(2t+2), A(2t+3)
-    const int bt = b0;
     b0 = b1;
-    b1 = b2;
-    b2 = bt;
+    b1 = NB == 4 ? (b1 + 1) & 3 : (b1 + 1) % 3;
   }
   stage_C(b0, 0);                       // C(J-2)
   stage_B(s1, d1);                      // B(J-1)
@@ -524,9 +556,17 @@ bool dq_pipe_enabled() {  // LTX_ATTN_DQ_PIPE=0: the plain dQ kernel (A/B switch
   return v != 0;
 }
 
+static int dq_nbuf() {  // LTX_ATTN_DQ_NBUF=3: the 3-buffer ring (read per call: A/B in one process)
+  const char* e = std::getenv("LTX_ATTN_DQ_NBUF");
+  return (e && e[0] == '3') ? 3 : 4;
+}
+
 int launch_dq_pipe(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nq + D_QUERIES - 1) / D_QUERIES), (unsigned)p.H, (unsigned)p.B);
-  hipLaunchKernelGGL(attn_dq_pipe_kernel, g, dim3(256), 0, s, p);
+  if (dq_nbuf() == 4)
+    hipLaunchKernelGGL(attn_dq_pipe_kernel<4>, g, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(attn_dq_pipe_kernel<3>, g, dim3(256), 0, s, p);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
@@ -637,12 +677,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
       for (int u = 0; u < 2; ++u) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[u][r] = fast_exp2(fmaf(s[u][r], c2, nm));
-        if constexpr (F32SUM) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) ls[r & 3] += s[u][r];
-        }
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
+          if constexpr (F32SUM) {  // this k-step's 8 probabilities, then their bf16 pack
+#pragma unroll
+            for (int r = 0; r < 8; ++r) ls[(2 * u + ss) & 3] += s[u][8 * ss + r];
+          }
           pk[u][ss] = acc_frag(s[u], ss);
           if constexpr (!F32SUM) {
 #pragma unroll
@@ -731,12 +771,21 @@ bool dkdv_pipe_enabled() {  // LTX_ATTN_DKDV_PIPE=0: the plain dK/dV kernel (A/B
   return v != 0;
 }
 
+static int dkdv_nbuf() {  // LTX_ATTN_DKDV_NBUF=3: the 3-buffer ring (read per call: A/B in one process)
+  const char* e = std::getenv("LTX_ATTN_DKDV_NBUF");
+  return (e && e[0] == '3') ? 3 : 4;
+}
+
 int launch_dkdv_pipe(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nk + P_KEYS - 1) / P_KEYS), (unsigned)p.H, (unsigned)p.B);
-  if (p.key_bias != nullptr || (p.Nk % 64) != 0)
-    hipLaunchKernelGGL(attn_dkdv_pipe_kernel<true>, g, dim3(256), 0, s, p);
-  else
-    hipLaunchKernelGGL(attn_dkdv_pipe_kernel<false>, g, dim3(256), 0, s, p);
+  const bool bias = p.key_bias != nullptr || (p.Nk % 64) != 0;
+  if (dkdv_nbuf() == 4) {
+    if (bias) hipLaunchKernelGGL((attn_dkdv_pipe_kernel<true, 4>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_dkdv_pipe_kernel<false, 4>), g, dim3(256), 0, s, p);
+  } else {
+    if (bias) hipLaunchKernelGGL((attn_dkdv_pipe_kernel<true, 3>), g, dim3(256), 0, s, p);
+    else hipLaunchKernelGGL((attn_dkdv_pipe_kernel<false, 3>), g, dim3(256), 0, s, p);
+  }
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

@@ -552,14 +552,17 @@ extern "C" int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u
   // ~512 blocks of 128 columns x >= 512 rows (8 waves x 4-quad steps): enough waves to stream
   // y while keeping the f32 atomics (128 * r per block) small
   const int nb = (int)((N + 127) / 128);
-  // ~512 blocks (two per CU): 17.9 us vs 20.0 us with 256 at M = 14336, N = 2048, r = 16
+  // ~512 blocks (two per CU): 17.9 us vs 20.0 us with 256 at M = 14336, N = 2048, r = 16. Splits
+  // of >= 256 rows in multiples of 32 (a wave's row quads stay aligned; the last 128-row step of a
+  // split may be partial): M = 14336 -> 32 splits of 448 rows = exactly 512 blocks (with 512-row
+  // multiples it was 28 x 16 = 448 blocks, 1.75 per CU)
   const int target = 512;
   int splits = (int)((target + nb * groups - 1) / (nb * groups));
-  const int max_splits = (int)((M + 511) / 512);
+  const int max_splits = (int)((M + 255) / 256);
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int rps = (int)((M + splits - 1) / splits);
-  rps = (rps + 127) / 128 * 128;
+  rps = (rps + 31) / 32 * 32;
   splits = (int)((M + rps - 1) / rps);
   const dim3 grid((unsigned)nb, (unsigned)splits, (unsigned)groups);
   switch (r) {

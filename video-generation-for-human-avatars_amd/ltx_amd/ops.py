@@ -331,7 +331,8 @@ def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
     if d == 64 and Nk <= 256 and os.environ.get("LTX_ATTN_FWD1", "1") != "0":
         label = f"attention forward: ltx::attn_fwd1_kernel<{d}, {bias}>"  # K/V staged once
     elif d == 64 and bias == "false" and _env_on("LTX_ATTN_FWD_PIPE"):  # attention_pipe.hip
-        label = "attention forward: ltx::attn_fwd_pipe_kernel"
+        f32sum = "false" if os.environ.get("LTX_ATTN_FWD_F32SUM", "1")[:1] == "0" else "true"
+        label = f"attention forward: ltx::attn_fwd_pipe_kernel<{f32sum}>"
     elif d == 64 and int(os.environ.get("LTX_ATTN_W8", "1")) & 1:  # 8 waves x 32 queries
         label = f"attention forward: ltx::attn_q_kernel<{d}, 0, {bias}, 8>"
     else:
@@ -372,9 +373,12 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
         kern = f"ltx::attn_bwd1_kernel<{d}, {'true' if biased else 'false'}, {qs}>"
     elif d == 64 and _env_on("LTX_ATTN_DKDV_PIPE"):  # the pipelined kernels (attention_pipe.hip)
         kb = "true" if (key_bias is not None or Nk % 64) else "false"
-        dqk = ("ltx::attn_dq_pipe_kernel" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
+        # LDS buffers of the pipelined kernels (attention_pipe.hip dq_nbuf / dkdv_nbuf: 4 unless "3")
+        nq = "3" if os.environ.get("LTX_ATTN_DQ_NBUF", "4")[:1] == "3" else "4"
+        nk = "3" if os.environ.get("LTX_ATTN_DKDV_NBUF", "4")[:1] == "3" else "4"
+        dqk = (f"ltx::attn_dq_pipe_kernel<{nq}>" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
                else f"ltx::attn_q_kernel<{d}, 1, {kb}, 4>")
-        kern = f"ltx::attn_dkdv_pipe_kernel<{kb}> + {dqk}"
+        kern = f"ltx::attn_dkdv_pipe_kernel<{kb}, {nk}> + {dqk}"
     else:
         kern = f"ltx::attn_dkdv_kernel<{d}, {bias}, 4> + ltx::attn_q_kernel<{d}, 1, {bias}, 4>"
     label = ("attention backward: " + ("" if ready else f"ltx::attn_delta_kernel<{d}> + ") + kern)
