@@ -433,6 +433,186 @@ def ext_body2(MF, T2):
     return L
 
 
+def body4(MF):
+    """The K loop with THREE X stages and two W stages (gemm_ring_kernel, round 4): the X pieces of
+    tile t+3 (not t+2) go out in S3(t) into tile t's X stage, so an X piece has ~2 K-tiles to land
+    instead of ~1; W keeps two stages (W pieces of t+2 in S2(t)). LDS: X stages 3 x 32 MF x 128 B,
+    then W stages 2 x 256 x 128 B (MF = 8: exactly 160 KiB). Segments and reads as body3(); X
+    stage t % 3, W stage t % 2, so the loop body is 6 K-tiles (period lcm(2, 3)); the last
+    R = T - 6 G tiles (R in 2, 4, 6, 8 for even T; G = floor((T - 3) / 6) loop passes, %[iters])
+    are one of four tails, chosen at run time, whose DMA and waits stop at tile T - 1.
+    %[koff] = byte offset of tile t+2 during tile t: W(t+2) at koff, X(t+3) at koff + 128.
+    Every accumulator takes its K in the same 32-deep steps in the same order as body3()."""
+    NA = 8 * MF
+    NFR = 8 + MF
+    XT = MF * 32 * 128
+    WT = 256 * 128
+    NP = MF + 8
+    fr = lambda st, k: "%" + str(NA + st * NFR + k)
+    acc = lambda i, jm: "%" + str(i * MF + jm)
+    L = []
+    a = L.append
+
+    def reads(st, xs, ws, kh):
+        out = []
+        for i in range(8):
+            out.append(f"ds_read_b128 {fr(st, i)}, %[wr{ws}{kh}] offset:{i * 2048}")
+        for jm in range(MF):
+            out.append(f"ds_read_b128 {fr(st, 8 + jm)}, %[xr{xs}{kh}] offset:{jm * 2048}")
+        return out
+
+    def wdma(ws, off):
+        return [(f"s_add_u32 m0, %[mw], {ws * WT + i * 4096}",
+                 f"buffer_load_dwordx4 %[ow{i}], %[wsrd], %[koff] offen offset:{off} lds") for i in range(8)]
+
+    def xdma(xs, off):
+        return [(f"s_add_u32 m0, %[mx], {xs * XT + i * 4096}",
+                 f"buffer_load_dwordx4 %[ox{i}], %[xsrd], %[koff] offen offset:{off} lds") for i in range(MF)]
+
+    mf = [(i, jm) for i in range(8) for jm in range(MF)]
+    nm = len(mf)
+    half = nm // 2
+
+    def run(st, qs, rd, dm, koff_after=False):
+        n = len(qs)
+        after = {q: [] for q in range(n)}
+        for k, r in enumerate(rd):
+            g = 2 * k if 2 * k < n else n - 1 - (2 * k - n)
+            after[g].append(r)
+        if dm:
+            step = max(2, (n - 2) // len(dm))
+            for k, (m0, ld) in enumerate(dm):
+                q = min(1 + k * step, n - 1)
+                after[q - 1].append(m0)
+                after[q].append(ld)
+        if koff_after:
+            after[n - 1].append("s_add_u32 %[koff], %[koff], 128")
+        for g, q in enumerate(qs):
+            i, jm = mf[q]
+            a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
+            L.extend(after[g])
+
+    def tile(t, T):
+        """K-tile with global index t of T (t, T may be symbolic-relative: only t % 6 and the
+        distances to T matter); DMA W(t+2) if t+2 < T, X(t+3) if t+3 < T"""
+        xs, ws = t % 3, t % 2
+        w_ok, x_ok, nxt = t + 2 < T, t + 3 < T, t + 1 < T
+        a("s_waitcnt lgkmcnt(0)")
+        run(0, range(nm), reads(1, xs, ws, 1), [])
+        a("s_waitcnt lgkmcnt(0)")
+        a("s_barrier")
+        run(1, range(half), [], wdma(ws, 0) if w_ok else [])
+        # M2: tile t+1 landed; issued after its W pieces: X(t+2) (S3 of t-1) and W(t+2) (S2 of t)
+        newer = (MF + 8) if w_ok else 0
+        a(f"s_waitcnt vmcnt({newer})")
+        a("s_barrier")
+        run(1, range(half, nm), reads(0, (t + 1) % 3, (t + 1) % 2, 0) if nxt else [],
+            xdma(xs, 128) if x_ok else [], koff_after=True)
+
+    a("s_nop 4")
+    a("s_mov_b32 %[keep], m0")
+    # prologue: X0 W0 X1 W1 X2, at fixed offsets from koff = 0; then koff = tile 2's offset
+    for t in range(2):
+        for m0, ld in xdma(t % 3, 128 * t) + wdma(t % 2, 128 * t):
+            a(m0)
+            a("s_nop 0")
+            a(ld)
+    a("s_cmp_eq_u32 %[tail], 2")  # T == 2: no X2
+    a("s_cbranch_scc1 L_p2_%=")
+    for m0, ld in xdma(2, 256):
+        a(m0)
+        a("s_nop 0")
+        a(ld)
+    a(f"s_waitcnt vmcnt({NP + MF})")  # tile 0 landed (X1 W1 X2 may be in flight)
+    a("s_branch L_p3_%=")
+    a("L_p2_%=:")
+    a(f"s_waitcnt vmcnt({NP})")
+    a("L_p3_%=:")
+    a("s_add_u32 %[koff], %[koff], 256")
+    a("s_barrier")
+    L.extend(reads(0, 0, 0, 0))
+    BIG = 1 << 20  # loop tiles: every DMA condition holds
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc1 L_tails_%=")
+    a("L_loop_%=:")
+    for t in range(6):
+        tile(t, BIG)
+    a("s_sub_u32 %[iters], %[iters], 1")
+    a("s_cmp_eq_u32 %[iters], 0")
+    a("s_cbranch_scc0 L_loop_%=")
+    a("L_tails_%=:")
+    # tails: R remaining tiles, starting at a multiple of 6 (stages 0 / 0)
+    a("s_cmp_eq_u32 %[tail], 2")
+    a("s_cbranch_scc1 L_t2_%=")
+    a("s_cmp_eq_u32 %[tail], 4")
+    a("s_cbranch_scc1 L_t4_%=")
+    a("s_cmp_eq_u32 %[tail], 6")
+    a("s_cbranch_scc1 L_t6_%=")
+    for R in (8, 6, 4, 2):
+        if R != 8:
+            a(f"L_t{R}_%=:")
+        for t in range(R):
+            tile(t, R)
+        if R != 2:
+            a("s_branch L_end_%=")
+    a("L_end_%=:")
+    a("s_mov_b32 m0, %[keep]")
+    a("s_nop 15")
+    a("s_nop 15")
+    return L
+
+
+def ext_body4(MF, T2):
+    """The K extension (K2 = 64 T2) for body4()'s LDS layout: ext tile i into X stage i and W
+    stage i (all reads of the main loop retired at its last barrier), then k-half by k-half; the
+    closing barrier keeps the epilogue's C image off a slower wave's last reads (ext_body2())."""
+    NA = 8 * MF
+    NFR = 8 + MF
+    XT = MF * 32 * 128
+    WT = 256 * 128
+    fr = lambda st, k: "%" + str(NA + st * NFR + k)
+    acc = lambda i, jm: "%" + str(i * MF + jm)
+    L = []
+    a = L.append
+
+    def reads(st, stage, kh):
+        out = []
+        for i in range(8):
+            out.append(f"ds_read_b128 {fr(st, i)}, %[wr{stage}{kh}] offset:{i * 2048}")
+        for jm in range(MF):
+            out.append(f"ds_read_b128 {fr(st, 8 + jm)}, %[xr{stage}{kh}] offset:{jm * 2048}")
+        return out
+
+    a("s_mov_b32 %[koff], 0")
+    for stage in range(T2):
+        for i in range(8):
+            a(f"s_add_u32 m0, %[mw], {stage * WT + i * 4096}")
+            a("s_nop 0")
+            a(f"buffer_load_dwordx4 %[ew{i}], %[w2srd], %[koff] offen offset:{128 * stage} lds")
+        for i in range(MF):
+            a(f"s_add_u32 m0, %[mx], {stage * XT + i * 4096}")
+            a("s_nop 0")
+            a(f"buffer_load_dwordx4 %[ex{i}], %[x2srd], %[koff] offen offset:{128 * stage} lds")
+    a("s_waitcnt vmcnt(0)")
+    a("s_barrier")
+    L.extend(reads(0, 0, 0))
+    halves = [(stage, kh) for stage in range(T2) for kh in range(2)]
+    mf = [(i, jm) for i in range(8) for jm in range(MF)]
+    for h, (stage, kh) in enumerate(halves):
+        st = h % 2
+        a("s_waitcnt lgkmcnt(0)")
+        rd = reads(1 - st, *halves[h + 1]) if h + 1 < len(halves) else []
+        for q, (i, jm) in enumerate(mf):
+            a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
+            if q % 2 == 0 and q // 2 < len(rd):
+                a(rd[q // 2])
+    a("s_barrier")
+    a("s_mov_b32 m0, %[keep]")
+    a("s_nop 15")
+    a("s_nop 15")
+    return L
+
+
 def main():
     out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -450,6 +630,11 @@ def main():
         assert main[-3:] == ["s_mov_b32 m0, %[keep]", "s_nop 15", "s_nop 15"]
         for T2 in (1, 2):
             define(f"LTX_RING_BODY_EXT{T2}_MF{MF}", main[:-3] + ext_body2(MF, T2))
+        main4 = body4(MF)
+        define(f"LTX_RING4_BODY_MF{MF}", main4)
+        assert main4[-3:] == ["s_mov_b32 m0, %[keep]", "s_nop 15", "s_nop 15"]
+        for T2 in (1, 2):
+            define(f"LTX_RING4_BODY_EXT{T2}_MF{MF}", main4[:-3] + ext_body4(MF, T2))
     open(out, "w").write("\n".join(txt))
     print(out)
 
