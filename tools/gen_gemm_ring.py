@@ -441,7 +441,8 @@ def body4(MF):
     stage t % 3, W stage t % 2, so the loop body is 6 K-tiles (period lcm(2, 3)); the last
     R = T - 6 G tiles (R in 2, 4, 6, 8 for even T; G = floor((T - 3) / 6) loop passes, %[iters])
     are one of four tails, chosen at run time, whose DMA and waits stop at tile T - 1.
-    %[koff] = byte offset of tile t+2 during tile t: W(t+2) at koff, X(t+3) at koff + 128.
+    %[koff] = byte offset of tile t+2 during tile t (W(t+2)), %[koffx] = koff + 128 (X(t+3)): two
+    SGPRs, since an LDS-DMA instruction's immediate offset moves its LDS destination too.
     Every accumulator takes its K in the same 32-deep steps in the same order as body3()."""
     NA = 8 * MF
     NFR = 8 + MF
@@ -461,13 +462,13 @@ def body4(MF):
             out.append(f"ds_read_b128 {fr(st, 8 + jm)}, %[xr{xs}{kh}] offset:{jm * 2048}")
         return out
 
-    def wdma(ws, off):
+    def wdma(ws, ko="koff"):
         return [(f"s_add_u32 m0, %[mw], {ws * WT + i * 4096}",
-                 f"buffer_load_dwordx4 %[ow{i}], %[wsrd], %[koff] offen offset:{off} lds") for i in range(8)]
+                 f"buffer_load_dwordx4 %[ow{i}], %[wsrd], %[{ko}] offen lds") for i in range(8)]
 
-    def xdma(xs, off):
+    def xdma(xs, ko="koffx"):
         return [(f"s_add_u32 m0, %[mx], {xs * XT + i * 4096}",
-                 f"buffer_load_dwordx4 %[ox{i}], %[xsrd], %[koff] offen offset:{off} lds") for i in range(MF)]
+                 f"buffer_load_dwordx4 %[ox{i}], %[xsrd], %[{ko}] offen lds") for i in range(MF)]
 
     mf = [(i, jm) for i in range(8) for jm in range(MF)]
     nm = len(mf)
@@ -487,6 +488,7 @@ def body4(MF):
                 after[q].append(ld)
         if koff_after:
             after[n - 1].append("s_add_u32 %[koff], %[koff], 128")
+            after[n - 1].append("s_add_u32 %[koffx], %[koffx], 128")
         for g, q in enumerate(qs):
             i, jm = mf[q]
             a(f"v_mfma_f32_16x16x32_bf16 {acc(i, jm)}, {fr(st, i)}, {fr(st, 8 + jm)}, {acc(i, jm)}")
@@ -501,25 +503,27 @@ def body4(MF):
         run(0, range(nm), reads(1, xs, ws, 1), [])
         a("s_waitcnt lgkmcnt(0)")
         a("s_barrier")
-        run(1, range(half), [], wdma(ws, 0) if w_ok else [])
+        run(1, range(half), [], wdma(ws) if w_ok else [])
         # M2: tile t+1 landed; issued after its W pieces: X(t+2) (S3 of t-1) and W(t+2) (S2 of t)
         newer = (MF + 8) if w_ok else 0
         a(f"s_waitcnt vmcnt({newer})")
         a("s_barrier")
         run(1, range(half, nm), reads(0, (t + 1) % 3, (t + 1) % 2, 0) if nxt else [],
-            xdma(xs, 128) if x_ok else [], koff_after=True)
+            xdma(xs) if x_ok else [], koff_after=True)
 
     a("s_nop 4")
     a("s_mov_b32 %[keep], m0")
-    # prologue: X0 W0 X1 W1 X2, at fixed offsets from koff = 0; then koff = tile 2's offset
+    # prologue: X0 W0 X1 W1 X2 (koff stepping from 0); then koff = tile 2's offset
     for t in range(2):
-        for m0, ld in xdma(t % 3, 128 * t) + wdma(t % 2, 128 * t):
+        for m0, ld in xdma(t % 3, "koff") + wdma(t % 2):
             a(m0)
             a("s_nop 0")
             a(ld)
+        a("s_add_u32 %[koff], %[koff], 128")
+    a("s_add_u32 %[koffx], %[koff], 128")
     a("s_cmp_eq_u32 %[tail], 2")  # T == 2: no X2
     a("s_cbranch_scc1 L_p2_%=")
-    for m0, ld in xdma(2, 256):
+    for m0, ld in xdma(2, "koff"):
         a(m0)
         a("s_nop 0")
         a(ld)
@@ -528,7 +532,6 @@ def body4(MF):
     a("L_p2_%=:")
     a(f"s_waitcnt vmcnt({NP})")
     a("L_p3_%=:")
-    a("s_add_u32 %[koff], %[koff], 256")
     a("s_barrier")
     L.extend(reads(0, 0, 0, 0))
     BIG = 1 << 20  # loop tiles: every DMA condition holds
@@ -588,11 +591,12 @@ def ext_body4(MF, T2):
         for i in range(8):
             a(f"s_add_u32 m0, %[mw], {stage * WT + i * 4096}")
             a("s_nop 0")
-            a(f"buffer_load_dwordx4 %[ew{i}], %[w2srd], %[koff] offen offset:{128 * stage} lds")
+            a(f"buffer_load_dwordx4 %[ew{i}], %[w2srd], %[koff] offen lds")
         for i in range(MF):
             a(f"s_add_u32 m0, %[mx], {stage * XT + i * 4096}")
             a("s_nop 0")
-            a(f"buffer_load_dwordx4 %[ex{i}], %[x2srd], %[koff] offen offset:{128 * stage} lds")
+            a(f"buffer_load_dwordx4 %[ex{i}], %[x2srd], %[koff] offen lds")
+        a("s_add_u32 %[koff], %[koff], 128")
     a("s_waitcnt vmcnt(0)")
     a("s_barrier")
     L.extend(reads(0, 0, 0))
