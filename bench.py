@@ -105,6 +105,32 @@ def synthetic_batch(device, rank):
     return batch, prompt, mask
 
 
+def selfcheck(device):
+    """After the timed region: the step's two dominant kernel families on a config-A shape against
+    torch fp32 (rel-Frobenius), so a bench line from a broken build cannot pass as a fast one (a
+    kernel writing garbage makes the chip clock up: zero-ish operands cost less energy). The QKV
+    GEMM (14336 x 6144 x 2048, the ring kernel) and the self-attention forward (B 1, 32 x 64 heads,
+    N 1792, the pipelined kernel) on seeded random inputs."""
+    from ltx_amd import ops
+    g = torch.Generator(device="cpu").manual_seed(7)
+    a = torch.randn(14336, 2048, generator=g).to(device, torch.bfloat16)
+    w = (torch.randn(6144, 2048, generator=g) / 2048 ** 0.5).to(device, torch.bfloat16)
+    ref = a.float() @ w.float().t()
+    gemm_err = float((ops.gemm(a, w).float() - ref).norm() / ref.norm())
+    del a, w, ref
+    q, k, v = (torch.randn(1792, 2048, generator=g).to(device, torch.bfloat16) for _ in range(3))
+    o, _ = ops.attn_fwd(q, k, v, 1, 32, 64, 64 ** -0.5)
+    qh, kh, vh = (t.float().view(1, 1792, 32, 64).transpose(1, 2) for t in (q, k, v))
+    ref = torch.nn.functional.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(1792, 2048)
+    attn_err = float((o.float() - ref).norm() / ref.norm())
+    ok = gemm_err < 1e-2 and attn_err < 2e-2
+    if not ok:
+        print(f"bench selfcheck FAILED: gemm rel err {gemm_err:.3e}, attention rel err {attn_err:.3e}",
+              file=sys.stderr, flush=True)
+    return {"ok": ok, "gemm_rel_err": round(gemm_err, 6), "attn_fwd_rel_err": round(attn_err, 6),
+            "what": "ring GEMM 14336x6144x2048 and self-attention forward (1x32x1792x64) vs torch fp32"}
+
+
 def cpu_baseline(budget_layers=28, warmup=2, timed=5):
     """The oracle restatement (oracle/ltx_oracle.py) on the host cores, as BASELINE.md 4 plans it:
     config A at B=1, N = 1792, all 28 blocks, `warmup` untimed + `timed` timed fwd+bwd steps, the
@@ -490,6 +516,7 @@ def main():
                      "ms_per_step": round(k["ms"], 3), "tflops": round(k["tflops"], 1),
                      "frac": round(k["tflops"] / MFMA_BF16_PEAK_TFLOPS, 4)} for k in kernels[:10]],
     }
+    line["selfcheck"] = selfcheck(device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "a" and not full:
         try:
             line["cpu_baseline"] = cpu_baseline()
