@@ -471,6 +471,30 @@ def test_qk_norm_rope_fwd_bwd(D, grid_float):
     assert rel(dq2, qi2.grad) < 1e-2
 
 
+@pytest.mark.parametrize("B,F_,H_,W_", [(4, 2, 4, 8), (8, 7, 4, 4)])
+def test_qk_norm_rope_shared_table_item_order(B, F_, H_, W_):
+    """One batch-shared RoPE table (cs_batch_rows = 0) against B copies of it, at config-A-like
+    batch counts and grids of a multiple of 8 blocks: bitwise the same outputs."""
+    from ltx_amd import ops
+    D, N = 2048, F_ * H_ * W_
+    coords = O.latent_coords(F_, H_, W_, 1, DEV)
+    per_batch = ops.RopeSpec(coords.expand(B, -1, -1).contiguous(), D, 10000.0, [20, 2048, 2048])
+    shared = ops.RopeSpec(coords.expand(B, -1, -1), D, 10000.0, [20, 2048, 2048])
+    assert per_batch.cs_batch_rows == N and shared.cs_batch_rows == 0
+    assert (B * N * 2 // 4) % 8 == 0
+    qkv = g(B * N, 3 * D, seed=11)
+    qw, kw = g(D, seed=12, scale=0.1) + 1, g(D, seed=13, scale=0.1) + 1
+    a = ops.qk_norm_rope_fwd(qkv[:, :D], qkv[:, D:2 * D], qw, kw, per_batch)
+    b = ops.qk_norm_rope_fwd(qkv[:, :D], qkv[:, D:2 * D], qw, kw, shared)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    dq, dk = g(B * N, D, seed=14), g(B * N, D, seed=15)
+    ga = ops.qk_norm_rope_bwd(dq, qkv[:, :D], qw, a[2], dk, qkv[:, D:2 * D], kw, a[3], per_batch)
+    gb = ops.qk_norm_rope_bwd(dq, qkv[:, :D], qw, a[2], dk, qkv[:, D:2 * D], kw, a[3], shared)
+    for x, y in zip(ga, gb):
+        assert torch.equal(x, y)
+
+
 # ------------------------------------------------------------------------- patchify / rf / misc
 def test_patchify_coords_bit_exact():
     from ltx_amd import ops
