@@ -172,6 +172,16 @@ int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const
                          void* dq_out, int64_t ldq_out, void* dk_out, int64_t ldk_out,
                          const uint32_t* rope_cs, int64_t cs_batch_rows, int64_t B, int64_t N,
                          int64_t D, int rope, void* stream);
+/* ltx_qk_norm_rope_fwd / _bwd without RoPE, q only, for `groups` independent row blocks in one
+ * launch: the attn2 k_norm (attention.py:434-436, RMSNorm eps 1e-5 with its own weight per block)
+ * of the text keys of every transformer block. Group g: rows x + g*x_gs + m*ldx (m < rows), weight
+ * + g*w_gs, rstd + g*r_gs; outputs likewise. Bitwise the per-group ungrouped calls. */
+int ltx_qk_norm_fwd_grouped(const void* x, int64_t ldx, int64_t x_gs, void* y, int64_t ldy, int64_t y_gs,
+                            const void* weight, int64_t w_gs, float* rstd, int64_t r_gs, int64_t rows,
+                            int64_t groups, int64_t D, float eps, void* stream);
+int ltx_qk_norm_bwd_grouped(const void* dy, int64_t lddy, int64_t dy_gs, const void* x, int64_t ldx, int64_t x_gs,
+                            const void* weight, int64_t w_gs, const float* rstd, int64_t r_gs, void* dx,
+                            int64_t lddx, int64_t dx_gs, int64_t rows, int64_t groups, int64_t D, void* stream);
 
 /* ---- K10/K14: flash attention (F.scaled_dot_product_attention, attention.py:1057-1064) ------- */
 /* Q [B,Nq,H,d] (row stride ldq per token, head h at column h*d), K/V [B,Nk,H,d], O likewise;

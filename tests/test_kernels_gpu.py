@@ -495,6 +495,26 @@ def test_qk_norm_rope_shared_table_item_order(B, F_, H_, W_):
         assert torch.equal(x, y)
 
 
+def test_qk_norm_grouped_matches_per_group():
+    """ltx_qk_norm_{fwd,bwd}_grouped (every block's text k_norm in one launch) against one
+    qk_norm_rope_{fwd,bwd} call per group: bitwise, at LTX-2B widths with strided group views."""
+    from ltx_amd import ops
+    G, L, D = 5, 256, 2048
+    kv = g(L, 2 * G * D, seed=21)                          # [k_0 | v_0 | k_1 | v_1 | ...]
+    w = torch.stack([g(D, seed=30 + i, scale=0.1) + 1 for i in range(G)]).contiguous()
+    y, rstd = ops.qk_norm_fwd_grouped(kv, 2 * D, w)
+    dy = g(G, L, D, seed=22)
+    dx = torch.zeros(L, 2 * G * D, dtype=torch.bfloat16, device=DEV)
+    ops.qk_norm_bwd_grouped(dy, kv, 2 * D, w, rstd, dx, 2 * D)
+    for i in range(G):
+        xi = kv[:, 2 * i * D:(2 * i + 1) * D]
+        yi, _, ri, _ = ops.qk_norm_rope_fwd(xi, None, w[i], None, None, B=1, N=L)
+        assert torch.equal(y[i], yi) and torch.equal(rstd[i], ri)
+        dxi, _ = ops.qk_norm_rope_bwd(dy[i], xi, w[i], ri, B=1, N=L)
+        assert torch.equal(dx[:, 2 * i * D:(2 * i + 1) * D], dxi)
+        assert float(dx[:, (2 * i + 1) * D:(2 * i + 2) * D].abs().max()) == 0.0  # v columns untouched
+
+
 # ------------------------------------------------------------------------- patchify / rf / misc
 def test_patchify_coords_bit_exact():
     from ltx_amd import ops

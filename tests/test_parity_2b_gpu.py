@@ -278,6 +278,34 @@ def test_text_stack_matches_per_block():
         assert e <= 1e-2, f"{name}: batched vs per-block {e:.3e}"
 
 
+def test_text_stack_grouped_knorm():
+    """The batched text side's attn2 k_norm as ONE grouped launch for every block, forward and
+    backward (LTX_TEXT_KNORM_GROUPED, ltx_qk_norm_{fwd,bwd}_grouped), against one launch per block:
+    the same kernels per row, so the loss is bitwise and the grads agree to the run-to-run order of
+    the adapter-gradient atomics."""
+    from ltx_amd import transformer3d as T
+    cfg = dict(T.OURS_TRANSFORMER_CONFIG, num_layers=3)
+    params = O.make_params(cfg, 43, lora_rank=16, requires_grad=False)
+    d = _inputs(8, 7, 16, 16, 256, 16, seed=17)
+    res = {}
+    saved = T._TEXT_KNORM_GROUPED
+    try:
+        for grouped in (False, True):
+            T._TEXT_KNORM_GROUPED = grouped
+            model = build_model(cfg, params, 16, device=DEV)
+            assert model._text_batchable()
+            loss = _build_step(model, d)
+            res[grouped] = (loss, grads_by_canonical(model))
+    finally:
+        T._TEXT_KNORM_GROUPED = saved
+    (l0, g0), (l1, g1) = res[False], res[True]
+    assert l0 == l1, (l0, l1)
+    assert set(g0) == set(g1)
+    for name in g0:
+        e = rel(g1[name].float(), g0[name].float())
+        assert e <= 1e-5, f"{name}: grouped vs per-block k_norm {e:.3e}"
+
+
 def test_frozen_caption_projection_keeps_text_adapter_grads():
     """LoRA on attn2 with caption_projection FROZEN: enc2 then carries no grad, so the
     batched text side -- whose backward runs as enc2's -- must not be used; the per-block path

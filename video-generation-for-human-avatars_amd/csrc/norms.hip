@@ -344,21 +344,31 @@ __device__ __forceinline__ void load_cs_raw(const uint32_t* __restrict__ csr, in
   for (int p = 0; p < MAXP; ++p) raw[p] = *(const u32x4*)(csr + (min(p * 512 + lane * 8, D - 8) >> 1));
 }
 
+// Grouped q-only launches: rows [g * rows, (g + 1) * rows) are group g, whose input / gradient /
+// output rows start g * in / gin / out elements further and whose weight / rstd rows g * w / r
+// (ungrouped launches: rows = M, every stride 0)
+struct QkGroups {
+  int rows;
+  int64_t in, gin, out, w, r;
+};
+
 // one wave = one (row, q|k) item
 __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
     const bf16_t* __restrict__ q_in, int64_t ldq_in, const bf16_t* __restrict__ k_in, int64_t ldk_in,
     bf16_t* __restrict__ q_out, int64_t ldq_out, bf16_t* __restrict__ k_out, int64_t ldk_out,
     const bf16_t* __restrict__ qw, const bf16_t* __restrict__ kw, float* __restrict__ rstd_q,
     float* __restrict__ rstd_k, const uint32_t* __restrict__ cs, int64_t cs_batch_rows, int N, int M, int D,
-    int rope, int nsel, float eps) {
+    int rope, int nsel, float eps, QkGroups gq) {
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
   const int m = item / nsel;
   const int which = item - m * nsel;  // 0 = q, 1 = k
   if (m >= M) return;
-  const bf16_t* in = which ? k_in + (int64_t)m * ldk_in : q_in + (int64_t)m * ldq_in;
-  bf16_t* out = which ? k_out + (int64_t)m * ldk_out : q_out + (int64_t)m * ldq_out;
-  const bf16_t* w = which ? kw : qw;
+  // grouped q-only launches (ltx_qk_norm_fwd_grouped): row m is row mr of group g
+  const int g = m / gq.rows, mr = m - g * gq.rows;
+  const bf16_t* in = which ? k_in + (int64_t)m * ldk_in : q_in + g * gq.in + (int64_t)mr * ldq_in;
+  bf16_t* out = which ? k_out + (int64_t)m * ldk_out : q_out + g * gq.out + (int64_t)mr * ldq_out;
+  const bf16_t* w = which ? kw : qw + g * gq.w;
   float v[MAXP][8];
   float ss = 0.f;
   // the row, the weight and the RoPE words: one round trip
@@ -380,7 +390,10 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_fwd_kernel(
   }
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)D + eps);
-  if (lane == 0) (which ? rstd_k : rstd_q)[m] = r;
+  if (lane == 0) {
+    if (which) rstd_k[m] = r;
+    else rstd_q[g * gq.r + mr] = r;
+  }
 #pragma unroll
   for (int p = 0; p < MAXP; ++p) {
     const int e = p * 512 + lane * 8;
@@ -417,25 +430,28 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
     int64_t ldk_raw, const bf16_t* __restrict__ qw, const bf16_t* __restrict__ kw,
     const float* __restrict__ rstd_q, const float* __restrict__ rstd_k, bf16_t* __restrict__ dq_out,
     int64_t ldq_out, bf16_t* __restrict__ dk_out, int64_t ldk_out, const uint32_t* __restrict__ cs,
-    int64_t cs_batch_rows, int N, int M, int D, int rope, int nsel) {
+    int64_t cs_batch_rows, int N, int M, int D, int rope, int nsel, QkGroups gq) {
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * (ROW_THREADS / 64) + (threadIdx.x >> 6);
   const int m = item / nsel;
   const int which = item - m * nsel;
   if (m >= M) return;
-  const void* gin = which ? dk_in : dq_in;
+  // grouped q-only launches (ltx_qk_norm_bwd_grouped): row m is row mr of group g
+  const int g = m / gq.rows, mr = m - g * gq.rows;
+  const void* gin = which ? dk_in : (const void*)((const bf16_t*)dq_in + g * gq.gin);
   const int64_t ldg = which ? ldk_in : ldq_in;
   const int gf32 = which ? dk_f32 : dq_f32;
-  const bf16_t* xin = which ? k_raw + (int64_t)m * ldk_raw : q_raw + (int64_t)m * ldq_raw;
-  bf16_t* out = which ? dk_out + (int64_t)m * ldk_out : dq_out + (int64_t)m * ldq_out;
-  const bf16_t* w = which ? kw : qw;
-  const float r = (which ? rstd_k : rstd_q)[m];
+  const bf16_t* xin = which ? k_raw + (int64_t)m * ldk_raw : q_raw + g * gq.in + (int64_t)mr * ldq_raw;
+  bf16_t* out = which ? dk_out + (int64_t)m * ldk_out : dq_out + g * gq.out + (int64_t)mr * ldq_out;
+  const bf16_t* w = which ? kw : qw + g * gq.w;
+  const float r = which ? rstd_k[m] : rstd_q[g * gq.r + mr];
   const int64_t csrow = ((int64_t)(m / N) * cs_batch_rows + (m % N)) * (D / 2);
   float gx[MAXP][8], xv[MAXP][8];
   float dr = 0.f;
   // the bf16 gradient row and the input row: all chunks in flight together
   u32x4 graw[MAXP], xraw[MAXP], wraw[MAXP], csraw[MAXP];
-  if (!gf32) load_row_raw((const bf16_t*)gin + (int64_t)m * ldg, D, lane, graw);
+  const int mg = which ? m : mr;  // the gradient row inside its group (m when ungrouped)
+  if (!gf32) load_row_raw((const bf16_t*)gin + (int64_t)mg * ldg, D, lane, graw);
   load_row_raw(xin, D, lane, xraw);
   load_row_raw(w, D, lane, wraw);
   if (rope) load_cs_raw(cs + csrow, D, lane, csraw);
@@ -445,7 +461,7 @@ __global__ __launch_bounds__(ROW_THREADS) void qk_norm_rope_bwd_kernel(
     if (e < D) {
       float g8[8], w8[8], dn[8];
       if (gf32) {
-        load8f((const float*)gin + (int64_t)m * ldg + e, g8);
+        load8f((const float*)gin + (int64_t)mg * ldg + e, g8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) g8[j] = rbf(g8[j]);
       } else {
@@ -652,7 +668,8 @@ int ltx_qk_norm_rope_fwd(const void* q_in, int64_t ldq_in, const void* k_in, int
   hipLaunchKernelGGL(qk_norm_rope_fwd_kernel, dim3(row_blocks(M * nsel)), dim3(ROW_THREADS), 0,
                      (hipStream_t)stream, (const bf16_t*)q_in, ldq_in, (const bf16_t*)k_in, ldk_in, (bf16_t*)q_out,
                      ldq_out, (bf16_t*)k_out, ldk_out, (const bf16_t*)q_weight, (const bf16_t*)k_weight, rstd_q,
-                     rstd_k, rope_cs, cs_batch_rows, (int)N, (int)M, (int)D, rope, nsel, eps);
+                     rstd_k, rope_cs, cs_batch_rows, (int)N, (int)M, (int)D, rope, nsel, eps,
+                     QkGroups{(int)M, 0, 0, 0, 0, 0});
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }
@@ -679,7 +696,48 @@ int ltx_qk_norm_rope_bwd(const void* dq_in, int64_t ldq_in, int dq_is_f32, const
                      (hipStream_t)stream, dq_in, ldq_in, dq_is_f32, dk_in, ldk_in, dk_is_f32, (const bf16_t*)q_raw,
                      ldq_raw, (const bf16_t*)k_raw, ldk_raw, (const bf16_t*)q_weight, (const bf16_t*)k_weight,
                      rstd_q, rstd_k, (bf16_t*)dq_out, ldq_out, (bf16_t*)dk_out, ldk_out, rope_cs, cs_batch_rows,
-                     (int)N, (int)M, (int)D, rope, nsel);
+                     (int)N, (int)M, (int)D, rope, nsel, QkGroups{(int)M, 0, 0, 0, 0, 0});
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+// the text keys' RMSNorm of every block in one launch (the batched text side of LoRA training):
+// group g = block g, rows = the text tokens, no RoPE, bf16 in / out
+int ltx_qk_norm_fwd_grouped(const void* x, int64_t ldx, int64_t x_gs, void* y, int64_t ldy, int64_t y_gs,
+                            const void* weight, int64_t w_gs, float* rstd, int64_t r_gs, int64_t rows,
+                            int64_t groups, int64_t D, float eps, void* stream) {
+  LTX_CHECK_ARG(x && y && weight && rstd && rows > 0 && groups > 0, "qk_norm_fwd_grouped: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "qk_norm_fwd_grouped: D must be %8 and <= 2048");
+  LTX_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0 && x_gs % 8 == 0 && y_gs % 8 == 0 && w_gs % 8 == 0 &&
+                    ((((uintptr_t)x | (uintptr_t)y | (uintptr_t)weight) % 16) == 0),
+                "qk_norm_fwd_grouped: 16-B aligned rows and group strides");
+  LTX_CHECK_ARG(rows * groups < ((int64_t)1 << 31), "qk_norm_fwd_grouped: too many rows");
+  const int64_t M = rows * groups;
+  hipLaunchKernelGGL(qk_norm_rope_fwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, ldx, (const bf16_t*)nullptr, (int64_t)0, (bf16_t*)y, ldy, (bf16_t*)nullptr,
+                     (int64_t)0, (const bf16_t*)weight, (const bf16_t*)nullptr, rstd, (float*)nullptr,
+                     (const uint32_t*)nullptr, (int64_t)0, (int)rows, (int)M, (int)D, 0, 1, eps,
+                     QkGroups{(int)rows, x_gs, 0, y_gs, w_gs, r_gs});
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+int ltx_qk_norm_bwd_grouped(const void* dy, int64_t lddy, int64_t dy_gs, const void* x, int64_t ldx, int64_t x_gs,
+                            const void* weight, int64_t w_gs, const float* rstd, int64_t r_gs, void* dx,
+                            int64_t lddx, int64_t dx_gs, int64_t rows, int64_t groups, int64_t D, void* stream) {
+  LTX_CHECK_ARG(dy && x && weight && rstd && dx && rows > 0 && groups > 0, "qk_norm_bwd_grouped: bad args");
+  LTX_CHECK_ARG(D % 8 == 0 && D <= 2048, "qk_norm_bwd_grouped: D must be %8 and <= 2048");
+  LTX_CHECK_ARG(lddy % 8 == 0 && ldx % 8 == 0 && lddx % 8 == 0 && dy_gs % 8 == 0 && x_gs % 8 == 0 &&
+                    dx_gs % 8 == 0 && w_gs % 8 == 0 &&
+                    ((((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dx | (uintptr_t)weight) % 16) == 0),
+                "qk_norm_bwd_grouped: 16-B aligned rows and group strides");
+  LTX_CHECK_ARG(rows * groups < ((int64_t)1 << 31), "qk_norm_bwd_grouped: too many rows");
+  const int64_t M = rows * groups;
+  hipLaunchKernelGGL(qk_norm_rope_bwd_kernel, dim3(row_blocks(M)), dim3(ROW_THREADS), 0, (hipStream_t)stream, dy,
+                     lddy, 0, (const void*)nullptr, (int64_t)0, 0, (const bf16_t*)x, ldx, (const bf16_t*)nullptr,
+                     (int64_t)0, (const bf16_t*)weight, (const bf16_t*)nullptr, rstd, (const float*)nullptr,
+                     (bf16_t*)dx, lddx, (bf16_t*)nullptr, (int64_t)0, (const uint32_t*)nullptr, (int64_t)0,
+                     (int)rows, (int)M, (int)D, 0, 1, QkGroups{(int)rows, x_gs, dy_gs, dx_gs, w_gs, r_gs});
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

@@ -43,6 +43,10 @@ _SIGNATURES = {
                              _i64, _i64, _i64, _i32, _f32, _p],
     "ltx_qk_norm_rope_bwd": [_p, _i64, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _p, _p, _p, _p,
                              _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i32, _p],
+    "ltx_qk_norm_fwd_grouped": [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64,
+                                _f32, _p],
+    "ltx_qk_norm_bwd_grouped": [_p, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64, _p, _i64, _i64,
+                                _i64, _i64, _i64, _p],
     "ltx_attn_fwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _i64, _i64, _i64, _i64,
                      _i64, _f32, _p],
     "ltx_attn_bwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i32,

@@ -311,6 +311,33 @@ def qk_norm_rope_bwd(dq, q_raw, q_w, rq, dk=None, k_raw=None, k_w=None, rk=None,
     return dq_out, (dk_out if dk is not None else None)
 
 
+def qk_norm_fwd_grouped(x, x_gs, weights, eps=1e-5):
+    """The attn2 k_norm of every block's text keys in one launch (ltx_qk_norm_fwd_grouped):
+    group g is the [rows, D] view starting x_gs elements after x's first element (row stride
+    x.stride(0)), normalised with weights[g]. Returns y [G, rows, D] bf16 and rstd [G, rows] f32,
+    bitwise the per-group qk_norm_rope_fwd(x_g, None, weights[g], ...) calls."""
+    G, D = weights.shape
+    rows = x.shape[0]
+    _need(weights, BF16, "weights")
+    assert weights.is_contiguous() and x.shape[1] >= D and x_gs >= 0
+    y = torch.empty(G, rows, D, dtype=BF16, device=x.device)
+    rstd = torch.empty(G, rows, dtype=F32, device=x.device)
+    call("ltx_qk_norm_fwd_grouped", _p(x), _rows(x, "x"), x_gs, _p(y), D, rows * D, _p(weights), D,
+         _p(rstd), rows, rows, G, D, eps, _s())
+    return y, rstd
+
+
+def qk_norm_bwd_grouped(dy, x, x_gs, weights, rstd, dx, dx_gs):
+    """Backward of qk_norm_fwd_grouped: dy [G, rows, D] bf16 -> group g's input gradient written
+    to the [rows, D] view of dx starting dx_gs * g elements in (row stride dx.stride(0))."""
+    G, rows, D = dy.shape
+    assert dy.is_contiguous() and weights.is_contiguous() and rstd.is_contiguous()
+    assert rstd.shape == (G, rows) and x.shape[0] == rows and dx.shape[0] == rows
+    call("ltx_qk_norm_bwd_grouped", _p(dy), D, rows * D, _p(x), _rows(x, "x"), x_gs, _p(weights), D,
+         _p(rstd), rows, _p(dx), _rows(dx, "dx"), dx_gs, rows, G, D, _s())
+    return dx
+
+
 # ---------------------------------------------------------------------------------------------
 # attention
 # ---------------------------------------------------------------------------------------------

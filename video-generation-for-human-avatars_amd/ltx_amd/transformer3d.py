@@ -602,20 +602,26 @@ class _BlockFn(torch.autograd.Function):
         else:
             dkv = torch.empty(k2raw.shape[0], 2 * D, dtype=torch.bfloat16, device=h.device)
         dk2b = dv2b = None
+        # with the grouped text k_norm the stack keeps this block's dK (the norm's backward runs
+        # for every block at once in _TextStack.backward)
+        dk2_keep = tx.block_dk2(blk) if tx is not None and tx.grouped_norm else None
         if sh.text_shared:  # gradient of the shared text rows = sum over the query batches
             dq2, dk2b, dv2b = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
                                            key_bias=sh.enc_bias, kv_shared=True, delta=delta2)
-            dk2 = ops.batch_sum(dk2b, B)
+            dk2 = ops.batch_sum(dk2b, B, out=dk2_keep)
             dv2 = ops.batch_sum(dv2b, B, out=dkv[:, D:])
             if not full:
                 dk2b = dv2b = None
         else:
             dq2, dk2, dv2 = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
-                                         key_bias=sh.enc_bias, dv=dkv[:, D:], delta=delta2)
+                                         key_bias=sh.enc_bias, dk=dk2_keep, dv=dkv[:, D:], delta=delta2)
         del do2
         dq2raw, _ = ops.qk_norm_rope_bwd(dq2, q2raw, a2.q_norm.weight, rq2, B=B, N=N)
-        dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=sh.Bt, N=L,
-                                         dq_out=dkv[:, :D])
+        if dk2_keep is None:
+            dk2raw, _ = ops.qk_norm_rope_bwd(dk2, k2raw, a2.k_norm.weight, rk2, B=sh.Bt, N=L,
+                                             dq_out=dkv[:, :D])
+        else:
+            dk2raw = None
         if full:  # attn2 q/k norm weights, to_q / to_k / to_v
             ops.qk_norm_wgrad_into(dq2, q2raw, rq2, _pgrad(a2.q_norm.weight), B=B, N=N)
             ops.wgrad_into(_pgrad(a2.to_q.weight), dq2raw, h1)
@@ -803,6 +809,8 @@ _TEXT_BATCH = os.environ.get("LTX_TEXT_BATCH", "1") != "0"
 # the attention backward's delta = rowsum(dO*O) written by the dO GEMM's epilogue
 # (LTX_EPI_STORE_ROWDOT) instead of a separate pass over dO and O (LTX_DELTA_FUSED=0: separate)
 _DELTA_FUSED = os.environ.get("LTX_DELTA_FUSED", "1") != "0"
+# LTX_TEXT_KNORM_GROUPED=0: the batched text side runs its attn2 k_norm per block (fwd and bwd)
+_TEXT_KNORM_GROUPED = os.environ.get("LTX_TEXT_KNORM_GROUPED", "1") != "0"
 
 
 class _TextStack:
@@ -847,6 +855,12 @@ class _TextStack:
                            ext_group=(2 * D, 2 * K2))
         del su
         self.dkv = torch.empty(Lt, 2 * n * D, dtype=torch.bfloat16, device=dev)
+        # the k_norm of every block's text keys: one grouped launch (bitwise the per-block calls)
+        self.knw = c["knw"]
+        self.grouped_norm = self.knw is not None and _TEXT_KNORM_GROUPED
+        if self.grouped_norm:
+            self.k2_all, self.rk2_all = ops.qk_norm_fwd_grouped(self.kv, 2 * D, self.knw)
+            self.dk2_all = torch.empty(n, Lt, D, dtype=torch.bfloat16, device=dev)
 
     def block_kv(self, blk, sh):
         """(k2raw, k2, rk2, v2, u_k, u_v) of one block: views of the stacked results + the k
@@ -856,8 +870,11 @@ class _TextStack:
         i, D, r = self.index[id(blk)], self.D, self.r
         k2raw = self.kv[:, 2 * i * D:(2 * i + 1) * D]
         v2 = self.kv[:, (2 * i + 1) * D:(2 * i + 2) * D]
-        k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, blk.attn2.k_norm.weight, None, None,
-                                             B=sh.Bt, N=sh.L)
+        if self.grouped_norm:
+            k2, rk2 = self.k2_all[i], self.rk2_all[i]
+        else:
+            k2, _, rk2, _ = ops.qk_norm_rope_fwd(k2raw, None, blk.attn2.k_norm.weight, None, None,
+                                                 B=sh.Bt, N=sh.L)
         return (k2raw, k2, rk2, v2, self.u[:, 2 * i * r:(2 * i + 1) * r],
                 self.u[:, (2 * i + 1) * r:(2 * i + 2) * r])
 
@@ -865,12 +882,19 @@ class _TextStack:
         i, D = self.index[id(blk)], self.D
         return self.dkv[:, 2 * i * D:2 * (i + 1) * D]
 
+    def block_dk2(self, blk):
+        """this block's dK of the normalised text keys (grouped_norm: the input of the grouped
+        k_norm backward)"""
+        return self.dk2_all[self.index[id(blk)]]
+
     def backward(self):
         """Adapter grads of every block's to_k / to_v (into .grad) and the encoder gradient."""
         n, D, r, K2, s = len(self.blocks), self.D, self.r, self.K2, self.s
         enc2, dkv = self.enc2, self.dkv
         Lt = enc2.shape[0]
         dev = enc2.device
+        if self.grouped_norm:  # every block's k_norm backward -> its dK_raw columns of dkv
+            ops.qk_norm_bwd_grouped(self.dk2_all, self.kv, 2 * D, self.knw, self.rk2_all, dkv, 2 * D)
         # lora_B grads: dB_j = s * dY_j^T . u_j  (dY of adapter j = columns j*D .. of dkv)
         dB = ops.lora_wgrad(dkv[:, :D], self.u[:, :r], alpha=s, groups=2 * n,
                             group_strides=(D, r))
@@ -1204,8 +1228,11 @@ class Transformer3DModel(nn.Module):
         packs = [b.packed() for b in blocks]
         exts = [_kv_ext(b, l[1], l[2]) for b, l in zip(blocks, lins)]
         abs_ = [t for m in adapters for t in _ab(m)]
+        knws = [b.attn2.k_norm.weight for b in blocks]
+        knws_ok = all(w is not None and w.dtype == torch.bfloat16 and w.numel() == st["D"] for w in knws)
         key = (tuple(id(pk) for pk in packs), tuple(id(e[0]) for e in exts),
-               tuple((t.data_ptr(), t._version) for t in abs_), ops.weight_generation())
+               tuple((t.data_ptr(), t._version) for t in abs_), ops.weight_generation(),
+               tuple((w.data_ptr(), w._version) for w in knws) if knws_ok else None)
         c = getattr(self, "_tx_cache", None)
         if c is not None and c["key"] == key:
             return c
@@ -1222,7 +1249,8 @@ class Transformer3DModel(nn.Module):
                   "ext_f": torch.cat([e[0] for e in exts], 0),
                   "ext_b": torch.cat([e[1] for e in exts], 1),
                   "A": torch.stack([_ab(m)[0] for m in adapters]),
-                  "B": torch.stack([_ab(m)[1] for m in adapters])})
+                  "B": torch.stack([_ab(m)[1] for m in adapters]),
+                  "knw": torch.stack([w.detach() for w in knws]).contiguous() if knws_ok else None})
         self._tx_cache = c
         return c
 
