@@ -856,7 +856,7 @@ class _TextStack:
         del su
         self.dkv = torch.empty(Lt, 2 * n * D, dtype=torch.bfloat16, device=dev)
         # the k_norm of every block's text keys: one grouped launch (bitwise the per-block calls)
-        self.knw = c["knw"]
+        self.knw = self.model._text_knorm_weights(self.blocks, D)
         self.grouped_norm = self.knw is not None and _TEXT_KNORM_GROUPED
         if self.grouped_norm:
             self.k2_all, self.rk2_all = ops.qk_norm_fwd_grouped(self.kv, 2 * D, self.knw)
@@ -1177,6 +1177,19 @@ class Transformer3DModel(nn.Module):
             model.patchifier = patchifier
         return model
 
+    def _text_knorm_weights(self, blocks, D):
+        """[n, D] stack of the blocks' attn2 k_norm weights for the grouped text k_norm (frozen in
+        LoRA training: rebuilt only when one of them changes), or None when one is missing."""
+        knws = [b.attn2.k_norm.weight for b in blocks]
+        if not all(w is not None and w.dtype == torch.bfloat16 and w.numel() == D for w in knws):
+            return None
+        key = tuple((w.data_ptr(), w._version) for w in knws)
+        c = getattr(self, "_knw_cache", None)
+        if c is None or c[0] != key:
+            c = (key, torch.stack([w.detach() for w in knws]).contiguous())
+            self._knw_cache = c
+        return c[1]
+
     def _text_structure(self):
         """Module-structure facts of the batched text side, cached on the identity of every
         block's attn2 projections and the trainability of the K/V base weights (cheap to check;
@@ -1228,11 +1241,8 @@ class Transformer3DModel(nn.Module):
         packs = [b.packed() for b in blocks]
         exts = [_kv_ext(b, l[1], l[2]) for b, l in zip(blocks, lins)]
         abs_ = [t for m in adapters for t in _ab(m)]
-        knws = [b.attn2.k_norm.weight for b in blocks]
-        knws_ok = all(w is not None and w.dtype == torch.bfloat16 and w.numel() == st["D"] for w in knws)
         key = (tuple(id(pk) for pk in packs), tuple(id(e[0]) for e in exts),
-               tuple((t.data_ptr(), t._version) for t in abs_), ops.weight_generation(),
-               tuple((w.data_ptr(), w._version) for w in knws) if knws_ok else None)
+               tuple((t.data_ptr(), t._version) for t in abs_), ops.weight_generation())
         c = getattr(self, "_tx_cache", None)
         if c is not None and c["key"] == key:
             return c
@@ -1249,8 +1259,7 @@ class Transformer3DModel(nn.Module):
                   "ext_f": torch.cat([e[0] for e in exts], 0),
                   "ext_b": torch.cat([e[1] for e in exts], 1),
                   "A": torch.stack([_ab(m)[0] for m in adapters]),
-                  "B": torch.stack([_ab(m)[1] for m in adapters]),
-                  "knw": torch.stack([w.detach() for w in knws]).contiguous() if knws_ok else None})
+                  "B": torch.stack([_ab(m)[1] for m in adapters])})
         self._tx_cache = c
         return c
 
