@@ -505,7 +505,13 @@ def test_qk_norm_grouped_matches_per_group():
     y, rstd = ops.qk_norm_fwd_grouped(kv, 2 * D, w)
     dy = g(G, L, D, seed=22)
     dx = torch.zeros(L, 2 * G * D, dtype=torch.bfloat16, device=DEV)
-    ops.qk_norm_bwd_grouped(dy, kv, 2 * D, w, rstd, dx, 2 * D)
+    ops.qk_norm_bwd_grouped(dy.view(G * L, D), L * D, kv, 2 * D, w, rstd, dx, 2 * D)
+    # in place on a strided stack (the batched text side's dkv k columns)
+    dk_inplace = torch.zeros(L, 2 * G * D, dtype=torch.bfloat16, device=DEV)
+    for i in range(G):
+        dk_inplace[:, 2 * i * D:(2 * i + 1) * D] = dy[i]
+    ops.qk_norm_bwd_grouped(dk_inplace, 2 * D, kv, 2 * D, w, rstd, dk_inplace, 2 * D)
+    assert torch.equal(dk_inplace, dx)
     for i in range(G):
         xi = kv[:, 2 * i * D:(2 * i + 1) * D]
         yi, _, ri, _ = ops.qk_norm_rope_fwd(xi, None, w[i], None, None, B=1, N=L)

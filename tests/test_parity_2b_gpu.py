@@ -280,7 +280,8 @@ def test_text_stack_matches_per_block():
 
 def test_text_stack_grouped_knorm():
     """The batched text side's attn2 k_norm as ONE grouped launch for every block, forward and
-    backward (LTX_TEXT_KNORM_GROUPED, ltx_qk_norm_{fwd,bwd}_grouped), against one launch per block:
+    backward (LTX_TEXT_KNORM_GROUPED, ltx_qk_norm_{fwd,bwd}_grouped), and the query-batch sums of
+    the text-key gradients as one launch (LTX_TEXT_BSUM_GROUPED), against one launch per block:
     the same kernels per row, so the loss is bitwise and the grads agree to the run-to-run order of
     the adapter-gradient atomics."""
     from ltx_amd import transformer3d as T
@@ -288,22 +289,25 @@ def test_text_stack_grouped_knorm():
     params = O.make_params(cfg, 43, lora_rank=16, requires_grad=False)
     d = _inputs(8, 7, 16, 16, 256, 16, seed=17)
     res = {}
-    saved = T._TEXT_KNORM_GROUPED
+    saved = T._TEXT_KNORM_GROUPED, T._TEXT_BSUM_GROUPED
     try:
-        for grouped in (False, True):
-            T._TEXT_KNORM_GROUPED = grouped
+        # per block; grouped k_norm with per-block batch sums; grouped k_norm + grouped batch sums
+        for mode, (kn, bs) in {"block": (False, False), "knorm": (True, False), "both": (True, True)}.items():
+            T._TEXT_KNORM_GROUPED, T._TEXT_BSUM_GROUPED = kn, bs
             model = build_model(cfg, params, 16, device=DEV)
             assert model._text_batchable()
             loss = _build_step(model, d)
-            res[grouped] = (loss, grads_by_canonical(model))
+            res[mode] = (loss, grads_by_canonical(model))
     finally:
-        T._TEXT_KNORM_GROUPED = saved
-    (l0, g0), (l1, g1) = res[False], res[True]
-    assert l0 == l1, (l0, l1)
-    assert set(g0) == set(g1)
-    for name in g0:
-        e = rel(g1[name].float(), g0[name].float())
-        assert e <= 1e-5, f"{name}: grouped vs per-block k_norm {e:.3e}"
+        T._TEXT_KNORM_GROUPED, T._TEXT_BSUM_GROUPED = saved
+    l0, g0 = res["block"]
+    for mode in ("knorm", "both"):
+        l1, g1 = res[mode]
+        assert l0 == l1, (mode, l0, l1)
+        assert set(g0) == set(g1)
+        for name in g0:
+            e = rel(g1[name].float(), g0[name].float())
+            assert e <= 1e-5, f"{mode} {name}: grouped vs per-block {e:.3e}"
 
 
 def test_frozen_caption_projection_keeps_text_adapter_grads():

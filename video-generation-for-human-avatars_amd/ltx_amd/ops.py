@@ -327,14 +327,18 @@ def qk_norm_fwd_grouped(x, x_gs, weights, eps=1e-5):
     return y, rstd
 
 
-def qk_norm_bwd_grouped(dy, x, x_gs, weights, rstd, dx, dx_gs):
-    """Backward of qk_norm_fwd_grouped: dy [G, rows, D] bf16 -> group g's input gradient written
-    to the [rows, D] view of dx starting dx_gs * g elements in (row stride dx.stride(0))."""
-    G, rows, D = dy.shape
-    assert dy.is_contiguous() and weights.is_contiguous() and rstd.is_contiguous()
-    assert rstd.shape == (G, rows) and x.shape[0] == rows and dx.shape[0] == rows
-    call("ltx_qk_norm_bwd_grouped", _p(dy), D, rows * D, _p(x), _rows(x, "x"), x_gs, _p(weights), D,
-         _p(rstd), rows, _p(dx), _rows(dx, "dx"), dx_gs, rows, G, D, _s())
+def qk_norm_bwd_grouped(dy, dy_gs, x, x_gs, weights, rstd, dx, dx_gs):
+    """Backward of qk_norm_fwd_grouped: group g's incoming gradient is the [rows, D] view of the
+    2-D dy starting g * dy_gs elements in (row stride dy.stride(0)); its input gradient goes to
+    the view of dx starting g * dx_gs elements in. dx may be dy (in place: each row is read whole
+    before it is written)."""
+    G, D = weights.shape
+    rows = x.shape[0]
+    assert weights.is_contiguous() and rstd.is_contiguous()
+    assert rstd.shape == (G, rows) and dx.shape[0] == rows
+    assert dy.numel() >= (G - 1) * dy_gs + (rows - 1) * dy.stride(0) + D
+    call("ltx_qk_norm_bwd_grouped", _p(dy), _rows(dy, "dy"), dy_gs, _p(x), _rows(x, "x"), x_gs,
+         _p(weights), D, _p(rstd), rows, _p(dx), _rows(dx, "dx"), dx_gs, rows, G, D, _s())
     return dx
 
 

@@ -605,7 +605,13 @@ class _BlockFn(torch.autograd.Function):
         # with the grouped text k_norm the stack keeps this block's dK (the norm's backward runs
         # for every block at once in _TextStack.backward)
         dk2_keep = tx.block_dk2(blk) if tx is not None and tx.grouped_norm else None
-        if sh.text_shared:  # gradient of the shared text rows = sum over the query batches
+        if sh.text_shared and dk2_keep is not None and _TEXT_BSUM_GROUPED:
+            # the batch sums of every block run in _TextStack.backward (one launch)
+            dkb, dvb = tx.block_dkvb(blk, B)
+            dq2, _, _ = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale, key_bias=sh.enc_bias,
+                                     kv_shared=True, dk=dkb, dv=dvb, delta=delta2)
+            dk2 = dv2 = None
+        elif sh.text_shared:  # gradient of the shared text rows = sum over the query batches
             dq2, dk2b, dv2b = ops.attn_bwd(q2, k2, v2, o2, do2, lse2, B, H, d, a2.scale,
                                            key_bias=sh.enc_bias, kv_shared=True, delta=delta2)
             dk2 = ops.batch_sum(dk2b, B, out=dk2_keep)
@@ -811,6 +817,9 @@ _TEXT_BATCH = os.environ.get("LTX_TEXT_BATCH", "1") != "0"
 _DELTA_FUSED = os.environ.get("LTX_DELTA_FUSED", "1") != "0"
 # LTX_TEXT_KNORM_GROUPED=0: the batched text side runs its attn2 k_norm per block (fwd and bwd)
 _TEXT_KNORM_GROUPED = os.environ.get("LTX_TEXT_KNORM_GROUPED", "1") != "0"
+# LTX_TEXT_BSUM_GROUPED=0: with the grouped k_norm and a shared prompt, the query-batch sums of the
+# text-key gradients run per block (two launches each) instead of once for every block
+_TEXT_BSUM_GROUPED = os.environ.get("LTX_TEXT_BSUM_GROUPED", "1") != "0"
 
 
 class _TextStack:
@@ -858,6 +867,7 @@ class _TextStack:
         # the k_norm of every block's text keys: one grouped launch (bitwise the per-block calls)
         self.knw = self.model._text_knorm_weights(self.blocks, D)
         self.grouped_norm = self.knw is not None and _TEXT_KNORM_GROUPED
+        self.dkvb = None  # [B*Lt, 2nD] per-query-batch [dK | dV] of every block (block_dkvb)
         if self.grouped_norm:
             self.k2_all, self.rk2_all = ops.qk_norm_fwd_grouped(self.kv, 2 * D, self.knw)
             self.dk2_all = torch.empty(n, Lt, D, dtype=torch.bfloat16, device=dev)
@@ -882,6 +892,17 @@ class _TextStack:
         i, D = self.index[id(blk)], self.D
         return self.dkv[:, 2 * i * D:2 * (i + 1) * D]
 
+    def block_dkvb(self, blk, B):
+        """(dK, dV) column views of this block in the [B*Lt, 2nD] stack of the per-query-batch
+        text-key gradients (shared prompt, grouped_norm): _TextStack.backward sums the batches of
+        every block in one launch instead of two per block"""
+        n, D = len(self.blocks), self.D
+        if self.dkvb is None:
+            self.dkvb = torch.empty(B * self.kv.shape[0], 2 * n * D, dtype=torch.bfloat16,
+                                    device=self.kv.device)
+        i = self.index[id(blk)]
+        return self.dkvb[:, 2 * i * D:(2 * i + 1) * D], self.dkvb[:, (2 * i + 1) * D:(2 * i + 2) * D]
+
     def block_dk2(self, blk):
         """this block's dK of the normalised text keys (grouped_norm: the input of the grouped
         k_norm backward)"""
@@ -894,7 +915,14 @@ class _TextStack:
         Lt = enc2.shape[0]
         dev = enc2.device
         if self.grouped_norm:  # every block's k_norm backward -> its dK_raw columns of dkv
-            ops.qk_norm_bwd_grouped(self.dk2_all, self.kv, 2 * D, self.knw, self.rk2_all, dkv, 2 * D)
+            if self.dkvb is not None:
+                # the query batches' [dK | dV] of every block in one sum: dkv's k columns then
+                # hold each block's dK at the normalised keys, normalised in place below
+                ops.batch_sum(self.dkvb, self.dkvb.shape[0] // Lt, out=dkv)
+                ops.qk_norm_bwd_grouped(dkv, 2 * D, self.kv, 2 * D, self.knw, self.rk2_all, dkv, 2 * D)
+            else:
+                ops.qk_norm_bwd_grouped(self.dk2_all.view(n * Lt, D), Lt * D, self.kv, 2 * D, self.knw,
+                                        self.rk2_all, dkv, 2 * D)
         # lora_B grads: dB_j = s * dY_j^T . u_j  (dY of adapter j = columns j*D .. of dkv)
         dB = ops.lora_wgrad(dkv[:, :D], self.u[:, :r], alpha=s, groups=2 * n,
                             group_strides=(D, r))
