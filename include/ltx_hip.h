@@ -302,7 +302,9 @@ int ltx_lora_rows(const void* x, int64_t ldx, const void* w3, int64_t ldw, float
 /* dW(n,j) (+)= alpha * sum_m Y[m,n] * U[m,j] at dw[n*on + j*oj] (f32; overwritten, or added to
  * when accumulate != 0, e.g. straight into a .grad buffer across micro-steps):
  * lora_B grad (Y = dY, U = u: on = r, oj = 1) and lora_A grad (Y = x, U = w: on = 1, oj = K).
- * Y bf16 [M,N] (ldy), U f32 [M,r] (ldu). Split-M partial sums are combined with f32 atomics. */
+ * Y bf16 [M,N] (ldy), U f32 [M,r] (ldu). Deterministic: split-M partial sums go to the stream's
+ * GEMM workspace (ltx_gemm_set_stream_workspace / ltx_gemm_set_workspace) and are added in split
+ * order by a second kernel; without room there one workgroup per output column block covers all M. */
 int ltx_lora_wgrad(const void* y, int64_t ldy, const float* u, int64_t ldu, float* dw,
                    int64_t on, int64_t oj, int64_t M, int64_t N, int64_t r, float alpha,
                    int accumulate, void* stream);
@@ -386,7 +388,8 @@ int ltx_silu_bwd_bf16(const void* x, const void* dy, const void* dres, void* dx,
 /* ---- ZeRO-2 optimizer buffers (BASELINE config Z; csrc/zero.hip) ------------------------------ */
 int ltx_cast_bf16_f32(const void* src, float* dst, int64_t n, void* stream);
 int ltx_cast_f32_bf16(const float* src, void* dst, int64_t n, void* stream);
-/* out (one f64 on the device) [+]= sum x^2 */
+/* out (one f64 on the device) [+]= sum x^2; deterministic when the stream has a GEMM workspace
+ * (per-block f64 partials there, added in block order), else one f64 atomic per block */
 int ltx_sumsq_f32(const float* x, int64_t n, double* out, int accumulate, void* stream);
 /* coef = inv_world * min(1, max_norm / (sqrt(sumsq) * inv_world + 1e-6)) (max_norm <= 0: 1),
  * written to *coef; x *= coef (the averaged, global-norm-clipped gradient shard; DeepSpeed

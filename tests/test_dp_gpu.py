@@ -168,3 +168,119 @@ def test_dp_overlapped_allreduce_ltx2b_28_layers_real_buckets():
     n16 = sum(n for dt, n in bks if dt == "torch.bfloat16")
     assert n32 == 7_340_032 and n16 == 12_587_008, (n32, n16)
     assert len(bks) >= 4 and all(n * 4 <= 26e6 + 4 * 2048 * 4096 for _, n in bks), bks
+
+
+def _rccl_worker(rank, world, port, out_dir):
+    """World 1 over RCCL ("nccl", bench.py's init form): GradAllReduce and Zero2AdamW with
+    collectives_at_world1, so the armed bucket path launches real async RCCL all-reduce /
+    reduce-scatter / all-gather work on RCCL's stream and the optimizer takes the stream waits."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(os.path.dirname(here), "video-generation-for-human-avatars_amd"),
+              os.path.join(os.path.dirname(here), "oracle"), here):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+    try:
+        from safetensors.torch import load_file
+        from model_utils import build_full_model, build_model
+        from ltx_amd.config import TrainConfig
+        from ltx_amd.scheduler import RectifiedFlowScheduler
+        from ltx_amd.training import GradAllReduce, train_step
+        from ltx_amd.zero import Zero2AdamW
+        import ltx_oracle as O
+        dev = "cuda:0"
+        res = {"backend": dist.get_backend()}
+        x = torch.arange(1024, dtype=torch.float32, device=dev)
+        dist.all_reduce(x)
+        res["allreduce_ok"] = bool(torch.equal(x, torch.arange(1024, dtype=torch.float32, device=dev)))
+        tc = TrainConfig(checkpoint_path="-", gradient_accumulation_steps=2)
+
+        def micro_steps(model, shapes, prompt, pmask, g, red=None, arm_last=False, n=2):
+            for step in range(n):
+                if arm_last and step == n - 1:
+                    red.arm()
+                batch = {k: torch.randn(shapes[k], generator=g).to(dev, torch.bfloat16) for k in shapes}
+                B, C, F_, H_, W_ = batch["latents"].shape
+                t = torch.rand(B, generator=g).to(dev)
+                noise = torch.randn((B, F_ * H_ * W_, C), generator=g).to(dev, torch.bfloat16)
+                train_step(model, batch, RectifiedFlowScheduler(), model.patchifier, tc, prompt, pmask,
+                           t=t, noise=noise)
+
+        # LoRA mode: GradAllReduce armed (buckets launched from the backward hooks) / post hoc /
+        # no reducer at all
+        d = load_file(os.path.join(GOLD, "tiny_train_step.safetensors"))
+        with open(os.path.join(GOLD, "tiny_train_step.json")) as f:
+            meta = json.load(f)
+        shapes = {k: d["in." + k].shape for k in ("latents", "ref_image_latents", "pose_latents")}
+        prompt, pmask = d["in.prompt_embeds"].to(dev), d["in.prompt_attention_mask"].to(dev)
+        for mode in ("overlap", "posthoc", "local"):
+            params = {k[2:]: v for k, v in d.items() if k.startswith("w.")}
+            model = build_model(meta["config"], params, meta["lora_rank"], device=dev)
+            red = None
+            if mode != "local":
+                red = GradAllReduce([p for p in model.parameters() if p.requires_grad], bucket_mb=0.05,
+                                    order=model.grad_ready_order()).install(model)
+                red.collectives_at_world1 = True
+                red.zero_grad()
+            micro_steps(model, shapes, prompt, pmask, torch.Generator().manual_seed(500), red,
+                        arm_last=(mode == "overlap"))
+            if red is not None:
+                if mode == "overlap":
+                    res["launched_in_backward"] = red._launched
+                    res["n_buckets"] = len(red.buckets)
+                red()
+                red.uninstall()
+            torch.cuda.synchronize()
+            res[mode] = {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()
+                         if p.requires_grad}
+            del model, red
+        # full mode: Zero2AdamW, two optimizer steps with RCCL reduce-scatter / all-reduce /
+        # all-gather (armed on the last micro-step) vs the same optimizer without collectives
+        d = load_file(os.path.join(GOLD, "tiny_full_step.safetensors"))
+        with open(os.path.join(GOLD, "tiny_full_step.json")) as f:
+            meta = json.load(f)
+        shapes = {k: d["in." + k].shape for k in ("latents", "ref_image_latents", "pose_latents")}
+        prompt, pmask = d["in.prompt_embeds"].to(dev), d["in.prompt_attention_mask"].to(dev)
+        for mode in ("zero_rccl", "zero_local"):
+            params = O.make_params(meta["config"], meta["param_seed"], lora_rank=0, requires_grad=False)
+            model = build_full_model(meta["config"], params, device=dev)
+            opt = Zero2AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3,
+                             bucket_elems=20_000, order=model.grad_ready_order()).install(model)
+            opt.collectives_at_world1 = mode == "zero_rccl"
+            g = torch.Generator().manual_seed(700)
+            for _ in range(2):
+                micro_steps(model, shapes, prompt, pmask, g, opt, arm_last=True)
+                if mode == "zero_rccl":
+                    res.setdefault("zero_launched_in_backward", []).append(opt._launched)
+                opt.step()
+                opt.zero_grad()
+            torch.cuda.synchronize()
+            res[mode] = opt.flat_param.detach().cpu().clone()
+            res[mode + "_buckets"] = len(opt.buckets)
+            opt.uninstall()
+            del model, opt
+        torch.save(res, os.path.join(out_dir, "rccl.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_armed_buckets_bitwise():
+    """RCCL runs on gfx950 through this code: a world-1 "nccl" process group (the bench's init
+    form), GradAllReduce's armed buckets (async all_reduce launched from the backward hooks) and
+    Zero2AdamW's async reduce-scatter / sumsq all-reduce / all-gather forced at world 1; every
+    result bitwise equal to the same step without collectives (a world-1 SUM is the identity),
+    so the stream waits (training.py GradAllReduce.__call__, zero.py _reduce_scatter) order RCCL's
+    stream correctly against the optimizer kernels."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.start_processes(_rccl_worker, args=(1, _port(), td), nprocs=1, start_method="spawn", join=True)
+        res = torch.load(os.path.join(td, "rccl.pt"), weights_only=True)
+    assert res["backend"] == "nccl" and res["allreduce_ok"]
+    assert res["n_buckets"] > 2 and res["launched_in_backward"] >= 1, res.get("launched_in_backward")
+    for n, gl in res["local"].items():
+        assert torch.equal(res["overlap"][n], gl), n
+        assert torch.equal(res["posthoc"][n], gl), n
+    assert res["zero_rccl_buckets"] > 2
+    assert all(k >= 1 for k in res["zero_launched_in_backward"]), res["zero_launched_in_backward"]
+    assert torch.equal(res["zero_rccl"], res["zero_local"])

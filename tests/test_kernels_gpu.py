@@ -218,16 +218,29 @@ def test_attention_fwd_bwd(B, H, Nq, Nk, d, masked):
     assert rel(dq32, qf.grad) <= 1.25 * rel(qh.grad, qf.grad) + 1e-3
 
 
-@pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),  # no key bias
-                                                      (8, 4, 1792, 256, True, True),    # bench's attn2
-                                                      (8, 4, 1792, 128, True, True),    # 128 keys: QS
-                                                      (1, 2, 300, 200, True, False),    # ragged both
-                                                      (2, 2, 64, 33, False, False),     # < 2 waves
-                                                      (1, 32, 7488, 256, True, False)])  # config X, B=1:
-def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):        # query split
+def _cross_bias(Nk, Bk, valid):
+    """Caption-style key bias bf16(-10000) on padded keys: `valid` None -> Nk - 5 - 3b keys of batch
+    b kept; an int -> the first `valid` keys (the bench's prompt keeps 16 of 256)."""
+    if valid is None:
+        keep = torch.arange(Nk, device=DEV)[None, :] < (Nk - 5 - 3 * torch.arange(Bk, device=DEV)[:, None])
+    else:
+        keep = (torch.arange(Nk, device=DEV)[None, :] < valid).expand(Bk, Nk)
+    return ((1 - keep.to(torch.bfloat16)) * -10000.0).float().contiguous()
+
+
+@pytest.mark.parametrize("B,H,Nq,Nk,masked,shared,valid", [
+    (2, 4, 1792, 256, False, False, None),  # no key bias
+    (8, 4, 1792, 256, True, True, None),    # shared prompt, bias
+    (8, 32, 1792, 256, True, True, 16),     # the bench's attn2: config A, 16 valid keys, shared
+    (8, 4, 1792, 128, True, True, None),    # 128 keys: QS
+    (1, 2, 300, 200, True, False, None),    # ragged both
+    (2, 2, 64, 33, False, False, None),     # < 2 waves
+    (1, 32, 7488, 256, True, False, None)])  # config X, B=1: query split
+def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, valid, monkeypatch):
     """Nk <= 256 runs the one-pass backward (attn_bwd1_kernel: S/dP once, dQ from the dS image);
-    LTX_ATTN_BWD1=0 forces the split dQ + dK/dV kernels. Both against fp32 autograd: rel-Frobenius
-    <= 2e-2, and the one-pass error within 1.25x the split path's (+1e-3)."""
+    LTX_ATTN_BWD1=0 forces the split dQ + dK/dV kernels. SURVEY 8(c)(4) noise criterion for dQ,
+    dK and dV of both paths against fp32 autograd: rel-Frobenius within 1.25x torch's own bf16
+    SDPA backward error (+1e-3); the one-pass error also within 1.25x the split path's (+1e-3)."""
     from ltx_amd import ops
     d = 64
     scale = d ** -0.5
@@ -236,34 +249,33 @@ def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):     
     k = g(Bk * Nk, H * d, seed=12)
     v = g(Bk * Nk, H * d, seed=13)
     do = g(B * Nq, H * d, seed=14)
-    bias = None
-    if masked:
-        keep = torch.arange(Nk, device=DEV)[None, :] < (Nk - 5 - 3 * torch.arange(Bk, device=DEV)[:, None])
-        bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
+    bias = _cross_bias(Nk, Bk, valid) if masked else None
     o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias, kv_shared=shared)
     kx = k.repeat(B, 1) if shared else k
     vx = v.repeat(B, 1) if shared else v
     bx = (bias.repeat(B, 1) if shared else bias) if bias is not None else None
     qf, kf, vf = (t.float().clone().requires_grad_(True) for t in (q, kx, vx))
     _sdpa_ref(qf, kf, vf, B, H, d, bx).backward(do.float())
+    qh, kh, vh = (t.clone().requires_grad_(True) for t in (q, kx, vx))  # torch's bf16 SDPA backward
+    _sdpa_ref(qh, kh, vh, B, H, d, bx, dtype=torch.bfloat16).backward(do)
+
+    def batch_summed(t):  # shared keys: the per-batch rows of one key summed, then re-expanded
+        return t.float().view(B, Nk, H * d).sum(0).repeat(B, 1) if shared else t
+    refs32 = (qf.grad, batch_summed(kf.grad), batch_summed(vf.grad))
+    refs16 = (qh.grad, batch_summed(kh.grad), batch_summed(vh.grad))
+    e16 = tuple(rel(a, b_) for a, b_ in zip(refs16, refs32))
     errs = {}
     for mode in ("1", "0"):
         monkeypatch.setenv("LTX_ATTN_BWD1", mode)
         for f32 in (False, True):
             dq, dk, dv = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, dq_f32=f32,
                                       kv_shared=shared)
-            if shared:
-                dk = dk.float().view(B, Nk, H * d).sum(0).repeat(B, 1)
-                dv = dv.float().view(B, Nk, H * d).sum(0).repeat(B, 1)
-                kg = kf.grad.view(B, Nk, H * d).sum(0).repeat(B, 1)
-                vg = vf.grad.view(B, Nk, H * d).sum(0).repeat(B, 1)
-            else:
-                kg, vg = kf.grad, vf.grad
-            errs[mode, f32] = (rel(dq, qf.grad), rel(dk, kg), rel(dv, vg))
+            errs[mode, f32] = tuple(rel(a, b_) for a, b_ in zip((dq, batch_summed(dk), batch_summed(dv)),
+                                                                refs32))
     for f32 in (False, True):
-        for e1, e0 in zip(errs["1", f32], errs["0", f32]):
-            assert e1 < 2e-2 and e0 < 2e-2, errs
-            assert e1 <= 1.25 * e0 + 1e-3, errs
+        for e1, e0, er in zip(errs["1", f32], errs["0", f32], e16):
+            assert e1 <= 1.25 * er + 1e-3 and e0 <= 1.25 * er + 1e-3, (errs, e16)
+            assert e1 <= 1.25 * e0 + 1e-3, (errs, e16)
     if H * B < 128 and (Nq + 63) // 64 >= 4:  # the one-pass kernel split over the queries
         monkeypatch.setenv("LTX_ATTN_BWD1", "1")
         ops._gemm_workspace(q.device)  # its dK / dV partials live in the stream's workspace
@@ -282,28 +294,27 @@ def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):     
             outs[qs] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias,
                                     kv_shared=shared)
         assert torch.equal(outs["1"][0], outs["0"][0])
-        for a, b_ in zip(outs["1"][1:], outs["0"][1:]):
-            assert rel(a, b_) < 1e-2
+        for a, r32, er in zip(outs["1"][1:], refs32[1:], e16[1:]):  # QS dK / dV: noise criterion
+            assert rel(batch_summed(a), r32) <= 1.25 * er + 1e-3, (rel(batch_summed(a), r32), er)
 
 
-@pytest.mark.parametrize("B,H,Nq,Nk,masked,shared", [(2, 4, 1792, 256, False, False),
-                                                      (8, 4, 1792, 256, True, True),
-                                                      (1, 2, 300, 200, True, False),
-                                                      (2, 2, 40, 64, False, False),
-                                                      (1, 32, 7488, 256, True, False)])  # 8 WGs per head
-def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
+@pytest.mark.parametrize("B,H,Nq,Nk,masked,shared,valid", [(2, 4, 1792, 256, False, False, None),
+                                                            (8, 4, 1792, 256, True, True, None),
+                                                            (8, 32, 1792, 256, True, True, 16),  # bench attn2
+                                                            (1, 2, 300, 200, True, False, None),
+                                                            (2, 2, 40, 64, False, False, None),
+                                                            (1, 32, 7488, 256, True, False, None)])  # 8 WGs/head
+def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, valid, monkeypatch):
     """Nk <= 256 runs attn_fwd1_kernel (K/V staged once per (batch, head)); its per-slice
-    arithmetic is the tiled kernel's, so O and lse are bitwise those of LTX_ATTN_FWD1=0."""
+    arithmetic is the tiled kernel's, so O and lse are bitwise those of LTX_ATTN_FWD1=0; O against
+    fp32 SDPA by the SURVEY 8(c)(4) noise criterion (within 1.25x torch's bf16 SDPA error + 1e-3)."""
     from ltx_amd import ops
     d = 64
     Bk = 1 if shared else B
     q = g(B * Nq, H * d, seed=21)
     k = g(Bk * Nk, H * d, seed=22)
     v = g(Bk * Nk, H * d, seed=23)
-    bias = None
-    if masked:
-        keep = torch.arange(Nk, device=DEV)[None, :] < (Nk - 5 - 3 * torch.arange(Bk, device=DEV)[:, None])
-        bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
+    bias = _cross_bias(Nk, Bk, valid) if masked else None
     monkeypatch.setenv("LTX_ATTN_FWD1", "1")
     o1, l1 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)
     monkeypatch.setenv("LTX_ATTN_FWD1", "0")
@@ -314,7 +325,9 @@ def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, monkeypatch):
     kx = k.repeat(B, 1) if shared else k
     vx = v.repeat(B, 1) if shared else v
     bx = (bias.repeat(B, 1) if shared else bias) if bias is not None else None
-    assert rel(o1, _sdpa_ref(q, kx, vx, B, H, d, bx)) < 1e-2
+    ref = _sdpa_ref(q, kx, vx, B, H, d, bx)
+    ref16 = _sdpa_ref(q, kx, vx, B, H, d, bx, dtype=torch.bfloat16)
+    assert rel(o1, ref) <= 1.25 * rel(ref16, ref) + 1e-3, (rel(o1, ref), rel(ref16, ref))
 
 
 @pytest.mark.parametrize("B,H,Nq,Nk,valid,shared", [(8, 4, 1792, 256, 16, True),   # bench's attn2
@@ -360,7 +373,9 @@ def test_attention_padding_blocks_skipped_exactly(B, H, Nq, Nk, valid, shared, m
     kx = k.repeat(B, 1) if shared else k
     vx = v.repeat(B, 1) if shared else v
     bx = bias.repeat(B, 1) if shared else bias
-    assert rel(o, _sdpa_ref(q, kx, vx, B, H, d, bx)) < 1e-2
+    ref = _sdpa_ref(q, kx, vx, B, H, d, bx)
+    ref16 = _sdpa_ref(q, kx, vx, B, H, d, bx, dtype=torch.bfloat16)
+    assert rel(o, ref) <= 1.25 * rel(ref16, ref) + 1e-3, (rel(o, ref), rel(ref16, ref))
     pad = ~(keep.repeat(B, 1) if shared else keep).reshape(-1)
     assert float(dk.view(-1, H * d)[pad].abs().max()) == 0.0
     assert float(dv.view(-1, H * d)[pad].abs().max()) == 0.0
@@ -374,7 +389,9 @@ def test_attention_strided_fused_qkv():
     qkv = g(B * N, 3 * D, seed=5)
     q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
     o, _ = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5)
-    assert rel(o, _sdpa_ref(q, k, v, B, H, d)) < 1e-2
+    ref = _sdpa_ref(q, k, v, B, H, d)
+    ref16 = _sdpa_ref(q, k, v, B, H, d, dtype=torch.bfloat16)
+    assert rel(o, ref) <= 1.25 * rel(ref16, ref) + 1e-3, (rel(o, ref), rel(ref16, ref))
 
 
 # ---------------------------------------------------------------------------------- normalisation

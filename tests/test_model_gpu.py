@@ -264,3 +264,42 @@ def test_ffgate_fused_handoff_matches_separate_gate_mul(monkeypatch):
     assert g1.keys() == g0.keys()
     for k in g1:
         assert rel(g1[k], g0[k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("layers,B", [(28, 1), (2, 8)])
+def test_train_steps_are_bitwise_reproducible(layers, B):
+    """Two identical models fed identical inputs give bitwise-identical losses, gradients and
+    updated weights over 3 optimizer steps (no atomics, fixed-order partial sums everywhere; no
+    kernel may read uninitialised memory into a result). The second model is built while the
+    first one's buffers are still alive, so stale allocator contents differ between the runs."""
+    from ltx_amd.training import FusedAdamW
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    from model_utils import build_step, synth_inputs
+    cfg = dict(OURS_TRANSFORMER_CONFIG, num_layers=layers)
+    params = O.make_params(cfg, 43, lora_rank=16, requires_grad=False)
+    runs = []
+    keep = []
+    for run in range(2):
+        model = build_model(cfg, params, 16, device=DEV)
+        model.train()
+        opt = FusedAdamW([p for p in model.parameters() if p.requires_grad], lr=1e-4)
+        losses, grads = [], []
+        for step in range(3):
+            d = synth_inputs(B, 7, 16, 16, 256, 16, seed=7000 + step)
+            losses.append(build_step(model, d))
+            grads.append({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.requires_grad})
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+        weights = {n: p.detach().clone() for n, p in model.named_parameters() if p.requires_grad}
+        runs.append((losses, grads, weights))
+        keep.append((model, opt))
+        # poison freed memory between the runs: the caching allocator hands it back to run 2
+        junk = torch.empty(1 << 30, dtype=torch.uint8, device=DEV).fill_(0xFF)
+        del junk
+    (l0, g0, w0), (l1, g1, w1) = runs
+    assert l0 == l1, (l0, l1)
+    for s in range(3):
+        for n in g0[s]:
+            assert torch.equal(g0[s][n], g1[s][n]), (s, n)
+    for n in w0:
+        assert torch.equal(w0[n], w1[n]), n

@@ -618,29 +618,45 @@ def ext_body4(MF, T2):
 
 
 def main():
-    out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(
-        os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-        "video-generation-for-human-avatars_amd", "csrc", "gemm_ring_body.h")
-    txt = ["// GENERATED by tools/gen_gemm_ring.py -- do not edit by hand.",
-           "// The hand-scheduled K loop of gemm_ring_kernel (gemm_ring.h): body3() and ext_body2() of the",
-           "// generator (body() / body2() are the measured-and-not-adopted variants, DESIGN.md §7).",
-           "#pragma once", ""]
+    """Writes the default header (body3 / ext_body2: what every build compiles) and, with
+    --x3 PATH, the measured-and-not-adopted three-X-stage bodies (body4 / ext_body4) into their own
+    header for the `make x3` A/B build only (gemm_ring.h includes it under LTX_RING_X3)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    args = sys.argv[1:]
+    x3 = None
+    if "--x3" in args:
+        i = args.index("--x3")
+        x3 = args[i + 1] if i + 1 < len(args) else os.path.join(root, "tools", "experiments",
+                                                                 "gemm_ring_body_x3.h")
+        del args[i:i + 2]
+    out = args[0] if args else os.path.join(root, "video-generation-for-human-avatars_amd", "csrc",
+                                            "gemm_ring_body.h")
 
-    def define(name, lines):
+    def header(what):
+        return ["// GENERATED by tools/gen_gemm_ring.py -- do not edit by hand.", what, "#pragma once", ""]
+
+    def define(txt, name, lines):
         txt.append(f"#define {name} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n")
+    txt = header("// The hand-scheduled K loop of gemm_ring_kernel (gemm_ring.h): body3() and ext_body2() of the\n"
+                 "// generator (body() / body2() / body4() are measured-and-not-adopted variants, DESIGN.md §7).")
     for MF in (7, 8):
-        define(f"LTX_RING_BODY_MF{MF}", body3(MF))
         main = body3(MF)
+        define(txt, f"LTX_RING_BODY_MF{MF}", main)
         assert main[-3:] == ["s_mov_b32 m0, %[keep]", "s_nop 15", "s_nop 15"]
         for T2 in (1, 2):
-            define(f"LTX_RING_BODY_EXT{T2}_MF{MF}", main[:-3] + ext_body2(MF, T2))
-        main4 = body4(MF)
-        define(f"LTX_RING4_BODY_MF{MF}", main4)
-        assert main4[-3:] == ["s_mov_b32 m0, %[keep]", "s_nop 15", "s_nop 15"]
-        for T2 in (1, 2):
-            define(f"LTX_RING4_BODY_EXT{T2}_MF{MF}", main4[:-3] + ext_body4(MF, T2))
+            define(txt, f"LTX_RING_BODY_EXT{T2}_MF{MF}", main[:-3] + ext_body2(MF, T2))
     open(out, "w").write("\n".join(txt))
     print(out)
+    if x3:
+        txt = header("// The three-X-stage K loop (body4 / ext_body4): `make x3` only (gemm_ring.h LTX_RING_X3).")
+        for MF in (7, 8):
+            main4 = body4(MF)
+            assert main4[-3:] == ["s_mov_b32 m0, %[keep]", "s_nop 15", "s_nop 15"]
+            define(txt, f"LTX_RING4_BODY_MF{MF}", main4)
+            for T2 in (1, 2):
+                define(txt, f"LTX_RING4_BODY_EXT{T2}_MF{MF}", main4[:-3] + ext_body4(MF, T2))
+        open(x3, "w").write("\n".join(txt))
+        print(x3)
 
 
 if __name__ == "__main__":

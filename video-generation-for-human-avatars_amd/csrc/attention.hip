@@ -1131,27 +1131,6 @@ static int launch_fwd(AttnParams p, hipStream_t s) {
   return LTX_OK;
 }
 
-// LTX_ATTN_BWD_CONC=1: the pipelined dQ and dK/dV kernels run concurrently (read per call)
-static bool bwd_conc_flag() {
-  const char* e = std::getenv("LTX_ATTN_BWD_CONC");
-  return e && e[0] == '1';
-}
-struct BwdSide {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-static BwdSide& bwd_side() {  // one per process (one GPU per process), created on first use
-  static BwdSide side = [] {
-    BwdSide b;
-    if (hipStreamCreateWithFlags(&b.s, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&b.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&b.join, hipEventDisableTiming) != hipSuccess)
-      b.s = nullptr;
-    return b;
-  }();
-  return side;
-}
-
 template <int HD>
 static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s) {
   if (!delta_ready) {
@@ -1169,11 +1148,12 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
       p.qsplit = 1;
       const int ntot = (p.Nq + 63) / 64;
       if (p.H * p.B < 128 && ntot >= 4 && qsplit_flag()) {
-        int S = std::min(ntot / 2, (256 + p.H * p.B - 1) / (p.H * p.B));
+        // S depends on the shape alone, so the dK / dV summation order does too; when its partials
+        // do not fit the stream's workspace the unsplit kernel runs instead (never a smaller S)
+        const int S = std::min(ntot / 2, (256 + p.H * p.B - 1) / (p.H * p.B));
         size_t ws = 0;
         float* part = stream_workspace(s, &ws);
-        while (S > 1 && (size_t)2 * S * p.B * p.Nk * p.H * HD * sizeof(float) > ws) --S;
-        if (S > 1) {
+        if (S > 1 && part != nullptr && (size_t)2 * S * p.B * p.Nk * p.H * HD * sizeof(float) <= ws) {
           p.qsplit = S;
           p.part = part;
           const dim3 gs((unsigned)p.H, (unsigned)p.B, (unsigned)S);
@@ -1204,21 +1184,6 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   if constexpr (HD == 64) k8 = waves8_flag(1);
   dim3 gk((unsigned)(k8 ? (p.Nk + 255) / 256 : (p.Nk + 127) / 128), (unsigned)p.H, (unsigned)p.B);
   if (HD == 64 && !k8 && dkdv_pipe_enabled()) {
-    if (!needs_bias(p) && dq_pipe_enabled() && bwd_conc_flag()) {
-      // dQ on the library's side stream beside dK/dV on the caller's: the two kernels read the
-      // same inputs and write disjoint outputs; each one's last partial round of workgroups then
-      // shares the chip with the other's instead of leaving CUs idle
-      BwdSide& side = bwd_side();
-      if (side.s == nullptr) return fail(LTX_ERR_UNSUPPORTED, "attn_bwd: no side stream for LTX_ATTN_BWD_CONC");
-      (void)hipEventRecord(side.fork, s);
-      (void)hipStreamWaitEvent(side.s, side.fork, 0);
-      int rc = launch_dq_pipe(p, side.s);
-      if (rc != LTX_OK) return rc;
-      rc = launch_dkdv_pipe(p, s);
-      (void)hipEventRecord(side.join, side.s);
-      (void)hipStreamWaitEvent(s, side.join, 0);
-      return rc;
-    }
     if (needs_bias(p)) {
       hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
       LTX_LAUNCH_CHECK();

@@ -320,19 +320,22 @@ __global__ __launch_bounds__(64 * NW) void lora_rows_kernel(const bf16_t* __rest
   }
 }
 
-// dw(n,j) (+)= alpha * sum_m y[m,n] * u[m,j]   (f32 atomics across row splits)
+// dw(n,j) (+)= alpha * sum_m y[m,n] * u[m,j], deterministic: with one row split each block owns
+// its outputs (a plain store, or load + add + store when accumulating); with S > 1 row splits each
+// block stores its partial to part[g][split][r*N] and lora_wgrad_finish_kernel sums the S partials
+// in split order (no atomics: the result does not depend on the order blocks finish).
 // Computed as C[j][n] += U^T[j][m] . Y[m][n] on v_mfma_f32_16x16x4_f32: per 4 rows a lane loads
 // u[m][j] (4 B) and 8 consecutive columns of y (one 16-B load; 16 lanes = 128 columns, 256 B
 // per row), and MFMA t (t = 0..7) takes element t, so its output column c stands for
 // n0 + 8c + t (a fixed permutation undone at the store). Block = 8 waves on the same 128
-// columns, interleaved row quads; the wave partials are reduced through LDS, then one atomic
-// per output element and block.
+// columns, interleaved row quads; the wave partials are reduced through LDS in wave order.
 template <int R>
 __global__ __launch_bounds__(512) void lora_wgrad_kernel(const bf16_t* __restrict__ y, int64_t ldy,
                                                          const float* __restrict__ u, int64_t ldu,
                                                          float* __restrict__ dw, int64_t on, int64_t oj, int M,
                                                          int N, int rows_per_split, float alpha, int64_t gy,
-                                                         int64_t gu, int64_t gd) {
+                                                         int64_t gu, int64_t gd, float* __restrict__ part,
+                                                         int accumulate) {
   // group blockIdx.z: one launch for several adapters (element strides; 0 = shared operand)
   y += blockIdx.z * gy;
   u += blockIdx.z * gu;
@@ -397,9 +400,34 @@ __global__ __launch_bounds__(512) void lora_wgrad_kernel(const bf16_t* __restric
 #pragma unroll
       for (int w = 0; w < NW; ++w) sum += red[w][j][c];
       const float v = sum * alpha;
-      atomicAdd(dw + (int64_t)n * on + (int64_t)j * oj, v);
+      const int64_t o = (int64_t)n * on + (int64_t)j * oj;
+      if (part != nullptr) {  // this split's partial, in the output's own layout
+        part[((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * ((int64_t)N * R) + o] = v;
+      } else {
+        float* d = dw + o;
+        *d = accumulate ? *d + v : v;
+      }
     }
   }
+}
+
+// dw[g][e] (+)= sum over the S row splits, in split order, of part[g][s][e]; 4 elements per thread
+__global__ void lora_wgrad_finish_kernel(const float* __restrict__ part, float* __restrict__ dw, int64_t n_per_group,
+                                         int S, int64_t gd, int accumulate) {
+  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= n_per_group) return;
+  const float* p = part + (int64_t)blockIdx.y * S * n_per_group + i4;
+  f32x4 acc = *(const f32x4*)p;
+  for (int s = 1; s < S; ++s) {
+    const f32x4 v = *(const f32x4*)(p + (int64_t)s * n_per_group);
+    acc[0] += v[0]; acc[1] += v[1]; acc[2] += v[2]; acc[3] += v[3];
+  }
+  float* d = dw + (int64_t)blockIdx.y * gd + i4;
+  if (accumulate) {
+    const f32x4 o = *(const f32x4*)d;
+    acc[0] = o[0] + acc[0]; acc[1] = o[1] + acc[1]; acc[2] = o[2] + acc[2]; acc[3] = o[3] + acc[3];
+  }
+  *(f32x4*)d = acc;
 }
 
 // 3-term bf16 split of an f32 [R, r] operand for the K-extension LoRA fusion: with
@@ -542,20 +570,11 @@ extern "C" int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u
   LTX_CHECK_ARG(groups >= 1 && groups <= 65535 && gy % 8 == 0 && (groups == 1 || gd >= N * r),
                 "lora_wgrad: groups in [1, 65535], 16-B aligned y groups, disjoint outputs");
   hipStream_t s = (hipStream_t)stream;
-  if (!accumulate) {
-    const bool dense = groups == 1 || gd == N * r;  // one memset covers a dense stack
-    for (int64_t g = 0; g < (dense ? 1 : groups); ++g) {
-      hipError_t e = hipMemsetAsync(dw + g * gd, 0, (size_t)N * r * (dense ? groups : 1) * sizeof(float), s);
-      if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
-    }
-  }
-  // ~512 blocks of 128 columns x >= 512 rows (8 waves x 4-quad steps): enough waves to stream
-  // y while keeping the f32 atomics (128 * r per block) small
-  const int nb = (int)((N + 127) / 128);
+  // ~512 blocks of 128 columns x >= 512 rows (8 waves x 4-quad steps): enough waves to stream y.
   // ~512 blocks (two per CU): 17.9 us vs 20.0 us with 256 at M = 14336, N = 2048, r = 16. Splits
   // of >= 256 rows in multiples of 32 (a wave's row quads stay aligned; the last 128-row step of a
-  // split may be partial): M = 14336 -> 32 splits of 448 rows = exactly 512 blocks (with 512-row
-  // multiples it was 28 x 16 = 448 blocks, 1.75 per CU)
+  // split may be partial): M = 14336 -> 32 splits of 448 rows = exactly 512 blocks
+  const int nb = (int)((N + 127) / 128);
   const int target = 512;
   int splits = (int)((target + nb * groups - 1) / (nb * groups));
   const int max_splits = (int)((M + 255) / 256);
@@ -564,14 +583,35 @@ extern "C" int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u
   int rps = (int)((M + splits - 1) / splits);
   rps = (rps + 31) / 32 * 32;
   splits = (int)((M + rps - 1) / rps);
+  // S > 1: per-split partials in the stream's workspace (caller-owned, stream-ordered), summed in
+  // order by the finish kernel; with no room for them, one split (each block owns its outputs)
+  float* part = nullptr;
+  if (splits > 1) {
+    size_t ws = 0;
+    float* w = stream_workspace(s, &ws);
+    const bool aligned = ((uintptr_t)dw % 16) == 0 && (N * r) % 4 == 0 && (groups == 1 || gd % 4 == 0);
+    if (w != nullptr && aligned && (size_t)groups * splits * N * r * sizeof(float) <= ws) {
+      part = w;
+    } else {
+      splits = 1;
+      rps = (int)M;
+    }
+  }
   const dim3 grid((unsigned)nb, (unsigned)splits, (unsigned)groups);
+  const int acc = accumulate ? 1 : 0;
   switch (r) {
-    case 8: hipLaunchKernelGGL(lora_wgrad_kernel<8>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd); break;
-    case 16: hipLaunchKernelGGL(lora_wgrad_kernel<16>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd); break;
-    case 32: hipLaunchKernelGGL(lora_wgrad_kernel<32>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd); break;
+    case 8: hipLaunchKernelGGL(lora_wgrad_kernel<8>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd, part, acc); break;
+    case 16: hipLaunchKernelGGL(lora_wgrad_kernel<16>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd, part, acc); break;
+    case 32: hipLaunchKernelGGL(lora_wgrad_kernel<32>, grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu, dw, on, oj, (int)M, (int)N, rps, alpha, gy, gu, gd, part, acc); break;
     default: return fail(LTX_ERR_BAD_ARG, "lora_wgrad: rank must be 8, 16 or 32");
   }
   LTX_LAUNCH_CHECK();
+  if (part != nullptr) {
+    const int64_t npg = N * r;
+    const dim3 gf((unsigned)((npg / 4 + 255) / 256), (unsigned)groups);
+    hipLaunchKernelGGL(lora_wgrad_finish_kernel, gf, dim3(256), 0, s, part, dw, npg, splits, gd, acc);
+    LTX_LAUNCH_CHECK();
+  }
   return LTX_OK;
 }
 

@@ -1,7 +1,7 @@
 // Flat-buffer kernels of the ZeRO-2 optimizer (ltx_amd/zero.py; BASELINE config Z:
 // configs/ds_config_zero2.json -- stage 2, bf16, reduce_scatter, gradient_clipping 1.0):
 // bf16 <-> f32 casts of the contiguous grad / param buffers, the shard's sum of squares for the
-// global-norm clip (f64 atomics into one scalar per call site), and the clip coefficient applied
+// global-norm clip (f64 per-block partials in the stream's workspace, added in block order), and the clip coefficient applied
 // from device memory so no host sync sits between the collectives and the AdamW kernel.
 #include <cmath>
 
@@ -28,7 +28,10 @@ __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restr
     dst[i] = f2bf(src[i]);
 }
 
-__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ out) {
+// part != null: block b stores its sum to part[b] and sumsq_finish_kernel adds the partials in block
+// order (deterministic); part == null (no workspace): one f64 atomic per block
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x, int64_t n, double* __restrict__ out,
+                                                    double* __restrict__ part) {
   double s = 0.0;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double v = x[i];
@@ -39,7 +42,26 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
   __shared__ double red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) {
+    const double b = red[0] + red[1] + red[2] + red[3];
+    if (part != nullptr) part[blockIdx.x] = b;
+    else atomicAdd(out, b);
+  }
+}
+
+__global__ __launch_bounds__(256) void sumsq_finish_kernel(const double* __restrict__ part, int nparts,
+                                                           double* __restrict__ out) {
+  // 256 threads sum strided partials in a fixed order, then a fixed-shape tree
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out += red[0];
 }
 
 // coef = inv_world * min(1, max_norm / (sqrt(sumsq) * inv_world + 1e-6)) (max_norm <= 0: no clip)
@@ -93,8 +115,16 @@ int ltx_sumsq_f32(const float* x, int64_t n, double* out, int accumulate, void* 
     if (e != hipSuccess) return fail((int)e, hipGetErrorString(e));
   }
   if (n == 0) return LTX_OK;
-  hipLaunchKernelGGL(sumsq_kernel, dim3(grid_cap(n)), dim3(256), 0, s, x, n, out);
+  const unsigned g = grid_cap(n);
+  size_t ws = 0;
+  double* part = (double*)stream_workspace(s, &ws);
+  if (part == nullptr || ws < g * sizeof(double)) part = nullptr;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(g), dim3(256), 0, s, x, n, out, part);
   LTX_LAUNCH_CHECK();
+  if (part != nullptr) {
+    hipLaunchKernelGGL(sumsq_finish_kernel, dim3(1), dim3(256), 0, s, (const double*)part, (int)g, out);
+    LTX_LAUNCH_CHECK();
+  }
   return LTX_OK;
 }
 

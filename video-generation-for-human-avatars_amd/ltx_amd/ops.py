@@ -320,6 +320,8 @@ def qk_norm_fwd_grouped(x, x_gs, weights, eps=1e-5):
     rows = x.shape[0]
     _need(weights, BF16, "weights")
     assert weights.is_contiguous() and x.shape[1] >= D and x_gs >= 0
+    # group G-1's last row must lie inside x (the C entry checks alignment, not extents)
+    assert x.numel() >= (G - 1) * x_gs + (rows - 1) * x.stride(0) + D, "x too small for G groups"
     y = torch.empty(G, rows, D, dtype=BF16, device=x.device)
     rstd = torch.empty(G, rows, dtype=F32, device=x.device)
     call("ltx_qk_norm_fwd_grouped", _p(x), _rows(x, "x"), x_gs, _p(y), D, rows * D, _p(weights), D,
@@ -337,6 +339,9 @@ def qk_norm_bwd_grouped(dy, dy_gs, x, x_gs, weights, rstd, dx, dx_gs):
     assert weights.is_contiguous() and rstd.is_contiguous()
     assert rstd.shape == (G, rows) and dx.shape[0] == rows
     assert dy.numel() >= (G - 1) * dy_gs + (rows - 1) * dy.stride(0) + D
+    assert x.numel() >= (G - 1) * x_gs + (rows - 1) * x.stride(0) + D, "x too small for G groups"
+    assert dx.numel() >= (G - 1) * dx_gs + (rows - 1) * dx.stride(0) + D, "dx too small for G groups"
+    assert min(dy_gs, x_gs, dx_gs) >= 0
     call("ltx_qk_norm_bwd_grouped", _p(dy), _rows(dy, "dy"), dy_gs, _p(x), _rows(x, "x"), x_gs,
          _p(weights), D, _p(rstd), rows, _p(dx), _rows(dx, "dx"), dx_gs, rows, G, D, _s())
     return dx

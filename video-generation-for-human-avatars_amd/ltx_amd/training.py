@@ -180,6 +180,13 @@ class OverlapHooks:
     launches as soon as all of its grads are final, always in index order on every rank (a ready
     bucket waits for its predecessors), so the collectives match across ranks."""
 
+    # test-only: launch the collectives (and take their stream waits) even at world size 1, so a
+    # one-GPU box exercises RCCL's own stream and the armed bucket path (tests/test_dp_gpu.py)
+    collectives_at_world1 = False
+
+    def _collectives_on(self):
+        return self._world() > 1 or self.collectives_at_world1
+
     def _init_hooks(self):
         self._armed = False
         self._pending = None   # per bucket: grads not yet final
@@ -237,7 +244,7 @@ class OverlapHooks:
 
     def arm(self):
         """The next backward is the last of the accumulation cycle: reduce during it."""
-        if self._world() == 1:
+        if not self._collectives_on():
             return
         self._prepare_arm()
         self._armed = True
@@ -357,7 +364,7 @@ class GradAllReduce(OverlapHooks):
     @torch.no_grad()
     def __call__(self):
         world = self._world()
-        if world == 1:
+        if not self._collectives_on():
             self._armed = False
             return
         if not self._armed:

@@ -923,6 +923,10 @@ class _TextStack:
             else:
                 ops.qk_norm_bwd_grouped(self.dk2_all.view(n * Lt, D), Lt * D, self.kv, 2 * D, self.knw,
                                         self.rk2_all, dkv, 2 * D)
+            # the stacked per-batch gradients are consumed: release them now (the [B*Lt, 2nD]
+            # stack is ~470 MB at config A) instead of holding them until the next micro-step
+            self.dkvb = None
+            self.dk2_all = None
         # lora_B grads: dB_j = s * dY_j^T . u_j  (dY of adapter j = columns j*D .. of dkv)
         dB = ops.lora_wgrad(dkv[:, :D], self.u[:, :r], alpha=s, groups=2 * n,
                             group_strides=(D, r))

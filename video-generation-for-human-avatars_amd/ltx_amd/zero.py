@@ -127,6 +127,7 @@ class Zero2AdamW(OverlapHooks):
         call("ltx_cast_f32_bf16", _p(src), _p(dst), src.numel(), _s())
 
     def _sumsq(self, x, out):
+        ops._gemm_workspace(x.device)  # the per-block partials (deterministic order) live there
         call("ltx_sumsq_f32", _p(x), x.numel(), _p(out), 0, _s())
 
     def _clip_scale(self, x, sumsq, coef):
@@ -150,7 +151,7 @@ class Zero2AdamW(OverlapHooks):
         else:
             inp = self.flat_grad[lo:hi]
             out = self.gshard16[out_lo:out_hi]
-        if self.world == 1:
+        if not self._collectives_on():
             out.copy_(inp)
         else:
             self._works.append(dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM,
@@ -176,14 +177,14 @@ class Zero2AdamW(OverlapHooks):
         self.step_count += 1
         self._reduce_scatter()
         self._sumsq(self.gshard, self.sumsq)
-        if self.world > 1 and self.clip > 0:
+        if self._collectives_on() and self.clip > 0:
             dist.all_reduce(self.sumsq, op=dist.ReduceOp.SUM, group=self.group)
         self._clip_scale(self.gshard, self.sumsq, self.coef)
         self._adamw(self.master, self.gshard, self.exp_avg, self.exp_avg_sq, self.step_count)
         for b in self.buckets:
             mine = self._my_slice(self.flat_param, b)
             self._cast_to_bf16(self.master[b["soff"]:b["soff"] + b["s"]], mine)
-            if self.world > 1:
+            if self._collectives_on():
                 dist.all_gather_into_tensor(self.flat_param[b["start"]:b["start"] + b["n"]], mine,
                                             group=self.group)
         ops.bump_weight_generation()  # weights changed in place: rebuild packed copies
