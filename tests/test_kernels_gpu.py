@@ -811,3 +811,27 @@ def test_fused_adamw_multi_tensor_bitwise():
     for x, y in zip(a, b):
         assert torch.equal(x, y)
 
+
+
+@pytest.mark.parametrize("B,H,Nq,Nk", [(2, 3, 1000, 768), (1, 4, 1792, 1792), (1, 2, 70, 320), (1, 2, 50, 512),
+                                       (2, 2, 320, 1792), (1, 3, 64, 256), (1, 2, 129, 192)])
+def test_attention_dkdv_w1_matches_pipe_bitwise(B, H, Nq, Nk, monkeypatch):
+    """attn_dkdv_w1_kernel (one wave per SIMD, 64 keys per wave, hand-scheduled loop from
+    tools/gen_attn_bwd.py; LTX_ATTN_DKDV_W1=1) keeps attn_dkdv_pipe_kernel's arithmetic and
+    accumulation order: dK and dV bitwise equal, including ragged query tiles (rows past Nq read as
+    zeros through the shrinking buffer descriptor) and key blocks past Nk; dQ is the same kernel."""
+    from ltx_amd import ops
+    d = 64
+    scale = d ** -0.5
+    qkv = g(B * Nq, 3 * H * d, seed=71)
+    q = qkv[:, :H * d]
+    k = g(B * Nk, H * d, seed=72)
+    v = g(B * Nk, H * d, seed=73)
+    do = g(B * Nq, H * d, seed=74)
+    o, lse = ops.attn_fwd(q, k, v, B, H, d, scale)
+    outs = {}
+    for w1 in ("0", "1"):
+        monkeypatch.setenv("LTX_ATTN_DKDV_W1", w1)
+        outs[w1] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale)
+    for a, b_ in zip(outs["1"], outs["0"]):
+        assert torch.equal(a, b_)

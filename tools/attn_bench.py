@@ -12,6 +12,7 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--which", default="self,cross")
 ap.add_argument("--env-ab", default=None, help="NAME: time each kernel with NAME=0 and NAME=1, interleaved")
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--env-vals", default="0,1", help="the values --env-ab cycles through")
 args = ap.parse_args()
 B, N, L, H, d = 8, 1792, 256, 32, 64
 D = H * d
@@ -50,7 +51,7 @@ for which in args.which.split(","):
     prod = 2.0 * B * H * N * Nk * d
     if args.env_ab:
         for rd in range(args.rounds):
-            for val in ("0", "1"):
+            for val in args.env_vals.split(","):
                 os.environ[args.env_ab] = val
                 tf, tb = timeit(fwd, args.iters), timeit(bwd, args.iters)
                 print(f"{which} {args.env_ab}={val} round {rd}: fwd {tf * 1e3:.1f} us  bwd {tb * 1e3:.1f} us", flush=True)

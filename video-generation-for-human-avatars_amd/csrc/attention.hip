@@ -1194,6 +1194,7 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
       hipLaunchKernelGGL((attn_q_kernel<HD, 1, false>), gq, dim3(ATT_THREADS), 0, s, p);
       LTX_LAUNCH_CHECK();
     }
+    if (!needs_bias(p) && dkdv_w1_enabled()) return launch_dkdv_w1(p, s);
     return launch_dkdv_pipe(p, s);
   }
   if (needs_bias(p)) {

@@ -20,6 +20,10 @@
 #include <cstdlib>
 
 #include "attention_common.h"
+#include "attn_bwd_body.h"
+#ifdef LTX_DKDV_DIAG  // `make diag`: timing-only variants of the loop (tools/gen_attn_bwd.py --diag)
+#include "attn_bwd_body_diag.h"
+#endif
 #include "ltx_hip.h"
 
 namespace ltx {
@@ -322,6 +326,136 @@ __global__ __launch_bounds__(256, 2) void attn_dkdv_pipe_kernel(const AttnParams
                      lane);
   store_rows_lds<HD>(smem + wave * 8192 + 4096, dva, 1.0f, p.dv + (int64_t)b * p.Nk * p.lddv + hh * HD, p.lddv, k0,
                      nk, lane);
+}
+
+// =============================================================================================
+// dK / dV at ONE wave per SIMD (self-attention shapes: no key bias, head dim 64): 4 waves x 64 keys
+// (two 32-key tiles per wave) = 256 keys per workgroup, the whole loop one hand-scheduled asm
+// statement (attn_bwd_body.h, generated by tools/gen_attn_bwd.py: register map, schedule and the
+// out-of-range handling of ragged query tiles are described there). Same arithmetic, fragment
+// layouts and MFMA accumulation order as attn_dkdv_pipe_kernel: dK / dV are bitwise equal to it.
+// =============================================================================================
+namespace {
+constexpr int W1_KEYS = 256;  // keys per workgroup
+}
+
+__device__ __forceinline__ uint64_t srd_half(const u32x4& d, int hi) {
+  return hi ? ((uint64_t)d[3] << 32 | d[2]) : ((uint64_t)d[1] << 32 | d[0]);
+}
+
+// raw buffer descriptor over [base, base + bytes): loads past `bytes` return zeros
+__device__ __forceinline__ u32x4 raw_srd(const void* base, uint64_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  u32x4 d;
+  d[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  d[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32) & 0xffffu);  // stride 0
+  d[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0xffffffffull ? 0xffffffffull : bytes));
+  d[3] = 0x00020000u;
+  return d;
+}
+
+template <int V>
+__global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p) {
+  constexpr int HD = PHD;
+  // the ring (3 x LTX_DKDV_W1_BUF B); after the loop the epilogue's dK / dV staging
+  __shared__ __attribute__((aligned(16))) char smem[LTX_DKDV_W1_NBUF * LTX_DKDV_W1_BUF];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int k0 = bx * W1_KEYS + wave * 64;
+  // K / V rows of the lane's key in each 32-key tile (clamped: keys past Nk are computed, not stored)
+  const bf16_t* kp[2];
+  const bf16_t* vp[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int kc = min(k0 + kt * 32 + (lane & 31), p.Nk - 1);
+    kp[kt] = p.k + ((int64_t)b * p.kvb + kc) * p.ldk + hh * HD + 8 * h;
+    vp[kt] = p.v + ((int64_t)b * p.kvb + kc) * p.ldv + hh * HD + 8 * h;
+  }
+  // buffer descriptors of this (batch, head)'s Q and dO columns and its lse / delta rows; each spans
+  // exactly the valid rows, so a query tile's rows past Nq read as zeros
+  const bf16_t* qbase = p.q + (int64_t)b * p.Nq * p.ldq + hh * HD;
+  const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
+  const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
+  const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
+  const u32x4 srdq = raw_srd(qbase, ((uint64_t)(p.Nq - 1) * p.ldq + HD) * 2);
+  const u32x4 srdo = raw_srd(obase, ((uint64_t)(p.Nq - 1) * p.lddo + HD) * 2);
+  // wave 0: lse, wave 1: delta; waves 2 and 3 repeat them into a dummy slot (every wave issues the
+  // same five DMA instructions per tile, so one counted wait fits all)
+  const u32x4 srds = raw_srd((wave & 1) ? (const void*)dbase : (const void*)lbase, (uint64_t)p.Nq * 4);
+  const uint32_t wst = __builtin_amdgcn_readfirstlane(2 * P_TILE + (wave < 2 ? wave * P_STAT : 2 * P_STAT));
+  // per-lane DMA offsets inside a tile: piece 2w + i = rows 8 (2w + i) .. + 7, chunk swizzled
+  uint32_t vq[2], vo[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
+    vq[i] = (uint32_t)(row * p.ldq + c * 8) * 2;
+    vo[i] = (uint32_t)(row * p.lddo + c * 8) * 2;
+  }
+  const uint32_t vl = (uint32_t)lane * 4, vs = (uint32_t)(16 * h);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
+  const uint32_t wq = __builtin_amdgcn_readfirstlane(wave * 2048);
+  const uint32_t qstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldq * 2));
+  const uint32_t ostep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.lddo * 2));
+  const uint32_t iters = __builtin_amdgcn_readfirstlane((uint32_t)((p.Nq + 63) / 64 - 1));
+  const float c2 = p.scale * LOG2E;
+  f32x16 dv00 = {}, dv01 = {}, dv10 = {}, dv11 = {}, dk00 = {}, dk01 = {}, dk10 = {}, dk11 = {};
+#define LTX_W1_OPERANDS                                                                                      \
+  : "+a"(dv00), "+a"(dv01), "+a"(dv10), "+a"(dv11), "+a"(dk00), "+a"(dk01), "+a"(dk10), "+a"(dk11) \
+               : [sq0] "s"(srd_half(srdq, 0)), [sq1] "s"(srd_half(srdq, 1)), [so0] "s"(srd_half(srdo, 0)), \
+                 [so1] "s"(srd_half(srdo, 1)), [ss0] "s"(srd_half(srds, 0)), [ss1] "s"(srd_half(srds, 1)), \
+                 [qstep] "s"(qstep), [ostep] "s"(ostep), [lds0] "s"(lds0), [wq] "s"(wq), [wst] "s"(wst), \
+                 [iters] "s"(iters), [c2] "s"(c2), [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]), \
+                 [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]), [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]), \
+                 [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]), [vs] "v"(vs), [vq0] "v"(vq[0]), \
+                 [vq1] "v"(vq[1]), [vo0] "v"(vo[0]), [vo1] "v"(vo[1]), [vl] "v"(vl), [kp0] "v"(kp[0]), \
+                 [kp1] "v"(kp[1]), [vp0] "v"(vp[0]), [vp1] "v"(vp[1]) \
+               : "memory", "scc", "vcc", LTX_DKDV_W1_CLOBBERS
+  if constexpr (V == 0) asm volatile(LTX_DKDV_W1_BODY LTX_W1_OPERANDS);
+#ifdef LTX_DKDV_DIAG
+  if constexpr (V == 1) asm volatile(LTX_DKDV_W1_BODY_V1 LTX_W1_OPERANDS);
+  if constexpr (V == 2) asm volatile(LTX_DKDV_W1_BODY_V2 LTX_W1_OPERANDS);
+  if constexpr (V == 3) asm volatile(LTX_DKDV_W1_BODY_V3 LTX_W1_OPERANDS);
+  if constexpr (V == 4) asm volatile(LTX_DKDV_W1_BODY_V4 LTX_W1_OPERANDS);
+#endif
+#undef LTX_W1_OPERANDS
+  // dK, dV as whole rows through wave-private LDS slots (every DMA retired inside the statement)
+  __syncthreads();
+  const f32x16 dk[2][2] = {{dk00, dk01}, {dk10, dk11}};
+  const f32x16 dvv[2][2] = {{dv00, dv01}, {dv10, dv11}};
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int kb = k0 + kt * 32, nk = min(32, p.Nk - kb);
+    if (nk > 0) {
+      store_rows_lds<HD>(smem + wave * 8192, dk[kt], p.scale, p.dk + (int64_t)b * p.Nk * p.lddk + hh * HD, p.lddk,
+                         kb, nk, lane);
+      store_rows_lds<HD>(smem + wave * 8192 + 4096, dvv[kt], 1.0f, p.dv + (int64_t)b * p.Nk * p.lddv + hh * HD,
+                         p.lddv, kb, nk, lane);
+    }
+  }
+}
+
+static int dkdv_w1_mode() {  // LTX_ATTN_DKDV_W1 (read per call): 1 the one-wave-per-SIMD kernel,
+  const char* e = std::getenv("LTX_ATTN_DKDV_W1");  // 2..5 its timing-only variants (`make diag` builds)
+  return e ? std::atoi(e) : 0;
+}
+bool dkdv_w1_enabled() { return dkdv_w1_mode() != 0; }
+
+int launch_dkdv_w1(const AttnParams& p, hipStream_t s) {
+  const dim3 g((unsigned)((p.Nk + W1_KEYS - 1) / W1_KEYS), (unsigned)p.H, (unsigned)p.B);
+  switch (dkdv_w1_mode()) {
+#ifdef LTX_DKDV_DIAG
+    case 2: hipLaunchKernelGGL(attn_dkdv_w1_kernel<1>, g, dim3(256), 0, s, p); break;
+    case 3: hipLaunchKernelGGL(attn_dkdv_w1_kernel<2>, g, dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(attn_dkdv_w1_kernel<3>, g, dim3(256), 0, s, p); break;
+    case 5: hipLaunchKernelGGL(attn_dkdv_w1_kernel<4>, g, dim3(256), 0, s, p); break;
+#endif
+    default: hipLaunchKernelGGL(attn_dkdv_w1_kernel<0>, g, dim3(256), 0, s, p); break;
+  }
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
 }
 
 // =============================================================================================
