@@ -2,18 +2,26 @@
 attn_dkdv_w1_kernel (attention_pipe.hip), the dK / dV half of F.scaled_dot_product_attention's
 backward (attention.py:1057-1064) for head dim 64 and no key bias, as ONE inline-asm statement.
 
-Why: at head dim 64 the softmax VALU of a score block costs as many
-issue cycles as its MFMAs, and at two waves per SIMD (attn_dkdv_pipe_kernel, 248 VGPRs) the two
+Why: at head dim 64 the softmax VALU of a score block costs about as
+many issue cycles as its MFMAs, and at two waves per SIMD (attn_dkdv_pipe_kernel, 248 VGPRs) the two
 streams' MFMAs and VALU compete for one issue port (MFMA-busy 0.53). Here one wave per SIMD owns 64
 keys (two 32-key tiles, so every Q / dO fragment read from LDS feeds two MFMAs) and every
-instruction is placed: per 32-query half j the wave issues 32 MFMAs -- C(j-1) (dV^T += dO^T.P,
-dK^T += Q^T.dS) and A(j+1) (S^T = K.Q^T, dP'^T = delta - V.dO^T) -- and each MFMA gap carries
-B(j)'s softmax work (phase 1: 2 x (v_fma, v_exp); phase 2: 2 x v_mul + 2 x v_cvt_pk) plus at most
-two LDS reads: 1 MFMA + <= 6 fillers per gap, at most 2 transcendental.
+instruction is placed. Per 32-query half j the wave issues 32 MFMAs in 32 slots: C(j-1)
+(dV^T += dO^T.P, dK^T += Q^T.dS) in slots 0-15 and A(j+1) (S^T = K.Q^T, dP'^T = delta - V.dO^T) in
+slots 16-31. The softmax of half j, B(j), is a stream of 32 elements (the lane's 2 x 16 scores)
+that runs LAG slots behind the half's start, one element per slot: element e has its exponent
+argument formed in slot e + LAG - 1 (v_fma), its exponential in e + LAG, its dS product in
+e + LAG + 2 (v_mul), its P / dS bf16 packs (pairs) in e + LAG + 2 / e + LAG + 3, so each MFMA gap
+carries one fma, one exp, one mul, about one cvt and one LDS read -- the same filler mix in every
+slot (the phase-split schedule, two exponentials per gap in one phase, measured ~50 cycles per MFMA
+in that phase with in-kernel stamps). The stream ends in slot 42 = slot 10 of the next half, and
+the C MFMAs run in pack order (ss, kt, d), so no pack is rewritten before the C stage of the
+previous half has read it and every pack is written before the next C stage reads it.
 
 Arithmetic and accumulation order are those of attn_dkdv_pipe_kernel (same fragment layouts, MFMA
 chains in the same k order, delta as dP's initial accumulator with V negated), so dK / dV are
-bitwise equal to it (tests/test_kernels_gpu.py).
+bitwise equal to it (tests/test_kernels_gpu.py). LDS reads carry tags; the generator inserts the
+counted s_waitcnt lgkmcnt(N) in front of the first consumer of a read (LDS returns in order).
 
 Tiles of 64 queries (Q | dO | lse | delta) arrive by LDS-DMA into a 3-buffer ring, one tile ahead,
 one barrier per tile. Rows past Nq are out of range of the tile's buffer descriptor (the base
@@ -22,17 +30,18 @@ their dO and delta rows are 0, so they add exactly 0 to dV (dO^T.P) and dS = -P 
 
 Registers (hard-coded, clobbered; the dV / dK accumulators are the statement's "+a" operands
 %0..%7, which hipcc must place in a0..a127):
-  v[0:127]   S / dP' tiles: set s (0, 1), tile T (0 S kt0, 1 dP kt0, 2 S kt1, 3 dP kt1) at 64 s + 16 T
-  v[128:143] P packs  PB[kt][ss] (B operands of dV) at 128 + 8 kt + 4 ss
-  v[144:159] dS packs SB[kt][ss] at 144 + 8 kt + 4 ss
-  v[160:175] lse tuple of the half being exponentiated (accumulator row order)
-  v[176:191] delta tuple of the half being multiplied (dP chains' initial accumulator)
-  v[192:204] LDS addresses: RA[ks] row fragments (A's tile), ST statistics (A's tile), TC / TN[2d+i]
+  v[0:63]    S tiles: set s (0, 1), key tile kt at 32 s + 16 kt; v[66:129] the dP' tiles likewise
+             at 66 + 32 s + 16 kt (two banks away from their S)
+  v[130:145] P packs  PB[kt][ss] (B operands of dV) at 130 + 8 kt + 4 ss
+  v[146:161] dS packs SB[kt][ss] at 146 + 8 kt + 4 ss
+  v[162:177], v[210:225]  lse tuples of even / odd halves (accumulator row order)
+  v[178:193] delta tuple of the half whose A stage runs (dP chains' initial accumulator)
+  v[194:206] LDS addresses: RA[ks] row fragments (A's tile), ST statistics (A's tile), TC / TN[2d+i]
              transposed fragments of the current / next tile
   a[128:159] K fragments KF[kt][ks], a[160:191] -V fragments, a[192:223] QA / OA row fragments,
   a[224:255] TO / TQ transposed fragments
   s[80:91]   buffer descriptors of Q, dO and this wave's statistic row (lse or delta)
-  s[92:98]   ring buffer bases B0 / B1 / BD, scratch, loop counter, saved M0
+  s[92:97]   ring buffer bases B0 / B1 / BD, scratch, loop counter, saved M0
 """
 import os
 import sys
@@ -41,26 +50,35 @@ P_TILE = 8192            # one [64][64] bf16 tile
 P_STAT = 256             # 64 f32
 W_BUF = 2 * P_TILE + 3 * P_STAT   # Q | dO | lse | delta | dummy (waves 2, 3)
 NBUF = 3
+LAG = 8                  # B(j)'s element e is exponentiated in slot e + LAG of half j
+
+VARIANT = set()          # diagnostic bodies (--diag): "stamps", "novalu", "nolds", "dmalast", "expfirst"
+
 
 # ---------------------------------------------------------------------------------------- registers
 def SD(s, T):
-    return 64 * s + 16 * T
+    """S tiles (T even) at 32 s + 16 kt, dP' tiles (T odd) at 66 + 32 s + 16 kt: an element's S and dP'
+    registers sit in different VGPR banks (index mod 4), as do S and its lse word, so no v_fma /
+    v_mul reads two operands from one bank"""
+    kt = T // 2
+    return 32 * s + 16 * kt + (66 if T % 2 else 0)
 
 
 def PB(kt, ss):
-    return 128 + 8 * kt + 4 * ss
+    return 130 + 8 * kt + 4 * ss
 
 
 def SB(kt, ss):
-    return 144 + 8 * kt + 4 * ss
+    return 146 + 8 * kt + 4 * ss
 
 
-LSE, DLT = 160, 176
-RA = [192, 193, 194, 195]
-ST = 196
-TC = [197, 198, 199, 200]
-TN = [201, 202, 203, 204]
-VLAST = 206
+LSEB = (162, 210)        # lse tuple of halves j with j % 2 == 0 / 1 (bank of row r: r + 2)
+DLT = 178
+RA = [194, 195, 196, 197]
+ST = 198
+TC = [199, 200, 201, 202]
+TN = [203, 204, 205, 206]
+VLAST = 225
 KF = lambda kt, ks: 128 + 16 * kt + 4 * ks
 VF = lambda kt, ks: 160 + 16 * kt + 4 * ks
 QA = lambda ks: 192 + 4 * ks
@@ -81,107 +99,106 @@ def a_(r, n=1):
     return f"a{r}" if n == 1 else f"a[{r}:{r + n - 1}]"
 
 
-def mfma(dst, A, B, C):
-    return f"v_mfma_f32_32x32x16_bf16 {dst}, {A}, {B}, {C}"
+class I:
+    """one instruction: text, the LDS-read tag it produces (reads) or the tags it needs (consumers)"""
+    def __init__(self, text, makes=None, needs=()):
+        self.text, self.makes, self.needs = text, makes, tuple(needs)
 
 
-# ---------------------------------------------------------------------------------------- pieces
+def mfma(dst, A, B, C, needs=()):
+    return I(f"v_mfma_f32_32x32x16_bf16 {dst}, {A}, {B}, {C}", needs=needs)
+
+
+# ---------------------------------------------------------------------------------------- stages
 def c_mfmas():
-    """C(j-1): dV^T[kt][d] += TO[ss][d] . PB[kt][ss], dK^T[kt][d] += TQ[ss][d] . SB[kt][ss], ss-major
-    (each accumulator takes ss = 0 then ss = 1, as attn_dkdv_pipe_kernel's stage C)"""
+    """C(j-1) in pack order (ss, kt, d): dV^T[kt][d] += TO[ss][d] . PB[kt][ss], then dK^T with TQ, SB;
+    each accumulator takes ss = 0 then ss = 1 (attn_dkdv_pipe_kernel's order)"""
     out = []
     for ss in range(2):
-        for d in range(2):
-            for kt in range(2):
+        for kt in range(2):
+            for d in range(2):
                 dv = "%" + str(ACC[("dv", kt, d)])
                 dk = "%" + str(ACC[("dk", kt, d)])
-                out.append(mfma(dv, a_(TO(ss, d), 4), v(PB(kt, ss), 4), dv))
-                out.append(mfma(dk, a_(TQ(ss, d), 4), v(SB(kt, ss), 4), dk))
+                out.append(mfma(dv, a_(TO(ss, d), 4), v(PB(kt, ss), 4), dv, needs=[f"TO{ss}{d}"]))
+                out.append(mfma(dk, a_(TQ(ss, d), 4), v(SB(kt, ss), 4), dk, needs=[f"TQ{ss}{d}"]))
     return out
 
 
 def a_mfmas(s):
-    """A(j+1) into set s, kt-major: S kt0 (ks 0..3), dP' kt0, S kt1, dP' kt1 (each chain in k order;
-    S starts from 0, dP' from the delta tuple)"""
+    """A(j+1) into set s: the chains S kt0, S kt1, dP' kt0, dP' kt1 interleaved k-step by k-step (each
+    chain in k order; S starts from 0, dP' from the delta tuple)"""
     out = []
-    for kt in range(2):
-        for ks in range(4):
-            dst = v(SD(s, 2 * kt), 16)
-            out.append(mfma(dst, a_(QA(ks), 4), a_(KF(kt, ks), 4), "0" if ks == 0 else dst))
-        for ks in range(4):
-            dst = v(SD(s, 2 * kt + 1), 16)
-            out.append(mfma(dst, a_(OA(ks), 4), a_(VF(kt, ks), 4), v(DLT, 16) if ks == 0 else dst))
+    for ks in range(4):
+        for T in (0, 1):
+            for kt in range(2):
+                dst = v(SD(s, 2 * kt + T), 16)
+                if T == 0:
+                    out.append(mfma(dst, a_(QA(ks), 4), a_(KF(kt, ks), 4), "0" if ks == 0 else dst,
+                                    needs=[f"QA{ks}"]))
+                else:
+                    out.append(mfma(dst, a_(OA(ks), 4), a_(VF(kt, ks), 4), v(DLT, 16) if ks == 0 else dst,
+                                    needs=[f"OA{ks}", "DLT"] if ks == 0 else [f"OA{ks}"]))
     return out
 
 
-def b_phase1(s):
-    """B(j) part 1 on set s: P = exp2(S c2 - lse) in place, 2 elements per slot (16 slots)"""
-    slots = []
-    for m in range(16):
-        ins = []
-        for e in (2 * m, 2 * m + 1):
-            kt, r = e // 16, e % 16
-            sr = SD(s, 2 * kt) + r
-            ins.append(f"v_fma_f32 {v(sr)}, {v(sr)}, %[c2], -{v(LSE + r)}")
-        for e in (2 * m, 2 * m + 1):
-            kt, r = e // 16, e % 16
-            sr = SD(s, 2 * kt) + r
-            ins.append(f"v_exp_f32 {v(sr)}, {v(sr)}")
-        slots.append(ins)
-    return slots
+def b_stream(s, lse):
+    """B(j) on S/dP set s with the lse tuple at `lse`: {slot (0 .. 43, relative to half j): [I]}"""
+    out = {}
 
-
-def b_phase2(s):
-    """B(j) part 2 on set s: dS = -(P dP') in place, then the bf16 packs of P and dS (2 per slot)"""
-    slots = []
-    for m in range(16):
-        kt, r = (2 * m) // 16, (2 * m) % 16
-        s0, d0 = SD(s, 2 * kt) + r, SD(s, 2 * kt + 1) + r
-        ss, i = r // 8, (r % 8) // 2
-        slots.append([f"v_mul_f32 {v(d0)}, -{v(s0)}, {v(d0)}",
-                      f"v_mul_f32 {v(d0 + 1)}, -{v(s0 + 1)}, {v(d0 + 1)}",
-                      f"v_cvt_pk_bf16_f32 {v(PB(kt, ss) + i)}, {v(s0)}, {v(s0 + 1)}",
-                      f"v_cvt_pk_bf16_f32 {v(SB(kt, ss) + i)}, {v(d0)}, {v(d0 + 1)}"])
-    return slots
+    def put(k, ins):
+        out.setdefault(k, []).append(ins)
+    for e in range(32):  # pack order: ss-major, then kt, then the 8 rows of the pack
+        ss, kt, i = e // 16, (e % 16) // 8, e % 8
+        r = 8 * ss + i
+        sr, dr = SD(s, 2 * kt) + r, SD(s, 2 * kt + 1) + r
+        k = e + LAG
+        put(k - 1, I(f"v_fma_f32 {v(sr)}, {v(sr)}, %[c2], -{v(lse + r)}", needs=[f"LSE{lse}"]))
+        put(k, I(f"v_exp_f32 {v(sr)}, {v(sr)}"))
+        put(k + 2, I(f"v_mul_f32 {v(dr)}, -{v(sr)}, {v(dr)}"))
+        if e % 2 == 1:  # the pair (e-1, e): rows r-1, r
+            put(k + 2, I(f"v_cvt_pk_bf16_f32 {v(PB(kt, ss) + i // 2)}, {v(sr - 1)}, {v(sr)}"))
+            put(k + 3, I(f"v_cvt_pk_bf16_f32 {v(SB(kt, ss) + i // 2)}, {v(dr - 1)}, {v(dr)}"))
+    return out
 
 
 def a_reads(u):
-    """A's operands for half u of the tile at RA / ST: Q rows, the delta tuple, dO rows (in the order
-    the kt-major A MFMAs consume them)"""
-    out = [f"ds_read_b128 {a_(QA(ks), 4)}, {v(RA[ks])} offset:{u * 4096}" for ks in range(4)]
-    out += [f"ds_read_b128 {v(DLT + 4 * g, 4)}, {v(ST)} offset:{2 * P_TILE + P_STAT + (u * 32 + 8 * g) * 4}"
-            for g in range(4)]
-    out += [f"ds_read_b128 {a_(OA(ks), 4)}, {v(RA[ks])} offset:{P_TILE + u * 4096}" for ks in range(4)]
+    """A's operands for half u of the tile at RA / ST: Q rows, the delta tuple, dO rows"""
+    out = [I(f"ds_read_b128 {a_(QA(ks), 4)}, {v(RA[ks])} offset:{u * 4096}", makes=f"QA{ks}") for ks in range(4)]
+    out += [I(f"ds_read_b128 {v(DLT + 4 * g, 4)}, {v(ST)} offset:{2 * P_TILE + P_STAT + (u * 32 + 8 * g) * 4}",
+              makes="DLT") for g in range(4)]
+    out += [I(f"ds_read_b128 {a_(OA(ks), 4)}, {v(RA[ks])} offset:{P_TILE + u * 4096}", makes=f"OA{ks}")
+            for ks in range(4)]
     return out
 
 
-def tr_reads(T, u):
-    """C's transposed fragments of half u of the tile at T (TC or TN), in the order C consumes them"""
+def tr_reads(T, u, ss):
+    """C's transposed fragments (k-step ss) of half u of the tile at T (TC or TN)"""
     out = []
-    for ss in range(2):
-        for d in range(2):
-            base = (u * 32 + 16 * ss) * 128
-            for dst, region in ((TO(ss, d), P_TILE), (TQ(ss, d), 0)):
-                out.append(f"ds_read_b64_tr_b16 {a_(dst, 2)}, {v(T[2 * d])} offset:{region + base}")
-                out.append(f"ds_read_b64_tr_b16 {a_(dst + 2, 2)}, {v(T[2 * d + 1])} offset:{region + base}")
+    for d in range(2):
+        base = (u * 32 + 16 * ss) * 128
+        for dst, region, nm in ((TO(ss, d), P_TILE, "TO"), (TQ(ss, d), 0, "TQ")):
+            tag = f"{nm}{ss}{d}"
+            out.append(I(f"ds_read_b64_tr_b16 {a_(dst, 2)}, {v(T[2 * d])} offset:{region + base}", makes=tag))
+            out.append(I(f"ds_read_b64_tr_b16 {a_(dst + 2, 2)}, {v(T[2 * d + 1])} offset:{region + base}",
+                         makes=tag))
     return out
 
 
-def lse_reads(u):
-    return [f"ds_read_b128 {v(LSE + 4 * g, 4)}, {v(ST)} offset:{2 * P_TILE + (u * 32 + 8 * g) * 4}"
-            for g in range(4)]
+def lse_reads(u, lse):
+    return [I(f"ds_read_b128 {v(lse + 4 * g, 4)}, {v(ST)} offset:{2 * P_TILE + (u * 32 + 8 * g) * 4}",
+              makes=f"LSE{lse}") for g in range(4)]
 
 
-def dma_pieces():
-    """this wave's DMA of one tile into buffer BD: Q pieces 2w, 2w+1, dO pieces, its statistic row;
-    (M0 write, load) pairs"""
+def dma_pieces(buf):
+    """this wave's DMA of one tile into the buffer at SGPR `buf` (STMP = buf + this wave's piece
+    offset): Q pieces 2w, 2w+1, dO pieces, its statistic row; (M0 write, load) pairs"""
     out = []
     for i in range(2):
         out.append((f"s_add_u32 m0, s{STMP}, {i * 1024}",
                     f"buffer_load_dwordx4 %[vq{i}], s[{SRDQ}:{SRDQ + 3}], 0 offen lds"))
         out.append((f"s_add_u32 m0, s{STMP}, {P_TILE + i * 1024}",
                     f"buffer_load_dwordx4 %[vo{i}], s[{SRDO}:{SRDO + 3}], 0 offen lds"))
-    out.append((f"s_add_u32 m0, s{SBD}, %[wst]",
+    out.append((f"s_add_u32 m0, s{buf}, %[wst]",
                 f"buffer_load_dword %[vl], s[{SRDS}:{SRDS + 3}], 0 offen lds"))
     return out
 
@@ -212,63 +229,118 @@ def addr_regs(which, sbase):
     return out
 
 
-# ---------------------------------------------------------------------------------------- iteration
-VARIANT = set()  # diagnostic bodies (make diag): "nowait", "novalu", "nolds", "nomfma"
+# ---------------------------------------------------------------------------------------- emission
+class Emitter:
+    """instruction list + the in-order LDS reads still outstanding (tags), for counted waits"""
+    def __init__(self):
+        self.L = []
+        self.pending = []
+
+    def raw(self, text):
+        self.L.append(text)
+
+    def drain(self, text, keep=0):
+        """a wait that leaves at most `keep` LDS reads outstanding (e.g. at a barrier)"""
+        self.L.append(text)
+        self.pending = self.pending[len(self.pending) - keep:] if keep else []
+
+    def put(self, ins):
+        if ins.needs and "nolds" not in VARIANT:
+            last = -1
+            for i, t in enumerate(self.pending):
+                if t in ins.needs:
+                    last = i
+            if last >= 0:
+                n = min(len(self.pending) - 1 - last, 15)
+                self.L.append(f"s_waitcnt lgkmcnt({n})")
+                self.pending = self.pending[len(self.pending) - n:] if n else []
+        if ins.makes is not None:
+            if "nolds" in VARIANT:
+                return
+            self.pending.append(ins.makes)
+        self.L.append(ins.text)
 
 
-def iteration(L, c, b_set, a_set, a_u, rd2, dma=()):
-    """one 32-query half: C(j-1) if c, B(j) on b_set (None: no B), A(j+1) into a_set from half a_u of
-    the tile at RA / ST (None: no A); rd2 = LDS reads for phase 2 (next C's fragments, next lse);
-    dma = (M0, load) pairs placed in phase 2"""
-    a = L.append
-    if "nolds" in VARIANT:
-        rd2 = []
-    # phase 1: C MFMAs (or none) + B exponentials + A's operand reads
-    if "nowait" not in VARIANT:
-        a("s_waitcnt lgkmcnt(0)")
-    cm = c_mfmas() if c and "nomfma" not in VARIANT else []
-    b1 = b_phase1(b_set) if b_set is not None and "novalu" not in VARIANT else [[] for _ in range(16)]
-    rd1 = a_reads(a_u) if a_set is not None and "nolds" not in VARIANT else []
-    for m in range(16):
-        if cm:
-            a(cm[m])
-        L.extend(b1[m])
-        if m < len(rd1):
-            a(rd1[m])
-    # phase 2: A MFMAs (or none) + B products and packs + the next C's / B's operand reads + DMA
-    if "nowait" not in VARIANT:
-        a("s_waitcnt lgkmcnt(0)")
-    am = a_mfmas(a_set) if a_set is not None and "nomfma" not in VARIANT else []
-    b2 = b_phase2(b_set) if b_set is not None and "novalu" not in VARIANT else [[] for _ in range(16)]
-    after = {m: [] for m in range(16)}
-    for k, r in enumerate(rd2):  # reads in slots 0 .. 11 (the last ones land before phase 1)
-        after[(k * 12) // max(len(rd2), 1)].append(r)
+STAMP_BODY = 10  # "stamps": the loop body (counted down from ntiles - 1) whose halves are stamped
+
+
+def stamp(E, k):
+    """s_memtime into s[60 + 2k : 61 + 2k] when the loop counter is STAMP_BODY (diagnostic only)"""
+    if "stamps" not in VARIANT:
+        return
+    for t in (f"s_cmp_eq_u32 s{SITER}, {STAMP_BODY}", f"s_cbranch_scc0 L_st{k}_%=",
+              f"s_memtime s[{60 + 2 * k}:{61 + 2 * k}]", f"L_st{k}_%=:"):
+        E.raw(t)
+
+
+def half(E, c, b_prev, b_cur, a_set, reads, dma=(), extra=None):
+    """one 32-query half j: C(j-1) MFMAs in slots 0-15 if c, A(j+1) MFMAs (into a_set) in 16-31,
+    the tail of B(j-1)'s stream (b_prev: its slots >= 32) and the head of B(j)'s (b_cur), the LDS
+    reads `reads` ({slot: [I]}) and the DMA (M0, load) pairs"""
+    cm = c_mfmas() if c else []
+    am = a_mfmas(a_set) if a_set is not None else []
+    if "novalu" in VARIANT:
+        b_prev, b_cur = {}, {}
+    dslot = {}
     for k, (m0, ld) in enumerate(dma):  # M0 one slot ahead of its load
-        q = 2 + 3 * k
-        after[q - 1].append(m0)
-        after[q].append(ld)
-    for m in range(16):
-        if am:
-            a(am[m])
-        L.extend(b2[m])
-        L.extend(after[m])
+        q = 2 + 6 * k
+        dslot.setdefault(q - 1, []).append(m0)
+        dslot.setdefault(q, []).append(ld)
+    for k in range(32):
+        if k < 16 and cm:
+            E.put(cm[k])
+        if k >= 16 and am:
+            E.put(am[k - 16])
+        valu = b_prev.get(k + 32, []) + b_cur.get(k, [])
+        if "expfirst" in VARIANT:  # timing variant: the exponential first among the VALU fillers
+            valu = [x for x in valu if "v_exp" in x.text] + [x for x in valu if "v_exp" not in x.text]
+        rd = reads.get(k, [])
+        dm = dslot.get(k, []) + (extra.get(k, []) if extra else [])
+        # the gap opens with its LDS read (and LDS-DMA piece): placed after the VALU fillers the same
+        # reads cost ~8 cycles more per gap (stamps: 1472 vs 1216 cycles per half)
+        if "dmalast" in VARIANT:
+            for ins in rd:
+                E.put(ins)
+            for ins in valu:
+                E.put(ins)
+            for t in dm:
+                E.raw(t)
+        else:
+            for t in dm:
+                E.raw(t)
+            for ins in rd + valu:
+                E.put(ins)
 
 
-def c_only(L):
-    """C(J-1) alone (16 MFMAs)"""
-    L.append("s_waitcnt lgkmcnt(0)")
-    L.extend(c_mfmas())
+def read_plan(a_u, tr_T, tr_u, lse_u, lse_buf):
+    """slot -> reads: A's operands (half a_u of the tile at RA / ST) in slots 0-11, C's k-step-0
+    transposed fragments (half tr_u of the tile at tr_T) in 12-19, the next half's lse (lse_u) into
+    lse_buf in 20-23, C's k-step-1 fragments in 24-31 (each set after the previous C stage's last
+    read of those registers)"""
+    plan = {}
+
+    def lay(ins, first):
+        for i, x in enumerate(ins):
+            plan.setdefault(first + i, []).append(x)
+    if a_u is not None:
+        lay(a_reads(a_u), 0)
+    if tr_T is not None:
+        lay(tr_reads(tr_T, tr_u, 0), 12)
+        lay(tr_reads(tr_T, tr_u, 1), 24)
+    if lse_u is not None:
+        lay(lse_reads(lse_u, lse_buf), 20)
+    return plan
 
 
 def body():
-    L = []
-    a = L.append
+    E = Emitter()
+    a = E.raw
     a("s_nop 4")  # SGPR operands fresh from v_readfirstlane -> descriptors / M0
     a(f"s_mov_b32 s{SKEEP}, m0")
     for srd, nm in ((SRDQ, "sq"), (SRDO, "so"), (SRDS, "ss")):  # descriptors as two 64-bit halves each
         a(f"s_mov_b64 s[{srd}:{srd + 1}], %[{nm}0]")
         a(f"s_mov_b64 s[{srd + 2}:{srd + 3}], %[{nm}1]")
-    # ---- prologue: K, V fragments; tiles 0 and 1; A(0); B(0) beside A(1) --------------------------
+    # ---- prologue: K, V fragments; tiles 0 and 1; A(0); half 0 (B(0) head, A(1)) ------------------
     for kt in range(2):
         for ks in range(4):
             a(f"global_load_dwordx4 {a_(KF(kt, ks), 4)}, %[kp{kt}], off offset:{ks * 32}")
@@ -280,31 +352,33 @@ def body():
     a(f"s_add_u32 s{SBD}, %[lds0], {2 * W_BUF}")
     for buf in (SB0, SB1):  # tiles 0 and 1 into buffers 0, 1
         a(f"s_add_u32 s{STMP}, s{buf}, %[wq]")
-        for m0, ld in dma_pieces():
-            a(m0.replace(f"s{SBD}", f"s{buf}"))
+        for m0, ld in dma_pieces(buf):
+            a(m0)
             a("s_nop 0")
             a(ld)
-        L.extend(advance_srds())
+        for t in advance_srds():
+            a(t)
     a("s_waitcnt vmcnt(5)")  # K, V and tile 0 landed (tile 1's five pieces may fly)
     for r in range(32):  # -V (sign flip, exact) into the accumulator file
         a(f"v_xor_b32 {v(r)}, 0x80008000, {v(r)}")
     for r in range(32):
         a(f"v_accvgpr_write_b32 {a_(160 + r)}, {v(r)}")
     a("s_barrier")
-    L.extend(addr_regs("A", f"s{SB0}"))
-    L.extend(addr_regs("TN", f"s{SB0}"))
-    # A(0) into set 0 (tile 0, half 0), lse of B(0)
-    for r in a_reads(0) + lse_reads(0):
-        a(r)
-    a("s_waitcnt lgkmcnt(0)")
+    for t in addr_regs("A", f"s{SB0}") + addr_regs("TN", f"s{SB0}"):
+        a(t)
+    # A(0) into set 0 (tile 0, half 0) and B(0)'s lse
+    for ins in a_reads(0) + lse_reads(0, LSEB[0]):
+        E.put(ins)
     a("s_nop 1")  # accvgpr writes of -V -> MFMA operand
-    L.extend(a_mfmas(0))
-    # B(0) on set 0 beside A(1) into set 1 (tile 0, half 1); phase 2 reads C(0)'s fragments (tile 0
-    # half 0) and B(1)'s lse (tile 0 half 1)
+    for ins in a_mfmas(0):
+        E.put(ins)
     a("s_nop 7")
     a("s_nop 7")
-    a("s_nop 3")  # the last A MFMA's results -> the first exponentials (no C MFMAs in between)
-    iteration(L, False, 0, 1, 1, tr_reads(TN, 0) + lse_reads(1))
+    a("s_nop 3")  # the last A MFMAs' results -> B(0)'s first v_fma (no MFMA in between)
+    # half 0: B(0) head (set 0, even lse), A(1) into set 1 (tile 0 half 1); reads: A(1)'s operands,
+    # C(0)'s fragments (tile 0 half 0 at TN), B(1)'s lse (tile 0 half 1) into the odd tuple
+    b_even, b_odd = b_stream(0, LSEB[0]), b_stream(1, LSEB[1])
+    half(E, False, {}, b_even, 1, read_plan(1, TN, 0, 1, LSEB[1]))
     # ---- steady state: tile t = 0 .. ntiles - 2 ----------------------------------------------------
     # every body opens by rotating (B0, B1, BD) <- (B1, BD, B0); the prologue left B0 = buffer 0,
     # B1 = buffer 1, BD = buffer 2, so pre-rotate backwards to (buffer 2, buffer 0, buffer 1)
@@ -313,46 +387,70 @@ def body():
     a(f"s_mov_b32 s{SB1}, s{SB0}")
     a(f"s_mov_b32 s{SB0}, s{STMP}")
     a(f"s_mov_b32 s{SITER}, %[iters]")
+    if "stamps" in VARIANT:
+        a("s_memtime s[72:73]")
     a(f"s_cmp_eq_u32 s{SITER}, 0")
     a("s_cbranch_scc1 L_dkdv_tail_%=")
     a("L_dkdv_loop_%=:")
-    # tile t+1 (DMA issued one tile ago) landed in every wave, all reads of tile t-1 done
-    a("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    stamp(E, 0)
+    # tile t+1 (DMA issued one tile ago) landed in every wave and every wave's reads of tile t-1 (the
+    # buffer the DMA below overwrites) are done: those ended a half ago, so only the previous half's
+    # last 15 reads (all of tile t, at most 15 in flight) may stay outstanding
+    E.drain("s_waitcnt vmcnt(0) lgkmcnt(15)", keep=15)
     a("s_barrier")
-    # buffers: B0 <- t % 3, B1 <- (t+1) % 3, BD <- (t+2) % 3 (rotate the three bases)
+    stamp(E, 1)
     a(f"s_mov_b32 s{STMP}, s{SB0}")
     a(f"s_mov_b32 s{SB0}, s{SB1}")
     a(f"s_mov_b32 s{SB1}, s{SBD}")
     a(f"s_mov_b32 s{SBD}, s{STMP}")
-    L.extend(addr_regs("A", f"s{SB1}"))
-    L.extend(addr_regs("TC", f"s{SB0}"))
-    L.extend(addr_regs("TN", f"s{SB1}"))
+    for t in addr_regs("A", f"s{SB1}"):  # A's reads start in slot 0; TC / TN are added in slots 1-8
+        a(t)
     a(f"s_add_u32 s{STMP}, s{SBD}, %[wq]")
-    # C(2t), B(2t+1) on set 1, A(2t+2) into set 0 (tile t+1 half 0); phase 2: C(2t+1)'s fragments
-    # (tile t half 1), B(2t+2)'s lse (tile t+1 half 0), the DMA of tile t+2 into BD
-    iteration(L, True, 1, 0, 0, tr_reads(TC, 1) + lse_reads(0), dma_pieces())
-    L.extend(advance_srds())
-    # C(2t+1), B(2t+2) on set 0, A(2t+3) into set 1 (tile t+1 half 1); phase 2: C(2t+2)'s fragments
-    # (tile t+1 half 0), B(2t+3)'s lse (tile t+1 half 1)
-    iteration(L, True, 0, 1, 1, tr_reads(TN, 0) + lse_reads(1))
+    later = {1 + i: [t] for i, t in enumerate(addr_regs("TC", f"s{SB0}") + addr_regs("TN", f"s{SB1}"))}
+    # half 2t+1: C(2t), B(2t) tail, B(2t+1) head (set 1, odd lse), A(2t+2) into set 0 (tile t+1 half
+    # 0); reads: A(2t+2)'s operands, C(2t+1)'s fragments (tile t half 1 at TC), B(2t+2)'s lse (tile
+    # t+1 half 0, even tuple); the DMA of tile t+2 into BD
+    half(E, True, b_even, b_odd, 0, read_plan(0, TC, 1, 0, LSEB[0]), dma_pieces(SBD), extra=later)
+    stamp(E, 2)
+    for t in advance_srds():
+        a(t)
+    # half 2t+2: C(2t+1), B(2t+1) tail, B(2t+2) head (set 0, even lse), A(2t+3) into set 1 (tile
+    # t+1 half 1); reads: A(2t+3)'s operands, C(2t+2)'s fragments (tile t+1 half 0 at TN), B(2t+3)'s
+    # lse (tile t+1 half 1, odd tuple)
+    half(E, True, b_odd, b_even, 1, read_plan(1, TN, 0, 1, LSEB[1]))
+    stamp(E, 3)
     a(f"s_sub_u32 s{SITER}, s{SITER}, 1")
     a(f"s_cmp_eq_u32 s{SITER}, 0")
     a("s_cbranch_scc0 L_dkdv_loop_%=")
     a("L_dkdv_tail_%=:")
-    # ---- last tile T-1: C(J-2), B(J-1) on set 1 (phase 2 reads C(J-1)'s fragments: tile T-1 half 1,
-    # at TN); then C(J-1) ------------------------------------------------------------------------
-    iteration(L, True, 1, None, None, tr_reads(TN, 1))
-    c_only(L)
+    if "stamps" in VARIANT:
+        a("s_memtime s[74:75]")
+    # the reads in flight at the loop exit are those at the end of a loop body, and the prologue's
+    # half 0 leaves the same kinds in the same order (an odd half's A operands, C's fragments, the
+    # odd lse tuple), so the counted waits below hold on both paths
+    # ---- last tile T-1: half J-1 = C(J-2), B(J-2) tail, B(J-1) head (set 1), reads C(J-1)'s
+    # fragments (tile T-1 half 1 at TN); then half J: C(J-1) and B(J-1)'s tail --------------------
+    half(E, True, b_even, b_odd, None, read_plan(None, TN, 1, None, None))
+    half(E, True, b_odd, {}, None, {})
+    if "stamps" in VARIANT:  # every lane of the wave stores the same 8 stamps to %[stp]
+        E.drain("s_waitcnt lgkmcnt(0)")
+        for k in range(8):
+            a(f"v_mov_b32 v0, s{60 + 2 * k}")
+            a(f"v_mov_b32 v1, s{61 + 2 * k}")
+            a(f"global_store_dwordx2 %[stp], v[0:1], off offset:{8 * k}")
+            a("s_nop 1")
     a("s_waitcnt vmcnt(0)")  # no DMA may land in the ring after the statement (epilogue staging)
     a(f"s_mov_b32 m0, s{SKEEP}")
     a("s_nop 15")
     a("s_nop 15")  # the last MFMAs' accumulators -> the compiler's reads after the statement
-    return L
+    return E.L
 
 
-def clobbers():
+def clobbers(diag):
     regs = [f'"v{r}"' for r in range(VLAST + 1)] + [f'"a{r}"' for r in range(128, 256)] + \
            [f'"s{r}"' for r in range(80, 98)]
+    if diag:
+        regs += [f'"s{r}"' for r in range(60, 76)]
     return ", ".join(regs)
 
 
@@ -361,26 +459,26 @@ def main():
     args = [x for x in sys.argv[1:] if not x.startswith("--")]
     out = args[0] if args else os.path.join(
         root, "video-generation-for-human-avatars_amd", "csrc", "attn_bwd_body.h")
-    # the tail after the loop must see TN = tile T-1's buffer: the last body computed TN from B1
-    # (= (T-1) % 3), and with no body at all (T = 1) the prologue's TN (buffer 0) is tile 0's
     diag = "--diag" in sys.argv
-    L = body()
 
     def define(name, lines):
         return f"#define {name} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n"
+    VARIANT.clear()
+    L = body()
     txt = ["// GENERATED by tools/gen_attn_bwd.py -- do not edit by hand.",
            "// The hand-scheduled loop of attn_dkdv_w1_kernel (attention_pipe.hip); see the generator's docstring.",
            "#pragma once", "",
            f"#define LTX_DKDV_W1_BUF {W_BUF}",
            f"#define LTX_DKDV_W1_NBUF {NBUF}",
-           define("LTX_DKDV_W1_BODY", L),
-           "#define LTX_DKDV_W1_CLOBBERS " + clobbers() + "\n"]
-    if diag:  # timing-only bodies (wrong results): what each part of the schedule costs
-        for k, var in enumerate(("nowait", "novalu", "nolds", "nomfma"), 1):
+           define("LTX_DKDV_W1_BODY", L)]
+    if diag:  # timing-only bodies: the loop with phase stamps, without VALU, without LDS reads
+        for k, var in enumerate(("stamps", "stamps+novalu", "stamps+nolds", "stamps+dmalast", "stamps+expfirst"), 1):
             VARIANT.clear()
-            VARIANT.add(var)
+            VARIANT.update(var.split("+"))
             txt.append(define(f"LTX_DKDV_W1_BODY_V{k}", body()))
         VARIANT.clear()
+        txt.append("#undef LTX_DKDV_W1_CLOBBERS")
+    txt.append("#define LTX_DKDV_W1_CLOBBERS " + clobbers(diag) + "\n")
     open(out, "w").write("\n".join(txt))
     print(out, len(L), "lines")
 

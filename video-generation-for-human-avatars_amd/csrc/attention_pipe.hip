@@ -401,6 +401,9 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p
   const uint32_t ostep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.lddo * 2));
   const uint32_t iters = __builtin_amdgcn_readfirstlane((uint32_t)((p.Nq + 63) / 64 - 1));
   const float c2 = p.scale * LOG2E;
+  // diagnostic builds only: this wave's 8 phase stamps (tools/gen_attn_bwd.py "stamps" variant)
+  uint64_t* stp = (uint64_t*)p.part +
+                  ((blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z)) * 4 + wave) * 8;
   f32x16 dv00 = {}, dv01 = {}, dv10 = {}, dv11 = {}, dk00 = {}, dk01 = {}, dk10 = {}, dk11 = {};
 #define LTX_W1_OPERANDS                                                                                      \
   : "+a"(dv00), "+a"(dv01), "+a"(dv10), "+a"(dv11), "+a"(dk00), "+a"(dk01), "+a"(dk10), "+a"(dk11) \
@@ -411,14 +414,15 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p
                  [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]), [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]), \
                  [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]), [vs] "v"(vs), [vq0] "v"(vq[0]), \
                  [vq1] "v"(vq[1]), [vo0] "v"(vo[0]), [vo1] "v"(vo[1]), [vl] "v"(vl), [kp0] "v"(kp[0]), \
-                 [kp1] "v"(kp[1]), [vp0] "v"(vp[0]), [vp1] "v"(vp[1]) \
+                 [kp1] "v"(kp[1]), [vp0] "v"(vp[0]), [vp1] "v"(vp[1]), [stp] "v"(stp) \
                : "memory", "scc", "vcc", LTX_DKDV_W1_CLOBBERS
   if constexpr (V == 0) asm volatile(LTX_DKDV_W1_BODY LTX_W1_OPERANDS);
-#ifdef LTX_DKDV_DIAG
+#ifdef LTX_DKDV_DIAG  // phase stamps into p.part (tools/dkdv_stamps.py): 1 as built, 2 without VALU, 3 without LDS reads
   if constexpr (V == 1) asm volatile(LTX_DKDV_W1_BODY_V1 LTX_W1_OPERANDS);
   if constexpr (V == 2) asm volatile(LTX_DKDV_W1_BODY_V2 LTX_W1_OPERANDS);
   if constexpr (V == 3) asm volatile(LTX_DKDV_W1_BODY_V3 LTX_W1_OPERANDS);
   if constexpr (V == 4) asm volatile(LTX_DKDV_W1_BODY_V4 LTX_W1_OPERANDS);
+  if constexpr (V == 5) asm volatile(LTX_DKDV_W1_BODY_V5 LTX_W1_OPERANDS);
 #endif
 #undef LTX_W1_OPERANDS
   // dK, dV as whole rows through wave-private LDS slots (every DMA retired inside the statement)
@@ -437,23 +441,34 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p
   }
 }
 
-static int dkdv_w1_mode() {  // LTX_ATTN_DKDV_W1 (read per call): 1 the one-wave-per-SIMD kernel,
-  const char* e = std::getenv("LTX_ATTN_DKDV_W1");  // 2..5 its timing-only variants (`make diag` builds)
-  return e ? std::atoi(e) : 0;
+// LTX_ATTN_DKDV_W1 (read per call): unset / 1 the one-wave-per-SIMD kernel, 0 attn_dkdv_pipe_kernel,
+// 12..16 the stamped diagnostic variants (`make diag` builds)
+static int dkdv_w1_mode() {
+  const char* e = std::getenv("LTX_ATTN_DKDV_W1");
+  return e ? std::atoi(e) : 1;
 }
 bool dkdv_w1_enabled() { return dkdv_w1_mode() != 0; }
 
 int launch_dkdv_w1(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nk + W1_KEYS - 1) / W1_KEYS), (unsigned)p.H, (unsigned)p.B);
-  switch (dkdv_w1_mode()) {
+  const int mode = dkdv_w1_mode();
 #ifdef LTX_DKDV_DIAG
-    case 2: hipLaunchKernelGGL(attn_dkdv_w1_kernel<1>, g, dim3(256), 0, s, p); break;
-    case 3: hipLaunchKernelGGL(attn_dkdv_w1_kernel<2>, g, dim3(256), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(attn_dkdv_w1_kernel<3>, g, dim3(256), 0, s, p); break;
-    case 5: hipLaunchKernelGGL(attn_dkdv_w1_kernel<4>, g, dim3(256), 0, s, p); break;
-#endif
-    default: hipLaunchKernelGGL(attn_dkdv_w1_kernel<0>, g, dim3(256), 0, s, p); break;
+  if (mode >= 12 && mode <= 16) {  // phase stamps into the stream's workspace (8 u64 per wave)
+    AttnParams q = p;
+    size_t ws = 0;
+    q.part = stream_workspace(s, &ws);
+    if (q.part == nullptr || ws < (size_t)g.x * g.y * g.z * 4 * 8 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
+    if (mode == 12) hipLaunchKernelGGL(attn_dkdv_w1_kernel<1>, g, dim3(256), 0, s, q);
+    if (mode == 13) hipLaunchKernelGGL(attn_dkdv_w1_kernel<2>, g, dim3(256), 0, s, q);
+    if (mode == 14) hipLaunchKernelGGL(attn_dkdv_w1_kernel<3>, g, dim3(256), 0, s, q);
+    if (mode == 15) hipLaunchKernelGGL(attn_dkdv_w1_kernel<4>, g, dim3(256), 0, s, q);
+    if (mode == 16) hipLaunchKernelGGL(attn_dkdv_w1_kernel<5>, g, dim3(256), 0, s, q);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
   }
+#endif
+  (void)mode;
+  hipLaunchKernelGGL(attn_dkdv_w1_kernel<0>, g, dim3(256), 0, s, p);
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

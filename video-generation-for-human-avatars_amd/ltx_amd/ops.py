@@ -414,7 +414,11 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
         nk = "3" if os.environ.get("LTX_ATTN_DKDV_NBUF", "4")[:1] == "3" else "4"
         dqk = (f"ltx::attn_dq_pipe_kernel<{nq}>" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
                else f"ltx::attn_q_kernel<{d}, 1, {kb}, 4>")
-        kern = f"ltx::attn_dkdv_pipe_kernel<{kb}, {nk}> + {dqk}"
+        if kb == "false" and os.environ.get("LTX_ATTN_DKDV_W1", "1").strip() not in ("0", ""):
+            # one wave per SIMD, hand-scheduled loop (attention_pipe.hip attn_dkdv_w1_kernel)
+            kern = f"ltx::attn_dkdv_w1_kernel<0> + {dqk}"
+        else:
+            kern = f"ltx::attn_dkdv_pipe_kernel<{kb}, {nk}> + {dqk}"
     else:
         kern = f"ltx::attn_dkdv_kernel<{d}, {bias}, 4> + ltx::attn_q_kernel<{d}, 1, {bias}, 4>"
     label = ("attention backward: " + ("" if ready else f"ltx::attn_delta_kernel<{d}> + ") + kern)
