@@ -835,3 +835,27 @@ def test_attention_dkdv_w1_matches_pipe_bitwise(B, H, Nq, Nk, monkeypatch):
         outs[w1] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale)
     for a, b_ in zip(outs["1"], outs["0"]):
         assert torch.equal(a, b_)
+
+
+@pytest.mark.parametrize("B,H,Nq,Nk", [(2, 3, 1000, 768), (1, 4, 1792, 1792), (1, 2, 70, 320), (1, 2, 50, 512),
+                                       (2, 2, 320, 1792), (1, 3, 300, 64), (1, 2, 129, 192)])
+def test_attention_dq_w1_matches_pipe_bitwise(B, H, Nq, Nk, monkeypatch):
+    """attn_dq_w1_kernel (one wave per SIMD, 64 queries per wave, hand-scheduled loop from
+    tools/gen_attn_bwd.py; LTX_ATTN_DQ_W1, default on) keeps attn_dq_pipe_kernel's arithmetic and
+    accumulation order: dQ bitwise equal in bf16 and in f32, ragged query blocks included."""
+    from ltx_amd import ops
+    d = 64
+    scale = d ** -0.5
+    qkv = g(B * Nq, 3 * H * d, seed=81)
+    q = qkv[:, :H * d]
+    k = g(B * Nk, H * d, seed=82)
+    v = g(B * Nk, H * d, seed=83)
+    do = g(B * Nq, H * d, seed=84)
+    o, lse = ops.attn_fwd(q, k, v, B, H, d, scale)
+    for f32 in (False, True):
+        outs = {}
+        for w1 in ("0", "1"):
+            monkeypatch.setenv("LTX_ATTN_DQ_W1", w1)
+            outs[w1] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, dq_f32=f32)
+        for a, b_ in zip(outs["1"], outs["0"]):
+            assert torch.equal(a, b_), f32

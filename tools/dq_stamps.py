@@ -1,0 +1,34 @@
+"""Phase stamps of attn_dq_w1_kernel (diag build: LTX_HIP_LIB=libltxhip_diag.so; LTX_ATTN_DQ_W1 = 12 as
+built, 13 without the softmax VALU): s_memtime at one loop body (counter == STAMP_BODY), medians over
+every wave of config A's self-attention backward."""
+import os, sys
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "video-generation-for-human-avatars_amd"))
+import torch
+from ltx_amd import ops
+
+os.environ["LTX_ATTN_DQ_W1"] = sys.argv[1] if len(sys.argv) > 1 else "12"
+B, N, H, d = 8, 1792, 32, 64
+D = H * d
+torch.manual_seed(0)
+qkv = torch.randn(B * N, 3 * D, device="cuda").bfloat16()
+q, k, v = qkv[:, :D], qkv[:, D:2 * D], qkv[:, 2 * D:]
+o, lse = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5)
+do = torch.randn(B * N, D, device="cuda").bfloat16()
+ws = ops._gemm_workspace(q.device)
+for _ in range(3):
+    ws.zero_()
+    ops.attn_bwd(q, k, v, o, do, lse, B, H, d, d ** -0.5)
+    torch.cuda.synchronize()
+nwg = 7 * H * B
+st = ws.view(torch.int64)[: nwg * 4 * 8].view(nwg * 4, 8).cpu().double()
+names = ["top", "barrier", "half A", "half B"]
+prev = st[:, 0]
+for i in range(1, 4):
+    dlt = st[:, i] - prev
+    print(f"{names[i - 1]:>8} -> {names[i]:<8} median {dlt.median():8.0f}  p10 {dlt.quantile(0.1):8.0f}  p90 {dlt.quantile(0.9):8.0f} cycles")
+    prev = st[:, i]
+body = st[:, 3] - st[:, 0]
+loop = st[:, 7] - st[:, 6]
+print(f"body total median {body.median():.0f} cycles (2 halves, 48 MFMAs: floor 1536)")
+print(f"whole loop median {loop.median():.0f} cycles over {N // 64 - 1} bodies = {loop.median() / (N // 64 - 1):.0f} per body")

@@ -453,6 +453,271 @@ def clobbers(diag):
         regs += [f'"s{r}"' for r in range(60, 76)]
     return ", ".join(regs)
 
+# =============================================================================================
+# dQ at one wave per SIMD (attn_dq_w1_kernel): 4 waves x 64 queries (two 32-query tiles qt per
+# wave), keys in tiles of 64 through the same 3-buffer LDS-DMA ring (K | V), per 32-key half j:
+#   A(j+1): S[qt] = K.Q^T, dP'[qt] = V.dO^T - delta (16 MFMAs; the K / V row fragments feed both qt);
+#   B(j):   dS = exp2(S c2 - lse) dP' -> bf16 packs (32 elements streamed over the half's 24 slots);
+#   C(j-1): dQ^T[qt][d] += K^T[ss][d] . dS[qt][ss] (8 MFMAs, the K^T fragments shared by both qt).
+# A half is 24 slots: C(j-1) in slots 0-7, A(j+1) in 8-23; B(j) runs from slot 1 of its half to slot
+# 4 of the next (element e in slot 3e/4 + 2). Arithmetic and accumulation order of
+# attn_dq_pipe_kernel (lse, delta per lane, -delta as dP's initial accumulator): bitwise equal to it.
+# Keys past Nk read as zeros (shrinking descriptors): their dS is -P delta, but their K rows are 0,
+# so they add exactly 0 to dQ = dS.K.
+# Registers: v[0:63] S tiles (32 s + 16 qt), v[66:129] dP' tiles, v[130:145] dS packs
+# SBF[qt][ss], v[146:177] -delta tuples NDL[qt], v[178:189] LDS addresses RK[ks], TC / TN;
+# a[128:159] Q fragments QF[qt][ks], a[160:191] dO fragments, a[192:223] K / V row fragments
+# KA / VA[ks], a[224:239] K^T fragments KT[ss][d]; the dQ accumulators are operands %0..%3
+# (acc[qt][d] at 2 qt + d, hipcc places them in a0..a127).
+# =============================================================================================
+D_TILE = 8192
+D_BUF = 2 * D_TILE       # K | V
+D_LAG = 2
+
+
+def DSD(s, T):           # T: 0 S qt0, 1 dP qt0, 2 S qt1, 3 dP qt1
+    qt = T // 2
+    return 32 * s + 16 * qt + (66 if T % 2 else 0)
+
+
+DSBF = lambda qt, ss: 130 + 8 * qt + 4 * ss
+DNDL = lambda qt: 146 + 16 * qt
+DRK = [178, 179, 180, 181]
+DTC = [182, 183, 184, 185]
+DTN = [186, 187, 188, 189]
+DVLAST = 189
+DQF = lambda qt, ks: 128 + 16 * qt + 4 * ks
+DOF = lambda qt, ks: 160 + 16 * qt + 4 * ks
+DKA = lambda ks: 192 + 4 * ks
+DVA = lambda ks: 208 + 4 * ks
+DKT = lambda ss, d: 224 + 4 * (2 * ss + d)
+SRDK, SRDV = 80, 84
+
+
+def dq_c_mfmas():
+    """C(j-1) in pack order (ss, qt, d): each accumulator takes ss = 0 then ss = 1"""
+    out = []
+    for ss in range(2):
+        for qt in range(2):
+            for d in range(2):
+                acc = "%" + str(2 * qt + d)
+                out.append(mfma(acc, a_(DKT(ss, d), 4), v(DSBF(qt, ss), 4), acc, needs=[f"KT{ss}{d}"]))
+    return out
+
+
+def dq_a_mfmas(s):
+    """A(j+1) into set s, the chains S qt0, S qt1, dP' qt0, dP' qt1 interleaved k-step by k-step"""
+    out = []
+    for ks in range(4):
+        for T in (0, 1):
+            for qt in range(2):
+                dst = v(DSD(s, 2 * qt + T), 16)
+                if T == 0:
+                    out.append(mfma(dst, a_(DKA(ks), 4), a_(DQF(qt, ks), 4), "0" if ks == 0 else dst,
+                                    needs=[f"KA{ks}"]))
+                else:
+                    out.append(mfma(dst, a_(DVA(ks), 4), a_(DOF(qt, ks), 4), v(DNDL(qt), 16) if ks == 0 else dst,
+                                    needs=[f"VA{ks}"]))
+    return out
+
+
+def dq_b_stream(s):
+    """B(j) on set s: {slot (relative to half j): [I]}, element e (pack order ss, qt, row) in slot
+    3e/4 + D_LAG (its exponent argument one slot earlier, its product two later, pair packs three)"""
+    out = {}
+
+    def put(k, ins):
+        out.setdefault(k, []).append(ins)
+    for e in range(32):
+        ss, qt, i = e // 16, (e % 16) // 8, e % 8
+        r = 8 * ss + i
+        sr, dr = DSD(s, 2 * qt) + r, DSD(s, 2 * qt + 1) + r
+        k = (3 * e) // 4 + D_LAG
+        put(k - 1, I(f"v_fma_f32 {v(sr)}, {v(sr)}, %[c2], %[nl{qt}]"))
+        put(k, I(f"v_exp_f32 {v(sr)}, {v(sr)}"))
+        put(k + 2, I(f"v_mul_f32 {v(dr)}, {v(sr)}, {v(dr)}"))
+        if e % 2 == 1:
+            put(k + 3, I(f"v_cvt_pk_bf16_f32 {v(DSBF(qt, ss) + i // 2)}, {v(dr - 1)}, {v(dr)}"))
+    return out
+
+
+def dq_a_reads(u):
+    out = [I(f"ds_read_b128 {a_(DKA(ks), 4)}, {v(DRK[ks])} offset:{u * 4096}", makes=f"KA{ks}") for ks in range(4)]
+    out += [I(f"ds_read_b128 {a_(DVA(ks), 4)}, {v(DRK[ks])} offset:{D_TILE + u * 4096}", makes=f"VA{ks}")
+            for ks in range(4)]
+    return out
+
+
+def dq_tr_reads(T, u):
+    out = []
+    for ss in range(2):
+        for d in range(2):
+            base = (u * 32 + 16 * ss) * 128
+            tag = f"KT{ss}{d}"
+            out.append(I(f"ds_read_b64_tr_b16 {a_(DKT(ss, d), 2)}, {v(T[2 * d])} offset:{base}", makes=tag))
+            out.append(I(f"ds_read_b64_tr_b16 {a_(DKT(ss, d) + 2, 2)}, {v(T[2 * d + 1])} offset:{base}", makes=tag))
+    return out
+
+
+def dq_dma(buf):
+    out = []
+    for i in range(2):
+        out.append((f"s_add_u32 m0, s{STMP}, {i * 1024}",
+                    f"buffer_load_dwordx4 %[vk{i}], s[{SRDK}:{SRDK + 3}], 0 offen lds"))
+        out.append((f"s_add_u32 m0, s{STMP}, {D_TILE + i * 1024}",
+                    f"buffer_load_dwordx4 %[vv{i}], s[{SRDV}:{SRDV + 3}], 0 offen lds"))
+    return out
+
+
+def dq_advance():
+    out = []
+    for srd, step in ((SRDK, "%[kstep]"), (SRDV, "%[vstep]")):
+        out += [f"s_add_u32 s{srd}, s{srd}, {step}",
+                f"s_addc_u32 s{srd + 1}, s{srd + 1}, 0",
+                f"s_sub_u32 s{srd + 2}, s{srd + 2}, {step}",
+                f"s_cselect_b32 s{srd + 2}, 0, s{srd + 2}"]
+    return out
+
+
+def dq_addr(which, sbase):
+    T = {"A": DRK, "TC": DTC, "TN": DTN}[which]
+    src = [f"%[vr{k}]" for k in range(4)] if which == "A" else [f"%[vt{k}]" for k in range(4)]
+    return [f"v_add_u32 {v(T[k])}, {sbase}, {src[k]}" for k in range(4)]
+
+
+def dq_half(E, c, b_prev, b_cur, a_set, a_u, tr, dma=(), extra=None):
+    """one 32-key half j (24 slots): C(j-1) in slots 0-7 if c, A(j+1) (set a_set, half a_u of the
+    tile at RK) in 8-23; B(j-1)'s tail and B(j)'s head; A's reads in slots 0-7, the next C's K^T
+    fragments (tr = (address regs, half)) in 10-17; DMA pieces and `extra` raw lines"""
+    cm = dq_c_mfmas() if c else []
+    am = dq_a_mfmas(a_set) if a_set is not None else []
+    if "novalu" in VARIANT:
+        b_prev, b_cur = {}, {}
+    reads = {}
+    if a_set is not None:
+        for i, x in enumerate(dq_a_reads(a_u)):
+            reads.setdefault(i, []).append(x)
+    if tr is not None:
+        for i, x in enumerate(dq_tr_reads(*tr)):
+            reads.setdefault(10 + i, []).append(x)
+    dslot = {}
+    for k, (m0, ld) in enumerate(dma):
+        q = 2 + 5 * k
+        dslot.setdefault(q - 1, []).append(m0)
+        dslot.setdefault(q, []).append(ld)
+    for k in range(24):
+        if k < 8 and cm:
+            E.put(cm[k])
+        if k >= 8 and am:
+            E.put(am[k - 8])
+        for t in dslot.get(k, []) + (extra.get(k, []) if extra else []):
+            E.raw(t)
+        for ins in reads.get(k, []) + b_prev.get(k + 24, []) + b_cur.get(k, []):
+            E.put(ins)
+
+
+def dq_body():
+    E = Emitter()
+    a = E.raw
+    a("s_nop 4")
+    a(f"s_mov_b32 s{SKEEP}, m0")
+    for srd, nm in ((SRDK, "sk"), (SRDV, "sv")):
+        a(f"s_mov_b64 s[{srd}:{srd + 1}], %[{nm}0]")
+        a(f"s_mov_b64 s[{srd + 2}:{srd + 3}], %[{nm}1]")
+    for qt in range(2):  # the lane's Q and dO fragments (B operands of S and dP) into AGPRs
+        for ks in range(4):
+            a(f"global_load_dwordx4 {a_(DQF(qt, ks), 4)}, %[qp{qt}], off offset:{ks * 32}")
+            a(f"global_load_dwordx4 {a_(DOF(qt, ks), 4)}, %[op{qt}], off offset:{ks * 32}")
+    for qt in range(2):  # -delta in every register of the dP chains' initial accumulator
+        for r in range(16):
+            a(f"v_mov_b32 {v(DNDL(qt) + r)}, %[nd{qt}]")
+    a(f"s_mov_b32 s{SB0}, %[lds0]")
+    a(f"s_add_u32 s{SB1}, %[lds0], {D_BUF}")
+    a(f"s_add_u32 s{SBD}, %[lds0], {2 * D_BUF}")
+    for buf in (SB0, SB1):  # key tiles 0 and 1
+        a(f"s_add_u32 s{STMP}, s{buf}, %[wq]")
+        for m0, ld in dq_dma(buf):
+            a(m0)
+            a("s_nop 0")
+            a(ld)
+        for t in dq_advance():
+            a(t)
+    a("s_waitcnt vmcnt(4)")  # Q, dO fragments and key tile 0 landed
+    a("s_barrier")
+    for t in dq_addr("A", f"s{SB0}") + dq_addr("TN", f"s{SB0}"):
+        a(t)
+    for ins in dq_a_reads(0):
+        E.put(ins)
+    a("s_nop 1")
+    for ins in dq_a_mfmas(0):
+        E.put(ins)
+    a("s_nop 7")
+    a("s_nop 7")
+    a("s_nop 3")
+    b_even, b_odd = dq_b_stream(0), dq_b_stream(1)
+    dq_half(E, False, {}, b_even, 1, 1, (DTN, 0))
+    a(f"s_mov_b32 s{STMP}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{STMP}")
+    a(f"s_mov_b32 s{SITER}, %[iters]")
+    if "stamps" in VARIANT:
+        a("s_memtime s[72:73]")
+    a(f"s_cmp_eq_u32 s{SITER}, 0")
+    a("s_cbranch_scc1 L_dq_tail_%=")
+    a("L_dq_loop_%=:")
+    stamp(E, 0)
+    E.drain("s_waitcnt vmcnt(0) lgkmcnt(15)", keep=15)
+    a("s_barrier")
+    stamp(E, 1)
+    a(f"s_mov_b32 s{STMP}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{STMP}")
+    for t in dq_addr("A", f"s{SB1}"):
+        a(t)
+    a(f"s_add_u32 s{STMP}, s{SBD}, %[wq]")
+    later = {1 + i: [t] for i, t in enumerate(dq_addr("TC", f"s{SB0}") + dq_addr("TN", f"s{SB1}"))}
+    # half 2t+1: C(2t), B(2t) tail, B(2t+1) head (set 1), A(2t+2) into set 0 (tile t+1 half 0); the
+    # K^T fragments of C(2t+1) (tile t half 1 at TC); the DMA of tile t+2
+    dq_half(E, True, b_even, b_odd, 0, 0, (DTC, 1), dq_dma(SBD), extra=later)
+    stamp(E, 2)
+    for t in dq_advance():
+        a(t)
+    # half 2t+2: C(2t+1), B(2t+1) tail, B(2t+2) head (set 0), A(2t+3) into set 1 (tile t+1 half 1);
+    # the K^T fragments of C(2t+2) (tile t+1 half 0 at TN)
+    dq_half(E, True, b_odd, b_even, 1, 1, (DTN, 0))
+    stamp(E, 3)
+    a(f"s_sub_u32 s{SITER}, s{SITER}, 1")
+    a(f"s_cmp_eq_u32 s{SITER}, 0")
+    a("s_cbranch_scc0 L_dq_loop_%=")
+    a("L_dq_tail_%=:")
+    if "stamps" in VARIANT:
+        a("s_memtime s[74:75]")
+    dq_half(E, True, b_even, b_odd, None, None, (DTN, 1))
+    dq_half(E, True, b_odd, {}, None, None, None)
+    if "stamps" in VARIANT:
+        E.drain("s_waitcnt lgkmcnt(0)")
+        for k in range(8):
+            a(f"v_mov_b32 v0, s{60 + 2 * k}")
+            a(f"v_mov_b32 v1, s{61 + 2 * k}")
+            a(f"global_store_dwordx2 %[stp], v[0:1], off offset:{8 * k}")
+            a("s_nop 1")
+    a("s_waitcnt vmcnt(0)")
+    a(f"s_mov_b32 m0, s{SKEEP}")
+    a("s_nop 15")
+    a("s_nop 15")
+    return E.L
+
+
+def dq_clobbers(diag=False):
+    regs = [f'"v{r}"' for r in range(DVLAST + 1)] + [f'"a{r}"' for r in range(128, 240)] + \
+           [f'"s{r}"' for r in list(range(80, 88)) + list(range(92, 98))]
+    if diag:
+        regs += [f'"s{r}"' for r in range(60, 76)]
+    return ", ".join(regs)
+
+
 
 def main():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -479,6 +744,15 @@ def main():
         VARIANT.clear()
         txt.append("#undef LTX_DKDV_W1_CLOBBERS")
     txt.append("#define LTX_DKDV_W1_CLOBBERS " + clobbers(diag) + "\n")
+    VARIANT.clear()
+    txt += [f"#define LTX_DQ_W1_BUF {D_BUF}", define("LTX_DQ_W1_BODY", dq_body())]
+    if diag:
+        for k, var in enumerate(("stamps", "stamps+novalu"), 1):
+            VARIANT.clear()
+            VARIANT.update(var.split("+"))
+            txt.append(define(f"LTX_DQ_W1_BODY_V{k}", dq_body()))
+        VARIANT.clear()
+    txt.append("#define LTX_DQ_W1_CLOBBERS " + dq_clobbers(diag) + "\n")
     open(out, "w").write("\n".join(txt))
     print(out, len(L), "lines")
 

@@ -1187,6 +1187,9 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
     if (needs_bias(p)) {
       hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
       LTX_LAUNCH_CHECK();
+    } else if (dq_w1_enabled()) {
+      const int rc = launch_dq_w1(p, s);
+      if (rc != LTX_OK) return rc;
     } else if (dq_pipe_enabled()) {
       const int rc = launch_dq_pipe(p, s);
       if (rc != LTX_OK) return rc;

@@ -298,6 +298,9 @@ bool dq_pipe_enabled();
 // the dK/dV kernel at one wave per SIMD (hand-scheduled loop, attn_bwd_body.h): no key bias, head dim 64
 int launch_dkdv_w1(const AttnParams& p, hipStream_t s);
 bool dkdv_w1_enabled();
+// the dQ kernel at one wave per SIMD (hand-scheduled loop, attn_bwd_body.h): no key bias, head dim 64
+int launch_dq_w1(const AttnParams& p, hipStream_t s);
+bool dq_w1_enabled();
 // the forward with K / V by LDS-DMA and one barrier per tile (no key bias, Nk % 64 == 0)
 int launch_fwd_pipe(const AttnParams& p, hipStream_t s);
 bool fwd_pipe_enabled();

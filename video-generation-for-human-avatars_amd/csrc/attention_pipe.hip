@@ -474,6 +474,129 @@ int launch_dkdv_w1(const AttnParams& p, hipStream_t s) {
 }
 
 // =============================================================================================
+// dQ at ONE wave per SIMD (self-attention shapes: no key bias, head dim 64): 4 waves x 64 queries
+// (two 32-query tiles per wave) = 256 queries per workgroup, the loop one hand-scheduled asm
+// statement (attn_bwd_body.h LTX_DQ_W1_BODY, tools/gen_attn_bwd.py dq_body). Same arithmetic and
+// accumulation order as attn_dq_pipe_kernel: dQ is bitwise equal to it.
+// =============================================================================================
+template <int V>
+__global__ __launch_bounds__(256, 1) void attn_dq_w1_kernel(const AttnParams p) {
+  constexpr int HD = PHD;
+  __shared__ __attribute__((aligned(16))) char smem[3 * LTX_DQ_W1_BUF];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int q0 = bx * 256 + wave * 64;
+  // the lane's query in each 32-query tile (clamped: queries past Nq are computed, not stored)
+  const bf16_t* qp[2];
+  const bf16_t* op[2];
+  float nl[2], nd[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qc = min(q0 + qt * 32 + (lane & 31), p.Nq - 1);
+    qp[qt] = p.q + ((int64_t)b * p.Nq + qc) * p.ldq + hh * HD + 8 * h;
+    op[qt] = p.dout + ((int64_t)b * p.Nq + qc) * p.lddo + hh * HD + 8 * h;
+    const int64_t si = ((int64_t)b * p.H + hh) * p.Nq + qc;
+    nl[qt] = -p.lse[si];
+    nd[qt] = -p.delta[si];
+  }
+  // K / V columns of this (batch, head), exactly the valid key rows (keys past Nk read as zeros)
+  const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  const bf16_t* vbase = p.v + (int64_t)b * p.kvb * p.ldv + hh * HD;
+  const u32x4 srdk = raw_srd(kbase, ((uint64_t)(p.Nk - 1) * p.ldk + HD) * 2);
+  const u32x4 srdv = raw_srd(vbase, ((uint64_t)(p.Nk - 1) * p.ldv + HD) * 2);
+  uint32_t vk[2], vv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
+    vk[i] = (uint32_t)(row * p.ldk + c * 8) * 2;
+    vv[i] = (uint32_t)(row * p.ldv + c * 8) * 2;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
+  const uint32_t wq = __builtin_amdgcn_readfirstlane(wave * 2048);
+  const uint32_t kstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldk * 2));
+  const uint32_t vstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldv * 2));
+  const uint32_t iters = __builtin_amdgcn_readfirstlane((uint32_t)((p.Nk + 63) / 64 - 1));
+  const float c2 = p.scale * LOG2E;
+  uint64_t* stp = (uint64_t*)p.part +  // diagnostic builds only: this wave's 8 stamps
+                  ((blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z)) * 4 + wave) * 8;
+  f32x16 a00 = {}, a01 = {}, a10 = {}, a11 = {};
+#define LTX_DQ_OPERANDS \
+               : "+a"(a00), "+a"(a01), "+a"(a10), "+a"(a11) \
+               : [sk0] "s"(srd_half(srdk, 0)), [sk1] "s"(srd_half(srdk, 1)), [sv0] "s"(srd_half(srdv, 0)), \
+                 [sv1] "s"(srd_half(srdv, 1)), [kstep] "s"(kstep), [vstep] "s"(vstep), [lds0] "s"(lds0), \
+                 [wq] "s"(wq), [iters] "s"(iters), [c2] "s"(c2), [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]), \
+                 [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]), [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]), \
+                 [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]), [vk0] "v"(vk[0]), [vk1] "v"(vk[1]), \
+                 [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), [qp0] "v"(qp[0]), [qp1] "v"(qp[1]), [op0] "v"(op[0]), \
+                 [op1] "v"(op[1]), [nl0] "v"(nl[0]), [nl1] "v"(nl[1]), [nd0] "v"(nd[0]), [nd1] "v"(nd[1]), \
+                 [stp] "v"(stp) \
+               : "memory", "scc", "vcc", LTX_DQ_W1_CLOBBERS
+  if constexpr (V == 0) asm volatile(LTX_DQ_W1_BODY LTX_DQ_OPERANDS);
+#ifdef LTX_DKDV_DIAG
+  if constexpr (V == 1) asm volatile(LTX_DQ_W1_BODY_V1 LTX_DQ_OPERANDS);
+  if constexpr (V == 2) asm volatile(LTX_DQ_W1_BODY_V2 LTX_DQ_OPERANDS);
+#endif
+#undef LTX_DQ_OPERANDS
+  const f32x16 acc[2][2] = {{a00, a01}, {a10, a11}};
+  if (!p.dq_f32) {  // dQ as whole rows through wave-private LDS slots
+    __syncthreads();
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qb = q0 + qt * 32;
+      if (qb < p.Nq)
+        store_rows_lds<HD>(smem + wave * 4096, acc[qt], p.scale, (bf16_t*)p.dq + (int64_t)b * p.Nq * p.lddq + hh * HD,
+                           p.lddq, qb, min(32, p.Nq - qb), lane);
+    }
+    return;
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = q0 + qt * 32 + (lane & 31);
+    if (qi >= p.Nq) continue;
+    float* qrow = (float*)p.dq + ((int64_t)b * p.Nq + qi) * p.lddq + hh * HD;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 w = {acc[qt][d][4 * g] * p.scale, acc[qt][d][4 * g + 1] * p.scale, acc[qt][d][4 * g + 2] * p.scale,
+                   acc[qt][d][4 * g + 3] * p.scale};
+        *(f32x4*)(qrow + d * 32 + 8 * g + 4 * h) = w;
+      }
+  }
+}
+
+// LTX_ATTN_DQ_W1 (read per call): unset / 1 the one-wave kernel, 0 attn_dq_pipe_kernel, 12 / 13 the
+// stamped diagnostic variants (`make diag` builds)
+static int dq_w1_mode() {
+  const char* e = std::getenv("LTX_ATTN_DQ_W1");
+  return e ? std::atoi(e) : 1;
+}
+bool dq_w1_enabled() { return dq_w1_mode() != 0; }
+
+int launch_dq_w1(const AttnParams& p, hipStream_t s) {
+  const dim3 g((unsigned)((p.Nq + 255) / 256), (unsigned)p.H, (unsigned)p.B);
+#ifdef LTX_DKDV_DIAG
+  const int mode = dq_w1_mode();
+  if (mode == 12 || mode == 13) {
+    AttnParams q = p;
+    size_t ws = 0;
+    q.part = stream_workspace(s, &ws);
+    if (q.part == nullptr || ws < (size_t)g.x * g.y * g.z * 4 * 8 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
+    if (mode == 12) hipLaunchKernelGGL(attn_dq_w1_kernel<1>, g, dim3(256), 0, s, q);
+    else hipLaunchKernelGGL(attn_dq_w1_kernel<2>, g, dim3(256), 0, s, q);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+#endif
+  hipLaunchKernelGGL(attn_dq_w1_kernel<0>, g, dim3(256), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+// =============================================================================================
 // dQ (attn_q_kernel MODE 1 semantics) for self-attention shapes (no key bias, Nk % 64 == 0),
 // software pipelined the same way. A workgroup = 4 waves x 32 queries (Q, dO fragments, -lse and
 // delta of the lane's query in registers); per 32-key half j:

@@ -412,8 +412,11 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
         # LDS buffers of the pipelined kernels (attention_pipe.hip dq_nbuf / dkdv_nbuf: 4 unless "3")
         nq = "3" if os.environ.get("LTX_ATTN_DQ_NBUF", "4")[:1] == "3" else "4"
         nk = "3" if os.environ.get("LTX_ATTN_DKDV_NBUF", "4")[:1] == "3" else "4"
-        dqk = (f"ltx::attn_dq_pipe_kernel<{nq}>" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
-               else f"ltx::attn_q_kernel<{d}, 1, {kb}, 4>")
+        if kb == "false" and os.environ.get("LTX_ATTN_DQ_W1", "1").strip()[:1] != "0":
+            dqk = "ltx::attn_dq_w1_kernel"  # one wave per SIMD (attention_pipe.hip)
+        else:
+            dqk = (f"ltx::attn_dq_pipe_kernel<{nq}>" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
+                   else f"ltx::attn_q_kernel<{d}, 1, {kb}, 4>")
         if kb == "false" and os.environ.get("LTX_ATTN_DKDV_W1", "1").strip() not in ("0", ""):
             # one wave per SIMD, hand-scheduled loop (attention_pipe.hip attn_dkdv_w1_kernel)
             kern = f"ltx::attn_dkdv_w1_kernel<0> + {dqk}"
