@@ -74,10 +74,12 @@ def test_gemm_ring_store_bitwise(M, N, K, variant=20):
         assert err <= 0.02 * ref.abs().max().item()
 
 
-@pytest.mark.parametrize("M,N,K", [(14336, 2048, 2048), (14336, 8192, 2048), (7000, 6152, 384)])
-def test_gemm_ring_epilogues_bitwise(M, N, K, variant=20):
+# B = 7 (2048-row batches): 224-row tiles that straddle two batches (the per-row gate path; the
+# config-A tiles each lie inside one batch and load the gate row once)
+@pytest.mark.parametrize("M,N,K,B", [(14336, 2048, 2048, 8), (14336, 8192, 2048, 8), (7000, 6152, 384, 1),
+                                     (14336, 2048, 2048, 7)])
+def test_gemm_ring_epilogues_bitwise(M, N, K, B, variant=20):
     g = torch.Generator(device="cuda").manual_seed(7 + M + N + K)
-    B = 8 if M % 8 == 0 else 1
     a = torch.randn(M, K, device="cuda", generator=g).bfloat16()
     w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).bfloat16()
     b = torch.randn(N, device="cuda", generator=g).bfloat16()

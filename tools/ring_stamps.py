@@ -20,8 +20,9 @@ VARIANT = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 lib = _lib.load()
 lib.ltx_gemm_set_stamps.argtypes = [ctypes.c_void_p]
 SHAPES = [("qkv", 6144, 2048, "store"), ("out1_gres", 2048, 2048, "gated_residual"),
-          ("ff_up_gelu", 8192, 2048, "gelu"), ("ff_down", 2048, 8192, "store"),
-          ("ffdgrad_gelubwd", 8192, 2048, "gelu_bwd")]
+          ("ff_up_gelu", 8192, 2048, "gelu"), ("ff_down_gres", 2048, 8192, "gated_residual"),
+          ("ffdgrad_gelubwd", 8192, 2048, "gelu_bwd"), ("ff1_dgrad", 2048, 8192, "store"),
+          ("dh1_accum_gate", 2048, 2048, "accum"), ("do_rowdot", 2048, 2048, "store_rowdot")]
 
 
 def pct(v, q):
@@ -36,20 +37,30 @@ for name, n, k, epi in SHAPES:
     aux0 = aux1 = None
     if epi == "gelu":
         aux0 = torch.empty(M, n, device="cuda", dtype=torch.bfloat16)
-    if epi in ("gated_residual", "gelu_bwd"):
+    aux2, rank = None, 0
+    if epi in ("gated_residual", "gelu_bwd", "accum", "store_rowdot"):
         aux0 = torch.randn(M, n, device="cuda").bfloat16()
-    if epi == "gated_residual":
+    if epi in ("gated_residual", "accum"):
         aux1 = torch.randn(8, n, device="cuda").bfloat16()
-    if epi == "gelu_bwd":
+    if epi == "accum":
+        aux2 = torch.empty(M, n, device="cuda", dtype=torch.bfloat16)
+    if epi == "store_rowdot":
+        aux1 = torch.empty(8, 32, M // 8, device="cuda", dtype=torch.float32)
+        rank = 64
+    if epi in ("gelu_bwd", "accum", "store_rowdot"):
         bias = None
     c = torch.empty(M, n, device="cuda", dtype=torch.bfloat16)
     lib.ltx_gemm_set_variant(VARIANT)
-    kern = ops.gemm_kernel_name(M, n, k, 0, epi)
+    kern = ops.gemm_kernel_name(M, n, k, 0, epi, rank)
     bmt = 224 if ", 7" in kern else 256
     tiles = ((M + bmt - 1) // bmt) * ((n + 255) // 256)
     stamps = torch.zeros(tiles * 8, dtype=torch.int64, device="cuda")
     lib.ltx_gemm_set_stamps(ctypes.c_void_p(stamps.data_ptr()))
     kw = dict(bias=bias, epilogue=epi, aux0=aux0, aux1=aux1, rows_per_batch=1792 if aux1 is not None else 0)
+    if aux2 is not None:
+        kw["aux2"] = aux2
+    if rank:
+        kw["rank"] = rank
     for _ in range(10):
         ops.gemm(x, w, out=c, **kw)
     torch.cuda.synchronize()

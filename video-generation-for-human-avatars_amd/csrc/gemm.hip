@@ -616,10 +616,12 @@ static int g_dma_batch = [] {
   const char* e = getenv("LTX_GEMM_DMA_BATCH");
   return (e && e[0] == '0') ? 0 : 1;
 }();
-// LTX_GEMM_EPI_BATCH=0: the large-tile epilogue row pass loads one row's aux operands at a time
+// LTX_GEMM_EPI_BATCH: how the large-tile epilogue row pass loads its aux operands -- 2 (default)
+// every row's before the ring kernel writes its C image, 1 in two batches of rows after it, 0 one
+// row at a time (gemm_nt_kernel_t treats 2 as 1)
 static int g_epi_batch = [] {
   const char* e = getenv("LTX_GEMM_EPI_BATCH");
-  return (e && e[0] == '0') ? 0 : 1;
+  return e ? atoi(e) : 2;
 }();
 
 // The dispatcher's choice for one call, shared by launch() and ltx_gemm_describe (so bench.py can

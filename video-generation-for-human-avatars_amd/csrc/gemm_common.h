@@ -80,6 +80,7 @@ __device__ __forceinline__ void block_to_tile(int bid, int ntm, int ntn, int& tm
 // flight instead of waiting on one per row.
 struct EpiAux {
   u32x4 a, g;
+  int di = -1;  // STORE_ROWDOT: the delta element this lane stores (>= 0), -2 none, -1 computed per row
 };
 template <int EPI>
 constexpr bool epi_has_aux() {
@@ -116,11 +117,16 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       out8[j] = v[j];
       s += v[j] * bf2f((bf16_t)(o4[j >> 1] >> ((j & 1) * 16)));
     }
+    // the butterfly on DPP lane moves (no LDS round trip per step, as __shfl_xor's ds_bpermute
+    // had): quad_perm [1,0,3,2] = xor 1, [2,3,0,1] = xor 2, row_half_mirror pairs quad 0 with quad
+    // 1 of each 8 lanes (= xor 4 once both quads hold their sums); the same sums in the same order
     const int hd = p.rank, lanes = hd >> 3;
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    if (lanes == 8) s += __shfl_xor(s, 4, 64);
-    if (((n0 >> 3) & (lanes - 1)) == 0) {
+    s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
+    s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
+    if (lanes == 8) s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x141, 0xF, 0xF, false));
+    if (pre && pre->di != -1) {  // index precomputed by the caller (no integer division per row)
+      if (pre->di >= 0) ((float*)p.aux1)[pre->di] = s;
+    } else if (((n0 >> 3) & (lanes - 1)) == 0) {
       const int rpb = p.rows_per_batch, H = p.N / hd;
       ((float*)p.aux1)[((int64_t)(m / rpb) * H + n0 / hd) * rpb + m % rpb] = s;
     }

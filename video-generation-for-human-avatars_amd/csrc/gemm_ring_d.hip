@@ -1,0 +1,10 @@
+// Ring GEMM kernels of the epilogues <4, 8>, <4, 16>, <4, 32> (gemm_ring.h; split from gemm.hip so the
+// ring instantiations compile in parallel)
+#define LTX_RING_DEFINE
+#include "gemm_ring.h"
+
+namespace ltx {
+template bool launch_ring<4, 8>(const GemmParams& p, int bmt, hipStream_t s);
+template bool launch_ring<4, 16>(const GemmParams& p, int bmt, hipStream_t s);
+template bool launch_ring<4, 32>(const GemmParams& p, int bmt, hipStream_t s);
+}  // namespace ltx
