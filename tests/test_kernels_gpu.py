@@ -837,6 +837,54 @@ def test_attention_dkdv_w1_matches_pipe_bitwise(B, H, Nq, Nk, monkeypatch):
         assert torch.equal(a, b_)
 
 
+# (8, 32, 1792, 1792): config A's self-attention, 7 blocks per workgroup; (4, 16, 7488, 7488): config
+# X-like, 30 blocks per workgroup; the small ones give every block its own workgroup
+@pytest.mark.parametrize("B,H,Nq,Nk", [(8, 32, 1792, 1792), (4, 16, 7488, 7488), (2, 3, 1000, 768), (1, 2, 70, 320),
+                                       (2, 2, 320, 1792), (1, 3, 64, 256), (1, 2, 129, 192), (3, 40, 200, 1300)])
+def test_attention_dkdv_w1p_matches_w1_bitwise(B, H, Nq, Nk, monkeypatch):
+    """attn_dkdv_w1p_kernel (persistent: one workgroup per CU walks 256-key blocks, the next block's
+    K / V fragments and first Q / dO tiles loaded under the previous block's tail and stores;
+    LTX_ATTN_DKDV_W1=2) runs attn_dkdv_w1_kernel's loop per block: dK and dV bitwise equal, ragged
+    key blocks (K / V past Nk read as zeros, their rows not stored) and query tiles included."""
+    from ltx_amd import ops
+    d = 64
+    scale = d ** -0.5
+    q = g(B * Nq, H * d, seed=91)
+    k = g(B * Nk, H * d, seed=92)
+    v = g(B * Nk, H * d, seed=93)
+    do = g(B * Nq, H * d, seed=94)
+    o, lse = ops.attn_fwd(q, k, v, B, H, d, scale)
+    outs = {}
+    for w1 in ("1", "2"):
+        monkeypatch.setenv("LTX_ATTN_DKDV_W1", w1)
+        outs[w1] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale)
+    for a, b_ in zip(outs["2"], outs["1"]):
+        assert torch.equal(a, b_)
+
+
+@pytest.mark.parametrize("B,H,Nq,Nk", [(8, 32, 1792, 1792), (4, 16, 7488, 7488), (2, 3, 1000, 768), (1, 2, 70, 320),
+                                       (2, 2, 320, 1792), (1, 3, 300, 64), (1, 2, 129, 192), (3, 40, 1300, 200)])
+def test_attention_dq_w1p_matches_w1_bitwise(B, H, Nq, Nk, monkeypatch):
+    """attn_dq_w1p_kernel (persistent: one workgroup per CU walks 256-query blocks, the next block's
+    Q / dO fragments, lse and delta loaded under the previous block's tail and stores;
+    LTX_ATTN_DQ_W1=2) runs attn_dq_w1_kernel's loop per block: bf16 dQ bitwise equal, ragged query
+    blocks (rows past Nq read as zeros, not stored) included; the f32 dQ keeps the per-block kernel."""
+    from ltx_amd import ops
+    d = 64
+    scale = d ** -0.5
+    q = g(B * Nq, H * d, seed=95)
+    k = g(B * Nk, H * d, seed=96)
+    v = g(B * Nk, H * d, seed=97)
+    do = g(B * Nq, H * d, seed=98)
+    o, lse = ops.attn_fwd(q, k, v, B, H, d, scale)
+    outs = {}
+    for w1 in ("1", "2"):
+        monkeypatch.setenv("LTX_ATTN_DQ_W1", w1)
+        outs[w1] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale)
+    for a, b_ in zip(outs["2"], outs["1"]):
+        assert torch.equal(a, b_)
+
+
 @pytest.mark.parametrize("B,H,Nq,Nk", [(2, 3, 1000, 768), (1, 4, 1792, 1792), (1, 2, 70, 320), (1, 2, 50, 512),
                                        (2, 2, 320, 1792), (1, 3, 300, 64), (1, 2, 129, 192)])
 def test_attention_dq_w1_matches_pipe_bitwise(B, H, Nq, Nk, monkeypatch):

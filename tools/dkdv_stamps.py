@@ -22,6 +22,8 @@ for _ in range(3):
     ops.attn_bwd(q, k, v, o, do, lse, B, H, d, d ** -0.5)
     torch.cuda.synchronize()
 nwg = 7 * H * B
+if os.environ['LTX_ATTN_DKDV_W1'] == "22":  # the persistent kernel: one workgroup per CU, 7 items each
+    nwg = 256
 st = ws.view(torch.int64)[: nwg * 4 * 8].view(nwg * 4, 8).cpu().double()
 names = ["top", "barrier", "half A", "half B"]
 prev = st[:, 0]
@@ -33,3 +35,17 @@ body = st[:, 3] - st[:, 0]
 loop = st[:, 7] - st[:, 6]
 print(f"body total median {body.median():.0f} cycles (2 iterations, 64 MFMAs: floor 2048)")
 print(f"whole loop median {loop.median():.0f} cycles over {N // 64 - 1} bodies = {loop.median() / (N // 64 - 1):.0f} per body")
+
+# kernel entry / exit (s_memtime, s_memrealtime) of every wave: the loop's share of the wave's time
+ed = ws.view(torch.int64)[nwg * 4 * 8: nwg * 4 * 12].view(nwg * 4, 4).cpu().double()
+tot = ed[:, 2] - ed[:, 0]
+clk = tot / ((ed[:, 3] - ed[:, 1]) * 10.0)  # cycles per ns
+pro = st[:, 6] - ed[:, 0]
+epi = ed[:, 2] - st[:, 7]
+print(f"wave total median {tot.median():.0f} cycles at {clk.median():.3f} GHz: prologue {pro.median():.0f}, "
+      f"loop {(st[:, 7] - st[:, 6]).median():.0f}, tail + epilogue {epi.median():.0f}")
+span = (ed[:, 3].max() - ed[:, 1].min()) / 100.0
+wall = (ed[:, 3] - ed[:, 1]) / 100.0
+print(f"launch span {span:.1f} us; per-wave wall median {wall.median():.2f} us (x 7 rounds = {7 * wall.median():.1f} us)")
+if nwg == 256:
+    print(f"persistent: per item {tot.median() / 7:.0f} cycles = {wall.median() / 7:.2f} us (loop of the last item {(st[:, 7] - st[:, 6]).median():.0f})")

@@ -91,6 +91,11 @@ ACC = {("dv", 0, 0): 0, ("dv", 0, 1): 1, ("dv", 1, 0): 2, ("dv", 1, 1): 3,
        ("dk", 0, 0): 4, ("dk", 0, 1): 5, ("dk", 1, 0): 6, ("dk", 1, 1): 7}
 
 
+def ACC_REG(kind, kt, d):
+    """the persistent kernel's accumulators: dV (kt, d) at a[16 (2 kt + d)], dK at a[64 + 16 (2 kt + d)]"""
+    return (64 if kind == "dk" else 0) + 16 * (2 * kt + d)
+
+
 def v(r, n=1):
     return f"v{r}" if n == 1 else f"v[{r}:{r + n - 1}]"
 
@@ -110,6 +115,15 @@ def mfma(dst, A, B, C, needs=()):
 
 
 # ---------------------------------------------------------------------------------------- stages
+HARD_ACC = [False]       # persistent kernel: accumulators at fixed AGPRs (ACC_REG) instead of operands
+
+
+def acc_name(kind, kt, d):
+    if HARD_ACC[0]:
+        return a_(ACC_REG(kind, kt, d), 16)
+    return "%" + str(ACC[(kind, kt, d)])
+
+
 def c_mfmas():
     """C(j-1) in pack order (ss, kt, d): dV^T[kt][d] += TO[ss][d] . PB[kt][ss], then dK^T with TQ, SB;
     each accumulator takes ss = 0 then ss = 1 (attn_dkdv_pipe_kernel's order)"""
@@ -117,8 +131,8 @@ def c_mfmas():
     for ss in range(2):
         for kt in range(2):
             for d in range(2):
-                dv = "%" + str(ACC[("dv", kt, d)])
-                dk = "%" + str(ACC[("dk", kt, d)])
+                dv = acc_name("dv", kt, d)
+                dk = acc_name("dk", kt, d)
                 out.append(mfma(dv, a_(TO(ss, d), 4), v(PB(kt, ss), 4), dv, needs=[f"TO{ss}{d}"]))
                 out.append(mfma(dk, a_(TQ(ss, d), 4), v(SB(kt, ss), 4), dk, needs=[f"TQ{ss}{d}"]))
     return out
@@ -454,6 +468,273 @@ def clobbers(diag):
     return ", ".join(regs)
 
 # =============================================================================================
+# Persistent dK / dV (attn_dkdv_w1p_kernel): one workgroup per CU walks its key blocks ("items") in ONE
+# asm statement. Per item: the body of attn_dkdv_w1_kernel (A(0), half 0, the tile loop, the two tail
+# halves), then the dK / dV stores from the accumulators (a[0:127], fixed: ACC_REG) through a wave-
+# private LDS staging area. The next item's K / V fragments (into KF and v[0:31]) are loaded during
+# the first tail half and its first two Q / dO tiles are DMA'd into the ring right after the last
+# half, so item i+1's loads fly while item i finishes and stores: the ~10k-cycle load burst that opens
+# every workgroup of the non-persistent kernel (tools/dkdv_stamps.py: prologue 10.7k of 89k cycles)
+# is hidden, and the round-to-round skew of 1792 short-lived workgroups disappears.
+# Item parameters come from a table the kernel writes into LDS before the statement: one 96-B row
+# per item (K / V descriptors, Q / dO / lse / delta bases, dK / dV descriptors) plus a null row whose
+# K / V descriptors are empty, so the last item's prefetch loads zeros.
+# =============================================================================================
+P_STG = NBUF * W_BUF                 # staging: 4 waves x 16 KiB ([kt][dK | dV], 4 KiB each)
+P_TAB = P_STG + 4 * 16384            # the item table
+ITEM_B = 96
+SK, SV, SDK, SDV = 40, 44, 48, 52    # descriptors: the item's K / V rows, its dK / dV block
+SLSE, SDLT = 56, 58                  # stats bases from the table (lse / delta: one per wave)
+SITEM = 39                           # items left
+TABV = 226                           # LDS address of the current item's table row (uniform)
+PRM = 66                             # v[66:81]: table reads (set 0's dP' tiles: free in the tail)
+P_VLAST = 226
+
+
+def p_params_next(first):
+    """read a table row (the next one, or row 0 in the prologue) into K / V descriptors and the Q / dO /
+    stats descriptors' bases: [(reads as I)], [(readfirstlane + descriptor lines as I needing them)]"""
+    off = 0 if first else ITEM_B
+    rd = [I(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{off + 16 * i}", makes="PRM") for i in range(4)]
+    use = []
+    for i in range(4):
+        use.append(I(f"v_readfirstlane_b32 s{SK + i}, {v(PRM + i)}", needs=["PRM"]))
+        use.append(I(f"v_readfirstlane_b32 s{SV + i}, {v(PRM + 4 + i)}", needs=["PRM"]))
+    for srd, w in ((SRDQ, 8), (SRDO, 10), (SLSE, 12), (SDLT, 14)):
+        use.append(I(f"v_readfirstlane_b32 s{srd}, {v(PRM + w)}", needs=["PRM"]))
+        use.append(I(f"v_readfirstlane_b32 s{srd + 1}, {v(PRM + w + 1)}", needs=["PRM"]))
+    return rd, use
+
+
+def p_srd_reset():
+    """the Q / dO / stats descriptors' sizes (shrunk by the previous item's loop) and this wave's stats base"""
+    return [f"s_mov_b32 s{SRDQ + 2}, %[sq2]", f"s_mov_b32 s{SRDQ + 3}, 0x20000",
+            f"s_mov_b32 s{SRDO + 2}, %[so2]", f"s_mov_b32 s{SRDO + 3}, 0x20000",
+            f"s_mov_b32 s{SRDS + 2}, %[ss2]", f"s_mov_b32 s{SRDS + 3}, 0x20000",
+            "s_cmp_eq_u32 %[wodd], 0",
+            f"s_cselect_b64 s[{SRDS}:{SRDS + 1}], s[{SLSE}:{SLSE + 1}], s[{SDLT}:{SDLT + 1}]"]
+
+
+def p_kv_loads():
+    """the item's K fragments into KF, its V fragments into v[0:31] (negated into VF at the item start)"""
+    out = []
+    for kt in range(2):
+        for ks in range(4):
+            out.append(f"buffer_load_dwordx4 {a_(KF(kt, ks), 4)}, %[vk{kt}], s[{SK}:{SK + 3}], 0 offen offset:{ks * 32}")
+            out.append(f"buffer_load_dwordx4 {v(16 * kt + 4 * ks, 4)}, %[vv{kt}], s[{SV}:{SV + 3}], 0 offen offset:{ks * 32}")
+    return out
+
+
+def p_dma_first_tiles():
+    """the item's Q / dO tiles 0 and 1 into ring buffers 0 and 1 (descriptors advanced past them)"""
+    out = [f"s_mov_b32 s{SB0}, %[lds0]", f"s_add_u32 s{SB1}, %[lds0], {W_BUF}", f"s_add_u32 s{SBD}, %[lds0], {2 * W_BUF}"]
+    for buf in (SB0, SB1):
+        out.append(f"s_add_u32 s{STMP}, s{buf}, %[wq]")
+        for m0, ld in dma_pieces(buf):
+            out += [m0, "s_nop 0", ld]
+        out += advance_srds()
+    return out
+
+
+def p_epilogue(E):
+    """dK (x scale) / dV of the item from the accumulators: bf16 rows through this wave's staging area
+    (16-B chunks XOR row & 7, as store_rows_lds), then buffer stores clipped to the block's valid keys"""
+    a = E.raw
+    a("s_nop 15")
+    a("s_nop 15")  # the last C MFMAs -> accvgpr reads
+    # x = row & 7 (WX), this lane's write base in the wave's staging area (WB); the swizzled write
+    # addresses rotate over v[198:205], the data over v[162:177]
+    WX, WB = 194, 195
+    a(f"v_bfe_u32 {v(WX)}, %[vwd], 7, 3")
+    a(f"v_add_u32 {v(WB)}, %[stg], %[vwd]")
+    for kt in range(2):
+        for ti, kind in enumerate(("dk", "dv")):
+            stage = (2 * kt + ti) * 4096
+            for d in range(2):
+                base = ACC_REG(kind, kt, d)
+                for r in range(16):
+                    a(f"v_accvgpr_read_b32 {v(130 + 16 * d + r)}, {a_(base + r)}")
+            if kind == "dk":
+                for r in range(32):
+                    a(f"v_mul_f32 {v(130 + r)}, %[scale], {v(130 + r)}")
+            for d in range(2):
+                for g in range(4):
+                    src = 130 + 16 * d + 4 * g
+                    c = 4 * d + g
+                    wd, wt = 162 + 2 * c, 198 + c
+                    a(f"v_cvt_pk_bf16_f32 {v(wd)}, {v(src)}, {v(src + 1)}")
+                    a(f"v_cvt_pk_bf16_f32 {v(wd + 1)}, {v(src + 2)}, {v(src + 3)}")
+                    a(f"v_xor_b32 {v(wt)}, {c}, {v(WX)}")
+                    a(f"v_lshl_add_u32 {v(wt)}, {v(wt)}, 4, {v(WB)}")
+                    a(f"ds_write_b64 {v(wt)}, {v(wd, 2)} offset:{stage}")
+    a("s_waitcnt lgkmcnt(0)")
+    for kt in range(2):
+        for ti in range(2):
+            stage = (2 * kt + ti) * 4096
+            dst = (32, 98)[ti] + 16 * kt
+            for i in range(4):
+                a(f"ds_read_b128 {v(dst + 4 * i, 4)}, %[vrd] offset:{stage + 1024 * i}")
+    a("s_waitcnt lgkmcnt(0)")
+    for kt in range(2):
+        for ti, (srd, vo, s8) in enumerate(((SDK, "%[vdk]", "%[s8dk]"), (SDV, "%[vdv]", "%[s8dv]"))):
+            dst = (32, 98)[ti] + 16 * kt
+            for i in range(4):
+                a(f"s_mul_i32 s{STMP}, {s8}, {4 * kt + i}")
+                a(f"buffer_store_dwordx4 {v(dst + 4 * i, 4)}, {vo}, s[{srd}:{srd + 3}], s{STMP} offen")
+
+
+def dkdv_p_body():
+    HARD_ACC[0] = True
+    try:
+        return _dkdv_p_body()
+    finally:
+        HARD_ACC[0] = False
+
+
+def _dkdv_p_body():
+    E = Emitter()
+    a = E.raw
+    a("s_nop 4")
+    a(f"s_mov_b32 s{SKEEP}, m0")
+    a(f"v_mov_b32 {v(TABV)}, %[tab]")
+    a(f"s_mov_b32 s{SITEM}, %[nitems]")
+    # ---- item 0: parameters, fragments, tiles 0 and 1 ----------------------------------------------
+    rd, use = p_params_next(True)
+    for ins in rd + use:
+        E.put(ins)
+    E.drain("s_waitcnt lgkmcnt(0)")
+    for i in range(2):  # item 0's dK / dV descriptors
+        a(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{64 + 16 * i}")
+    a("s_waitcnt lgkmcnt(0)")
+    for i in range(4):
+        a(f"v_readfirstlane_b32 s{SDK + i}, {v(PRM + i)}")
+        a(f"v_readfirstlane_b32 s{SDV + i}, {v(PRM + 4 + i)}")
+    for t in p_srd_reset():
+        a(t)
+    a("s_nop 4")  # SGPRs fresh from v_readfirstlane -> descriptors / M0
+    for t in p_kv_loads() + p_dma_first_tiles():
+        a(t)
+    a("s_waitcnt vmcnt(5)")  # K, V and tile 0 landed (tile 1's five pieces may fly)
+    a("s_branch L_p_item_%=")
+    a("L_p_next_%=:")
+    # the previous item left: K / V fragments (16), tiles 0, 1 (10 pieces), its dK / dV stores (16)
+    a("s_waitcnt vmcnt(21)")
+    a("L_p_item_%=:")
+    for r in range(32):  # -V (sign flip, exact) into the accumulator file
+        a(f"v_xor_b32 {v(r)}, 0x80008000, {v(r)}")
+    for r in range(32):
+        a(f"v_accvgpr_write_b32 {a_(160 + r)}, {v(r)}")
+    for r in range(128):
+        a(f"v_accvgpr_write_b32 {a_(r)}, 0")
+    a("s_barrier")
+    for t in addr_regs("A", f"s{SB0}") + addr_regs("TN", f"s{SB0}"):
+        a(t)
+    for ins in a_reads(0) + lse_reads(0, LSEB[0]):
+        E.put(ins)
+    a("s_nop 1")
+    for ins in a_mfmas(0):
+        E.put(ins)
+    a("s_nop 7")
+    a("s_nop 7")
+    a("s_nop 3")
+    b_even, b_odd = b_stream(0, LSEB[0]), b_stream(1, LSEB[1])
+    half(E, False, {}, b_even, 1, read_plan(1, TN, 0, 1, LSEB[1]))
+    a(f"s_mov_b32 s{STMP}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{STMP}")
+    a(f"s_mov_b32 s{SITER}, %[iters]")
+    if "stamps" in VARIANT:
+        a("s_memtime s[72:73]")
+    a(f"s_cmp_eq_u32 s{SITER}, 0")
+    a("s_cbranch_scc1 L_p_tail_%=")
+    a("L_p_loop_%=:")
+    stamp(E, 0)
+    E.drain("s_waitcnt vmcnt(0) lgkmcnt(15)", keep=15)
+    a("s_barrier")
+    stamp(E, 1)
+    a(f"s_mov_b32 s{STMP}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{STMP}")
+    for t in addr_regs("A", f"s{SB1}"):
+        a(t)
+    a(f"s_add_u32 s{STMP}, s{SBD}, %[wq]")
+    later = {1 + i: [t] for i, t in enumerate(addr_regs("TC", f"s{SB0}") + addr_regs("TN", f"s{SB1}"))}
+    half(E, True, b_even, b_odd, 0, read_plan(0, TC, 1, 0, LSEB[0]), dma_pieces(SBD), extra=later)
+    stamp(E, 2)
+    for t in advance_srds():
+        a(t)
+    half(E, True, b_odd, b_even, 1, read_plan(1, TN, 0, 1, LSEB[1]))
+    stamp(E, 3)
+    a(f"s_sub_u32 s{SITER}, s{SITER}, 1")
+    a(f"s_cmp_eq_u32 s{SITER}, 0")
+    a("s_cbranch_scc0 L_p_loop_%=")
+    a("L_p_tail_%=:")
+    if "stamps" in VARIANT:
+        a("s_memtime s[74:75]")
+    # ---- tail: half J-1 with the next item's parameters (slots 12-15, after B(J-2) freed set 0),
+    # descriptors (slots 20-23) and K / V fragment loads (slots 24-31) ------------------------------
+    plan = read_plan(None, TN, 1, None, None)
+    rd, use = p_params_next(False)
+    for i, x in enumerate(rd):
+        plan.setdefault(12 + i, []).append(x)
+    for i, x in enumerate(use):
+        plan.setdefault(20 + i // 6, []).append(x)
+    extra = {}
+    reset = p_srd_reset()
+    for i, t in enumerate(reset):
+        extra.setdefault(23 if i < 6 else 24, []).append(t)
+    extra.setdefault(24, []).append("s_nop 4")
+    for i, t in enumerate(p_kv_loads()):
+        extra.setdefault(25 + i // 3, []).append(t)
+    half(E, True, b_even, b_odd, None, plan, extra=extra)
+    half(E, True, b_odd, {}, None, {})
+    # ---- end of the item: ring free -> the next item's first tiles; the stores; the next dK / dV ----
+    E.drain("s_waitcnt lgkmcnt(0)")
+    a("s_barrier")
+    a(f"s_cmp_eq_u32 s{SITEM}, 1")
+    a("s_cbranch_scc1 L_p_nodma_%=")
+    # the loop's last (empty, past-the-end) tile DMA of this wave landed before its pieces of the
+    # next item's tiles 0 and 1 go into the same ring slots (the 16 fragment loads may fly)
+    a("s_waitcnt vmcnt(16)")
+    for t in p_dma_first_tiles():
+        a(t)
+    a("L_p_nodma_%=:")
+    p_epilogue(E)
+    a(f"s_cmp_eq_u32 s{SITEM}, 1")
+    a("s_cbranch_scc1 L_p_done_%=")
+    a("s_nop 4")  # the stores' descriptor reads before the descriptors are rewritten
+    for i in range(2):
+        a(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{ITEM_B + 64 + 16 * i}")
+    a("s_waitcnt lgkmcnt(0)")
+    for i in range(4):
+        a(f"v_readfirstlane_b32 s{SDK + i}, {v(PRM + i)}")
+        a(f"v_readfirstlane_b32 s{SDV + i}, {v(PRM + 4 + i)}")
+    a(f"v_add_u32 {v(TABV)}, {ITEM_B}, {v(TABV)}")
+    a(f"s_sub_u32 s{SITEM}, s{SITEM}, 1")
+    a("s_branch L_p_next_%=")
+    a("L_p_done_%=:")
+    if "stamps" in VARIANT:
+        for k in range(8):
+            a(f"v_mov_b32 v0, s{60 + 2 * k}")
+            a(f"v_mov_b32 v1, s{61 + 2 * k}")
+            a(f"global_store_dwordx2 %[stp], v[0:1], off offset:{8 * k}")
+            a("s_nop 1")
+    a("s_waitcnt vmcnt(0)")
+    a(f"s_mov_b32 m0, s{SKEEP}")
+    return E.L
+
+
+def p_clobbers(diag):
+    regs = [f'"v{r}"' for r in range(P_VLAST + 1)] + [f'"a{r}"' for r in range(256)] + \
+           [f'"s{r}"' for r in list(range(39, 60)) + list(range(80, 98))]
+    if diag:
+        regs += [f'"s{r}"' for r in range(60, 76)]
+    return ", ".join(regs)
+
+
+# =============================================================================================
 # dQ at one wave per SIMD (attn_dq_w1_kernel): 4 waves x 64 queries (two 32-query tiles qt per
 # wave), keys in tiles of 64 through the same 3-buffer LDS-DMA ring (K | V), per 32-key half j:
 #   A(j+1): S[qt] = K.Q^T, dP'[qt] = V.dO^T - delta (16 MFMAs; the K / V row fragments feed both qt);
@@ -500,7 +781,7 @@ def dq_c_mfmas():
     for ss in range(2):
         for qt in range(2):
             for d in range(2):
-                acc = "%" + str(2 * qt + d)
+                acc = a_(16 * (2 * qt + d), 16) if HARD_ACC[0] else "%" + str(2 * qt + d)
                 out.append(mfma(acc, a_(DKT(ss, d), 4), v(DSBF(qt, ss), 4), acc, needs=[f"KT{ss}{d}"]))
     return out
 
@@ -533,7 +814,8 @@ def dq_b_stream(s):
         r = 8 * ss + i
         sr, dr = DSD(s, 2 * qt) + r, DSD(s, 2 * qt + 1) + r
         k = (3 * e) // 4 + D_LAG
-        put(k - 1, I(f"v_fma_f32 {v(sr)}, {v(sr)}, %[c2], %[nl{qt}]"))
+        nl = v(DNLR + qt) if HARD_ACC[0] else f"%[nl{qt}]"
+        put(k - 1, I(f"v_fma_f32 {v(sr)}, {v(sr)}, %[c2], {nl}"))
         put(k, I(f"v_exp_f32 {v(sr)}, {v(sr)}"))
         put(k + 2, I(f"v_mul_f32 {v(dr)}, {v(sr)}, {v(dr)}"))
         if e % 2 == 1:
@@ -585,7 +867,7 @@ def dq_addr(which, sbase):
     return [f"v_add_u32 {v(T[k])}, {sbase}, {src[k]}" for k in range(4)]
 
 
-def dq_half(E, c, b_prev, b_cur, a_set, a_u, tr, dma=(), extra=None):
+def dq_half(E, c, b_prev, b_cur, a_set, a_u, tr, dma=(), extra=None, more=None):
     """one 32-key half j (24 slots): C(j-1) in slots 0-7 if c, A(j+1) (set a_set, half a_u of the
     tile at RK) in 8-23; B(j-1)'s tail and B(j)'s head; A's reads in slots 0-7, the next C's K^T
     fragments (tr = (address regs, half)) in 10-17; DMA pieces and `extra` raw lines"""
@@ -600,6 +882,8 @@ def dq_half(E, c, b_prev, b_cur, a_set, a_u, tr, dma=(), extra=None):
     if tr is not None:
         for i, x in enumerate(dq_tr_reads(*tr)):
             reads.setdefault(10 + i, []).append(x)
+    for k, ins in (more or {}).items():
+        reads.setdefault(k, []).extend(ins)
     dslot = {}
     for k, (m0, ld) in enumerate(dma):
         q = 2 + 5 * k
@@ -710,6 +994,245 @@ def dq_body():
     return E.L
 
 
+# =============================================================================================
+# Persistent dQ (attn_dq_w1p_kernel): one workgroup per CU walks its 256-query blocks in ONE asm
+# statement, as the persistent dK / dV kernel does: the next block's Q / dO fragments (into QF / OF),
+# lse and delta (v[0:3]) load in the first tail half, its first two K / V tiles right after the last
+# half, under the dQ stores of the block. Table row (96 B): Q, dO, lse, delta descriptors of the
+# block (sizes: its valid rows), K / V bases of the (batch, head), the dQ descriptor.
+# =============================================================================================
+DP_STG = 3 * D_BUF                    # staging: 4 waves x 8 KiB ([qt] 4 KiB each)
+DP_TAB = DP_STG + 4 * 8192
+DNLR = 190                            # -lse of the lane's query in qt 0 / 1 (the B stream's fma)
+DP_TABV = 192
+DP_VLAST = 192
+DSQ, DSO, DSL, DSD_, DSDQ = 40, 44, 48, 52, 56   # descriptors of the block's Q, dO, lse, delta, dQ
+DSITEM = 39
+
+
+def dqp_params_next(first):
+    """table row -> the Q / dO / lse / delta descriptors and the K / V descriptors' bases"""
+    off = 0 if first else ITEM_B
+    rd = [I(f"ds_read_b128 {v(66 + 4 * i, 4)}, {v(DP_TABV)} offset:{off + 16 * i}", makes="PRM") for i in range(5)]
+    use = []
+    for j, srd in enumerate((DSQ, DSO, DSL, DSD_)):
+        for i in range(4):
+            use.append(I(f"v_readfirstlane_b32 s{srd + i}, {v(66 + 4 * j + i)}", needs=["PRM"]))
+    for i in range(2):
+        use.append(I(f"v_readfirstlane_b32 s{SRDK + i}, {v(82 + i)}", needs=["PRM"]))
+        use.append(I(f"v_readfirstlane_b32 s{SRDV + i}, {v(84 + i)}", needs=["PRM"]))
+    return rd, use
+
+
+def dqp_loads():
+    """the block's Q / dO fragments into QF / OF, the lane's lse and delta per qt into v[0:3]"""
+    out = []
+    for qt in range(2):
+        for ks in range(4):
+            out.append(f"buffer_load_dwordx4 {a_(DQF(qt, ks), 4)}, %[vq{qt}], s[{DSQ}:{DSQ + 3}], 0 offen offset:{ks * 32}")
+            out.append(f"buffer_load_dwordx4 {a_(DOF(qt, ks), 4)}, %[vo{qt}], s[{DSO}:{DSO + 3}], 0 offen offset:{ks * 32}")
+    for qt in range(2):
+        out.append(f"buffer_load_dword {v(qt)}, %[vs{qt}], s[{DSL}:{DSL + 3}], 0 offen")
+        out.append(f"buffer_load_dword {v(2 + qt)}, %[vs{qt}], s[{DSD_}:{DSD_ + 3}], 0 offen")
+    return out
+
+
+def dqp_kv_reset():
+    return [f"s_mov_b32 s{SRDK + 2}, %[sk2]", f"s_mov_b32 s{SRDK + 3}, 0x20000",
+            f"s_mov_b32 s{SRDV + 2}, %[sv2]", f"s_mov_b32 s{SRDV + 3}, 0x20000"]
+
+
+def dqp_dma_first_tiles():
+    out = [f"s_mov_b32 s{SB0}, %[lds0]", f"s_add_u32 s{SB1}, %[lds0], {D_BUF}", f"s_add_u32 s{SBD}, %[lds0], {2 * D_BUF}"]
+    for buf in (SB0, SB1):
+        out.append(f"s_add_u32 s{STMP}, s{buf}, %[wq]")
+        for m0, ld in dq_dma(buf):
+            out += [m0, "s_nop 0", ld]
+        out += dq_advance()
+    return out
+
+
+def dqp_epilogue(E):
+    """dQ (x scale) of the block: bf16 rows through this wave's staging area, buffer stores clipped
+    to the block's valid queries"""
+    a = E.raw
+    a("s_nop 15")
+    a("s_nop 15")
+    WX, WB = 178, 179
+    a(f"v_bfe_u32 {v(WX)}, %[vwd], 7, 3")
+    a(f"v_add_u32 {v(WB)}, %[stg], %[vwd]")
+    for qt in range(2):
+        for d in range(2):
+            for r in range(16):
+                a(f"v_accvgpr_read_b32 {v(66 + 16 * d + r)}, {a_(16 * (2 * qt + d) + r)}")
+        for r in range(32):
+            a(f"v_mul_f32 {v(66 + r)}, %[scale], {v(66 + r)}")
+        for d in range(2):
+            for g in range(4):
+                src = 66 + 16 * d + 4 * g
+                c = 4 * d + g
+                wd, wt = 130 + 2 * c, 180 + c
+                a(f"v_cvt_pk_bf16_f32 {v(wd)}, {v(src)}, {v(src + 1)}")
+                a(f"v_cvt_pk_bf16_f32 {v(wd + 1)}, {v(src + 2)}, {v(src + 3)}")
+                a(f"v_xor_b32 {v(wt)}, {c}, {v(WX)}")
+                a(f"v_lshl_add_u32 {v(wt)}, {v(wt)}, 4, {v(WB)}")
+                a(f"ds_write_b64 {v(wt)}, {v(wd, 2)} offset:{qt * 4096}")
+    a("s_waitcnt lgkmcnt(0)")
+    for qt in range(2):
+        for i in range(4):
+            a(f"ds_read_b128 {v(98 + 16 * qt + 4 * i, 4)}, %[vrd] offset:{qt * 4096 + 1024 * i}")
+    a("s_waitcnt lgkmcnt(0)")
+    for qt in range(2):
+        for i in range(4):
+            a(f"s_mul_i32 s{STMP}, %[s8dq], {4 * qt + i}")
+            a(f"buffer_store_dwordx4 {v(98 + 16 * qt + 4 * i, 4)}, %[vdq], s[{DSDQ}:{DSDQ + 3}], s{STMP} offen")
+
+
+def dq_p_body():
+    HARD_ACC[0] = True
+    try:
+        return _dq_p_body()
+    finally:
+        HARD_ACC[0] = False
+
+
+def dqp_item_setup(a):
+    """the block's -lse (DNLR) and -delta tuples (the dP chains' initial accumulator) from v[0:3]"""
+    for qt in range(2):
+        a(f"v_xor_b32 {v(DNLR + qt)}, 0x80000000, {v(qt)}")
+        a(f"v_xor_b32 {v(2 + qt)}, 0x80000000, {v(2 + qt)}")
+        for r in range(16):
+            a(f"v_mov_b32 {v(DNDL(qt) + r)}, {v(2 + qt)}")
+
+
+def _dq_p_body():
+    E = Emitter()
+    a = E.raw
+    a("s_nop 4")
+    a(f"s_mov_b32 s{SKEEP}, m0")
+    a(f"v_mov_b32 {v(DP_TABV)}, %[tab]")
+    a(f"s_mov_b32 s{DSITEM}, %[nitems]")
+    rd, use = dqp_params_next(True)
+    for ins in rd + use:
+        E.put(ins)
+    E.drain("s_waitcnt lgkmcnt(0)")
+    a(f"ds_read_b128 {v(86, 4)}, {v(DP_TABV)} offset:80")  # the block's dQ descriptor
+    a("s_waitcnt lgkmcnt(0)")
+    for i in range(4):
+        a(f"v_readfirstlane_b32 s{DSDQ + i}, {v(86 + i)}")
+    for t in dqp_kv_reset():
+        a(t)
+    a("s_nop 4")
+    for t in dqp_loads() + dqp_dma_first_tiles():
+        a(t)
+    a("s_waitcnt vmcnt(4)")  # Q, dO fragments, lse, delta and key tile 0 landed
+    a("s_branch L_qp_item_%=")
+    a("L_qp_next_%=:")
+    # the previous block left: fragments + stats (20), K / V tiles 0, 1 (8 pieces), its dQ stores (8)
+    a("s_waitcnt vmcnt(12)")
+    a("L_qp_item_%=:")
+    dqp_item_setup(a)
+    for r in range(64):
+        a(f"v_accvgpr_write_b32 {a_(r)}, 0")
+    a("s_barrier")
+    for t in dq_addr("A", f"s{SB0}") + dq_addr("TN", f"s{SB0}"):
+        a(t)
+    for ins in dq_a_reads(0):
+        E.put(ins)
+    a("s_nop 1")
+    for ins in dq_a_mfmas(0):
+        E.put(ins)
+    a("s_nop 7")
+    a("s_nop 7")
+    a("s_nop 3")
+    b_even, b_odd = dq_b_stream(0), dq_b_stream(1)
+    dq_half(E, False, {}, b_even, 1, 1, (DTN, 0))
+    a(f"s_mov_b32 s{STMP}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{STMP}")
+    a(f"s_mov_b32 s{SITER}, %[iters]")
+    if "stamps" in VARIANT:
+        a("s_memtime s[72:73]")
+    a(f"s_cmp_eq_u32 s{SITER}, 0")
+    a("s_cbranch_scc1 L_qp_tail_%=")
+    a("L_qp_loop_%=:")
+    stamp(E, 0)
+    E.drain("s_waitcnt vmcnt(0) lgkmcnt(15)", keep=15)
+    a("s_barrier")
+    stamp(E, 1)
+    a(f"s_mov_b32 s{STMP}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{STMP}")
+    for t in dq_addr("A", f"s{SB1}"):
+        a(t)
+    a(f"s_add_u32 s{STMP}, s{SBD}, %[wq]")
+    later = {1 + i: [t] for i, t in enumerate(dq_addr("TC", f"s{SB0}") + dq_addr("TN", f"s{SB1}"))}
+    dq_half(E, True, b_even, b_odd, 0, 0, (DTC, 1), dq_dma(SBD), extra=later)
+    stamp(E, 2)
+    for t in dq_advance():
+        a(t)
+    dq_half(E, True, b_odd, b_even, 1, 1, (DTN, 0))
+    stamp(E, 3)
+    a(f"s_sub_u32 s{SITER}, s{SITER}, 1")
+    a(f"s_cmp_eq_u32 s{SITER}, 0")
+    a("s_cbranch_scc0 L_qp_loop_%=")
+    a("L_qp_tail_%=:")
+    if "stamps" in VARIANT:
+        a("s_memtime s[74:75]")
+    # tail half J-1: the next block's parameters (slots 5-9, once B(J-2) freed set 0), descriptors
+    # (slots 11-14), fragment / stats loads (slots 16-22)
+    rd, use = dqp_params_next(False)
+    more = {}
+    for i, x in enumerate(rd):
+        more.setdefault(5 + i, []).append(x)
+    for i, x in enumerate(use):
+        more.setdefault(11 + i // 6, []).append(x)
+    extra = {15: dqp_kv_reset() + ["s_nop 4"]}
+    for i, t in enumerate(dqp_loads()):
+        extra.setdefault(16 + i // 3, []).append(t)
+    dq_half(E, True, b_even, b_odd, None, None, (DTN, 1), extra=extra, more=more)
+    dq_half(E, True, b_odd, {}, None, None, None)
+    E.drain("s_waitcnt lgkmcnt(0)")
+    a("s_barrier")
+    a(f"s_cmp_eq_u32 s{DSITEM}, 1")
+    a("s_cbranch_scc1 L_qp_nodma_%=")
+    a("s_waitcnt vmcnt(20)")  # the loop's last (past-the-end) tile DMA landed; the 20 block loads may fly
+    for t in dqp_dma_first_tiles():
+        a(t)
+    a("L_qp_nodma_%=:")
+    dqp_epilogue(E)
+    a(f"s_cmp_eq_u32 s{DSITEM}, 1")
+    a("s_cbranch_scc1 L_qp_done_%=")
+    a("s_nop 4")
+    a(f"ds_read_b128 {v(66, 4)}, {v(DP_TABV)} offset:{ITEM_B + 80}")
+    a("s_waitcnt lgkmcnt(0)")
+    for i in range(4):
+        a(f"v_readfirstlane_b32 s{DSDQ + i}, {v(66 + i)}")
+    a(f"v_add_u32 {v(DP_TABV)}, {ITEM_B}, {v(DP_TABV)}")
+    a(f"s_sub_u32 s{DSITEM}, s{DSITEM}, 1")
+    a("s_branch L_qp_next_%=")
+    a("L_qp_done_%=:")
+    if "stamps" in VARIANT:
+        for k in range(8):
+            a(f"v_mov_b32 v0, s{60 + 2 * k}")
+            a(f"v_mov_b32 v1, s{61 + 2 * k}")
+            a(f"global_store_dwordx2 %[stp], v[0:1], off offset:{8 * k}")
+            a("s_nop 1")
+    a("s_waitcnt vmcnt(0)")
+    a(f"s_mov_b32 m0, s{SKEEP}")
+    return E.L
+
+
+def dqp_clobbers(diag=False):
+    regs = [f'"v{r}"' for r in range(DP_VLAST + 1)] + [f'"a{r}"' for r in range(240)] + \
+           [f'"s{r}"' for r in list(range(39, 60)) + list(range(80, 88)) + list(range(92, 98))]
+    if diag:
+        regs += [f'"s{r}"' for r in range(60, 76)]
+    return ", ".join(regs)
+
+
 def dq_clobbers(diag=False):
     regs = [f'"v{r}"' for r in range(DVLAST + 1)] + [f'"a{r}"' for r in range(128, 240)] + \
            [f'"s{r}"' for r in list(range(80, 88)) + list(range(92, 98))]
@@ -745,6 +1268,15 @@ def main():
         txt.append("#undef LTX_DKDV_W1_CLOBBERS")
     txt.append("#define LTX_DKDV_W1_CLOBBERS " + clobbers(diag) + "\n")
     VARIANT.clear()
+    txt += [f"#define LTX_DKDV_W1P_STG {P_STG}", f"#define LTX_DKDV_W1P_TAB {P_TAB}",
+            f"#define LTX_DKDV_W1P_ITEM {ITEM_B}", define("LTX_DKDV_W1P_BODY", dkdv_p_body())]
+    if diag:
+        VARIANT.update({"stamps"})
+        txt.append(define("LTX_DKDV_W1P_BODY_V1", dkdv_p_body()))
+        VARIANT.clear()
+        txt.append("#undef LTX_DKDV_W1P_CLOBBERS")
+    txt.append("#define LTX_DKDV_W1P_CLOBBERS " + p_clobbers(diag) + "\n")
+    VARIANT.clear()
     txt += [f"#define LTX_DQ_W1_BUF {D_BUF}", define("LTX_DQ_W1_BODY", dq_body())]
     if diag:
         for k, var in enumerate(("stamps", "stamps+novalu"), 1):
@@ -752,7 +1284,17 @@ def main():
             VARIANT.update(var.split("+"))
             txt.append(define(f"LTX_DQ_W1_BODY_V{k}", dq_body()))
         VARIANT.clear()
+        txt.append("#undef LTX_DQ_W1_CLOBBERS")
     txt.append("#define LTX_DQ_W1_CLOBBERS " + dq_clobbers(diag) + "\n")
+    VARIANT.clear()
+    txt += [f"#define LTX_DQ_W1P_STG {DP_STG}", f"#define LTX_DQ_W1P_TAB {DP_TAB}",
+            define("LTX_DQ_W1P_BODY", dq_p_body())]
+    if diag:
+        VARIANT.update({"stamps"})
+        txt.append(define("LTX_DQ_W1P_BODY_V1", dq_p_body()))
+        VARIANT.clear()
+        txt.append("#undef LTX_DQ_W1P_CLOBBERS")
+    txt.append("#define LTX_DQ_W1P_CLOBBERS " + dqp_clobbers(diag) + "\n")
     open(out, "w").write("\n".join(txt))
     print(out, len(L), "lines")
 

@@ -1187,6 +1187,9 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
     if (needs_bias(p)) {
       hipLaunchKernelGGL((attn_q_kernel<HD, 1, true>), gq, dim3(ATT_THREADS), 0, s, p);
       LTX_LAUNCH_CHECK();
+    } else if (dq_w1p_enabled() && dq_w1p_applies(p)) {
+      const int rc = launch_dq_w1p(p, s);
+      if (rc != LTX_OK) return rc;
     } else if (dq_w1_enabled()) {
       const int rc = launch_dq_w1(p, s);
       if (rc != LTX_OK) return rc;
@@ -1197,6 +1200,7 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
       hipLaunchKernelGGL((attn_q_kernel<HD, 1, false>), gq, dim3(ATT_THREADS), 0, s, p);
       LTX_LAUNCH_CHECK();
     }
+    if (!needs_bias(p) && dkdv_w1p_enabled() && dkdv_w1p_applies(p)) return launch_dkdv_w1p(p, s);
     if (!needs_bias(p) && dkdv_w1_enabled()) return launch_dkdv_w1(p, s);
     return launch_dkdv_pipe(p, s);
   }

@@ -298,6 +298,14 @@ bool dq_pipe_enabled();
 // the dK/dV kernel at one wave per SIMD (hand-scheduled loop, attn_bwd_body.h): no key bias, head dim 64
 int launch_dkdv_w1(const AttnParams& p, hipStream_t s);
 bool dkdv_w1_enabled();
+// the persistent dK/dV kernel (one workgroup per CU walking 256-key blocks; attn_bwd_body.h)
+int launch_dkdv_w1p(const AttnParams& p, hipStream_t s);
+bool dkdv_w1p_enabled();
+bool dkdv_w1p_applies(const AttnParams& p);
+// the persistent dQ kernel (one workgroup per CU walking 256-query blocks; bf16 dQ)
+int launch_dq_w1p(const AttnParams& p, hipStream_t s);
+bool dq_w1p_enabled();
+bool dq_w1p_applies(const AttnParams& p);
 // the dQ kernel at one wave per SIMD (hand-scheduled loop, attn_bwd_body.h): no key bias, head dim 64
 int launch_dq_w1(const AttnParams& p, hipStream_t s);
 bool dq_w1_enabled();

@@ -354,8 +354,28 @@ __device__ __forceinline__ u32x4 raw_srd(const void* base, uint64_t bytes) {
   return d;
 }
 
+// diagnostic builds: shader-clock (s_memtime) and 100-MHz (s_memrealtime) stamps of a wave at kernel
+// entry and exit, 4 u64 per wave after the 8 phase stamps of every wave (tools/dkdv_stamps.py)
+typedef uint64_t u64x4 __attribute__((ext_vector_type(4)));
+struct EdgeStamps {
+  uint64_t t0 = 0, r0 = 0;
+  __device__ __forceinline__ void start() {
+    t0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  __device__ __forceinline__ void stop(const AttnParams& p) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    const int64_t nw = (int64_t)gridDim.x * gridDim.y * gridDim.z * 4;
+    const int64_t w = (blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z)) * 4 +
+                      (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0) *(u64x4*)((uint64_t*)p.part + nw * 8 + w * 4) = (u64x4){t0, r0, t1, r1};
+  }
+};
+
 template <int V>
 __global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p) {
+  EdgeStamps es;
+  if constexpr (V > 0) es.start();
   constexpr int HD = PHD;
   // the ring (3 x LTX_DKDV_W1_BUF B); after the loop the epilogue's dK / dV staging
   __shared__ __attribute__((aligned(16))) char smem[LTX_DKDV_W1_NBUF * LTX_DKDV_W1_BUF];
@@ -439,6 +459,7 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p
                          p.lddv, kb, nk, lane);
     }
   }
+  if constexpr (V > 0) es.stop(p);
 }
 
 // LTX_ATTN_DKDV_W1 (read per call): unset / 1 the one-wave-per-SIMD kernel, 0 attn_dkdv_pipe_kernel,
@@ -448,6 +469,8 @@ static int dkdv_w1_mode() {
   return e ? std::atoi(e) : 1;
 }
 bool dkdv_w1_enabled() { return dkdv_w1_mode() != 0; }
+// LTX_ATTN_DKDV_W1=2 (22: its stamped diagnostic variant): the persistent kernel
+bool dkdv_w1p_enabled() { return dkdv_w1_mode() == 2 || dkdv_w1_mode() == 22; }
 
 int launch_dkdv_w1(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nk + W1_KEYS - 1) / W1_KEYS), (unsigned)p.H, (unsigned)p.B);
@@ -457,7 +480,7 @@ int launch_dkdv_w1(const AttnParams& p, hipStream_t s) {
     AttnParams q = p;
     size_t ws = 0;
     q.part = stream_workspace(s, &ws);
-    if (q.part == nullptr || ws < (size_t)g.x * g.y * g.z * 4 * 8 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
+    if (q.part == nullptr || ws < (size_t)g.x * g.y * g.z * 4 * 12 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
     if (mode == 12) hipLaunchKernelGGL(attn_dkdv_w1_kernel<1>, g, dim3(256), 0, s, q);
     if (mode == 13) hipLaunchKernelGGL(attn_dkdv_w1_kernel<2>, g, dim3(256), 0, s, q);
     if (mode == 14) hipLaunchKernelGGL(attn_dkdv_w1_kernel<3>, g, dim3(256), 0, s, q);
@@ -474,6 +497,160 @@ int launch_dkdv_w1(const AttnParams& p, hipStream_t s) {
 }
 
 // =============================================================================================
+// dK / dV, PERSISTENT (attn_bwd_body.h LTX_DKDV_W1P_BODY, tools/gen_attn_bwd.py dkdv_p_body): one
+// workgroup per CU walks the items L = blockIdx.x + i * gridDim.x (a 256-key block of one (batch,
+// head), in attn_dkdv_w1_kernel's XCD-aware order), the loads of item i+1 overlapping the tail and the
+// stores of item i. Per item the same loop as attn_dkdv_w1_kernel: dK / dV bitwise equal to it.
+// =============================================================================================
+namespace {
+constexpr int W1P_MAXIT = 63;  // items per workgroup (table rows, + the null row)
+constexpr int W1P_LDS = LTX_DKDV_W1P_TAB + (W1P_MAXIT + 1) * LTX_DKDV_W1P_ITEM;
+}
+
+// buffer descriptor words of [base, base + bytes) (stride 0; loads past `bytes` return zeros)
+__device__ __forceinline__ void srd_words(uint32_t* w, const void* base, uint64_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  w[0] = (uint32_t)a;
+  w[1] = (uint32_t)(a >> 32) & 0xffffu;
+  w[2] = (uint32_t)(bytes > 0xffffffffull ? 0xffffffffull : bytes);
+  w[3] = 0x00020000u;
+}
+__device__ __forceinline__ void base_words(uint32_t* w, const void* base) {
+  const uint64_t a = (uint64_t)base;
+  w[0] = (uint32_t)a;
+  w[1] = (uint32_t)(a >> 32) & 0xffffu;
+}
+
+// item L of I -> (block x, head, batch): xcd_block's bijective remap with L as the block id (the
+// workgroups of XCD x run the items L = x mod 8 when the grid is a multiple of 8 or every item has
+// its own workgroup), so each XCD walks a contiguous range of the (x fastest, head, batch) order
+__device__ __forceinline__ void item_coords(int L, int I, int gx, int gy, int xcd_order, int& bx, int& by, int& bz) {
+  int wg = L;
+  if (xcd_order) {
+    const int q = I / 8, r = I % 8, xcd = L % 8, idx = L / 8;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+  }
+  bx = wg % gx;
+  by = (wg / gx) % gy;
+  bz = wg / (gx * gy);
+}
+
+template <int V>
+__global__ __launch_bounds__(256, 1) void attn_dkdv_w1p_kernel(const AttnParams p) {
+  constexpr int HD = PHD;
+  EdgeStamps es;
+  if constexpr (V > 0) es.start();
+  __shared__ __attribute__((aligned(16))) char smem[W1P_LDS];  // ring | staging | item table
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  const int gx = (p.Nk + W1_KEYS - 1) / W1_KEYS, I = gx * p.H * p.B, G = gridDim.x, w = blockIdx.x;
+  const int nit = (I - w + G - 1) / G;  // >= 1: the launch has G <= I
+  if (tid <= nit) {  // row tid: item tid; row nit: the null row (empty K / V descriptors)
+    int bx, hh, b;
+    item_coords(w + min(tid, nit - 1) * G, I, gx, p.H, p.xcd_order, bx, hh, b);
+    const int k0 = bx * W1_KEYS, nk = min(W1_KEYS, p.Nk - k0);
+    const bool null = tid == nit;
+    uint32_t* row = (uint32_t*)(smem + LTX_DKDV_W1P_TAB + tid * LTX_DKDV_W1P_ITEM);
+    srd_words(row, p.k + ((int64_t)b * p.kvb + k0) * p.ldk + hh * HD, null ? 0 : ((uint64_t)(nk - 1) * p.ldk + HD) * 2);
+    srd_words(row + 4, p.v + ((int64_t)b * p.kvb + k0) * p.ldv + hh * HD, null ? 0 : ((uint64_t)(nk - 1) * p.ldv + HD) * 2);
+    base_words(row + 8, p.q + (int64_t)b * p.Nq * p.ldq + hh * HD);
+    base_words(row + 10, p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD);
+    base_words(row + 12, p.lse + ((int64_t)b * p.H + hh) * p.Nq);
+    base_words(row + 14, p.delta + ((int64_t)b * p.H + hh) * p.Nq);
+    srd_words(row + 16, p.dk + ((int64_t)b * p.Nk + k0) * p.lddk + hh * HD, ((uint64_t)(nk - 1) * p.lddk + HD) * 2);
+    srd_words(row + 20, p.dv + ((int64_t)b * p.Nk + k0) * p.lddv + hh * HD, ((uint64_t)(nk - 1) * p.lddv + HD) * 2);
+  }
+  __syncthreads();
+  // sizes (words 2, 3) of the Q, dO and stats descriptors: the same for every item
+  // (< 4 GiB: dkdv_w1p_applies)
+  const uint32_t sq2 = __builtin_amdgcn_readfirstlane((uint32_t)(((p.Nq - 1) * (uint32_t)p.ldq + HD) * 2));
+  const uint32_t so2 = __builtin_amdgcn_readfirstlane((uint32_t)(((p.Nq - 1) * (uint32_t)p.lddo + HD) * 2));
+  const uint32_t ss2 = __builtin_amdgcn_readfirstlane((uint32_t)(p.Nq * 4));
+  const uint32_t wst = __builtin_amdgcn_readfirstlane(2 * P_TILE + (wave < 2 ? wave * P_STAT : 2 * P_STAT));
+  uint32_t vq[2], vo[2], vk[2], vv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
+    vq[i] = (uint32_t)(row * p.ldq + c * 8) * 2;
+    vo[i] = (uint32_t)(row * p.lddo + c * 8) * 2;
+    const int key = wave * 64 + i * 32 + (lane & 31);  // fragment rows of key tile i
+    vk[i] = (uint32_t)(key * p.ldk + 8 * h) * 2;
+    vv[i] = (uint32_t)(key * p.ldv + 8 * h) * 2;
+  }
+  const uint32_t vl = (uint32_t)lane * 4, vs = (uint32_t)(16 * h);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
+  const uint32_t tab = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DKDV_W1P_TAB));
+  const uint32_t stg = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DKDV_W1P_STG) + wave * 16384);
+  const uint32_t wq = __builtin_amdgcn_readfirstlane(wave * 2048);
+  const uint32_t qstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldq * 2));
+  const uint32_t ostep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.lddo * 2));
+  const uint32_t iters = __builtin_amdgcn_readfirstlane((uint32_t)((p.Nq + 63) / 64 - 1));
+  const uint32_t nitems = __builtin_amdgcn_readfirstlane((uint32_t)nit);
+  const uint32_t wodd = __builtin_amdgcn_readfirstlane((uint32_t)(wave & 1));
+  const uint32_t s8dk = __builtin_amdgcn_readfirstlane((uint32_t)(16 * p.lddk)), s8dv = __builtin_amdgcn_readfirstlane((uint32_t)(16 * p.lddv));
+  // staging: this lane's write base (row lane & 31, half h) and read base (row lane >> 3, chunk lane & 7)
+  const uint32_t vwd = (uint32_t)((lane & 31) * 128 + h * 8);
+  const uint32_t vrd = stg + (uint32_t)((lane >> 3) * 128 + (((lane & 7) ^ ((lane >> 3) & 7)) << 4));
+  const uint32_t vdk = (uint32_t)(((wave * 64 + (lane >> 3)) * p.lddk + (lane & 7) * 8) * 2);
+  const uint32_t vdv = (uint32_t)(((wave * 64 + (lane >> 3)) * p.lddv + (lane & 7) * 8) * 2);
+  const float c2 = p.scale * LOG2E, scale = p.scale;
+  uint64_t* stp = (uint64_t*)p.part + ((int64_t)blockIdx.x * 4 + wave) * 8;  // diagnostic builds only
+#define LTX_W1P_OPERANDS                                                                                     \
+  ::[sq2] "s"(sq2), [so2] "s"(so2), [ss2] "s"(ss2), [qstep] "s"(qstep), [ostep] "s"(ostep), [lds0] "s"(lds0),  \
+    [wq] "s"(wq), [wst] "s"(wst), [iters] "s"(iters), [c2] "s"(c2), [tab] "s"(tab), [nitems] "s"(nitems),       \
+    [wodd] "s"(wodd), [scale] "s"(scale), [s8dk] "s"(s8dk), [s8dv] "s"(s8dv), [stg] "s"(stg),                   \
+    [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]), [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]),             \
+    [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]), [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]),     \
+    [vs] "v"(vs), [vq0] "v"(vq[0]), [vq1] "v"(vq[1]), [vo0] "v"(vo[0]), [vo1] "v"(vo[1]), [vl] "v"(vl),         \
+    [vk0] "v"(vk[0]), [vk1] "v"(vk[1]), [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), [vwd] "v"(vwd), [vrd] "v"(vrd),      \
+    [vdk] "v"(vdk), [vdv] "v"(vdv), [stp] "v"(stp)                                                              \
+      : "memory", "scc", "vcc", LTX_DKDV_W1P_CLOBBERS
+  if constexpr (V == 0) asm volatile(LTX_DKDV_W1P_BODY LTX_W1P_OPERANDS);
+#ifdef LTX_DKDV_DIAG
+  if constexpr (V == 1) asm volatile(LTX_DKDV_W1P_BODY_V1 LTX_W1P_OPERANDS);
+#endif
+#undef LTX_W1P_OPERANDS
+  if constexpr (V > 0) es.stop(p);
+}
+
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+// the persistent kernel applies when every workgroup's items fit its table
+bool dkdv_w1p_applies(const AttnParams& p) {
+  const int64_t I = (int64_t)((p.Nk + W1_KEYS - 1) / W1_KEYS) * p.H * p.B;
+  const uint64_t span = (uint64_t)p.Nq * (uint64_t)std::max<int64_t>(p.ldq, p.lddo) * 2;  // Q / dO descriptor sizes
+  return I <= (int64_t)W1P_MAXIT * cu_count() && span < 0xffffffffull;
+}
+
+int launch_dkdv_w1p(const AttnParams& p, hipStream_t s) {
+  const int I = ((p.Nk + W1_KEYS - 1) / W1_KEYS) * p.H * p.B;
+  const dim3 g((unsigned)min(I, cu_count()));
+#ifdef LTX_DKDV_DIAG
+  if (dkdv_w1_mode() == 22) {
+    AttnParams q = p;
+    size_t ws = 0;
+    q.part = stream_workspace(s, &ws);
+    if (q.part == nullptr || ws < (size_t)g.x * 4 * 12 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
+    hipLaunchKernelGGL(attn_dkdv_w1p_kernel<1>, g, dim3(256), 0, s, q);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+#endif
+  hipLaunchKernelGGL(attn_dkdv_w1p_kernel<0>, g, dim3(256), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+// =============================================================================================
 // dQ at ONE wave per SIMD (self-attention shapes: no key bias, head dim 64): 4 waves x 64 queries
 // (two 32-query tiles per wave) = 256 queries per workgroup, the loop one hand-scheduled asm
 // statement (attn_bwd_body.h LTX_DQ_W1_BODY, tools/gen_attn_bwd.py dq_body). Same arithmetic and
@@ -481,6 +658,8 @@ int launch_dkdv_w1(const AttnParams& p, hipStream_t s) {
 // =============================================================================================
 template <int V>
 __global__ __launch_bounds__(256, 1) void attn_dq_w1_kernel(const AttnParams p) {
+  EdgeStamps es;
+  if constexpr (V > 0) es.start();
   constexpr int HD = PHD;
   __shared__ __attribute__((aligned(16))) char smem[3 * LTX_DQ_W1_BUF];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
@@ -550,6 +729,7 @@ __global__ __launch_bounds__(256, 1) void attn_dq_w1_kernel(const AttnParams p) 
         store_rows_lds<HD>(smem + wave * 4096, acc[qt], p.scale, (bf16_t*)p.dq + (int64_t)b * p.Nq * p.lddq + hh * HD,
                            p.lddq, qb, min(32, p.Nq - qb), lane);
     }
+    if constexpr (V > 0) es.stop(p);
     return;
   }
 #pragma unroll
@@ -568,6 +748,112 @@ __global__ __launch_bounds__(256, 1) void attn_dq_w1_kernel(const AttnParams p) 
   }
 }
 
+// =============================================================================================
+// dQ, PERSISTENT (attn_bwd_body.h LTX_DQ_W1P_BODY, tools/gen_attn_bwd.py dq_p_body): one workgroup per
+// CU walks 256-query blocks as attn_dkdv_w1p_kernel walks key blocks; per block attn_dq_w1_kernel's
+// loop (dQ bitwise equal to it). bf16 dQ only (the f32 output stays on attn_dq_w1_kernel).
+// =============================================================================================
+static int dq_w1_mode();
+namespace {
+constexpr int DQP_LDS = LTX_DQ_W1P_TAB + (W1P_MAXIT + 1) * LTX_DKDV_W1P_ITEM;
+}
+
+template <int V>
+__global__ __launch_bounds__(256, 1) void attn_dq_w1p_kernel(const AttnParams p) {
+  constexpr int HD = PHD;
+  EdgeStamps es;
+  if constexpr (V > 0) es.start();
+  __shared__ __attribute__((aligned(16))) char smem[DQP_LDS];  // ring | staging | item table
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  const int gx = (p.Nq + 255) / 256, I = gx * p.H * p.B, G = gridDim.x, w = blockIdx.x;
+  const int nit = (I - w + G - 1) / G;
+  if (tid <= nit) {  // row tid: block tid; row nit: the null row (empty Q / dO / stats descriptors)
+    int bx, hh, b;
+    item_coords(w + min(tid, nit - 1) * G, I, gx, p.H, p.xcd_order, bx, hh, b);
+    const int q0 = bx * 256, nq = min(256, p.Nq - q0);
+    const bool null = tid == nit;
+    uint32_t* row = (uint32_t*)(smem + LTX_DQ_W1P_TAB + tid * LTX_DKDV_W1P_ITEM);
+    const int64_t st = ((int64_t)b * p.H + hh) * p.Nq + q0;
+    srd_words(row, p.q + ((int64_t)b * p.Nq + q0) * p.ldq + hh * HD, null ? 0 : ((uint64_t)(nq - 1) * p.ldq + HD) * 2);
+    srd_words(row + 4, p.dout + ((int64_t)b * p.Nq + q0) * p.lddo + hh * HD, null ? 0 : ((uint64_t)(nq - 1) * p.lddo + HD) * 2);
+    srd_words(row + 8, p.lse + st, null ? 0 : (uint64_t)nq * 4);
+    srd_words(row + 12, p.delta + st, null ? 0 : (uint64_t)nq * 4);
+    base_words(row + 16, p.k + (int64_t)b * p.kvb * p.ldk + hh * HD);
+    base_words(row + 18, p.v + (int64_t)b * p.kvb * p.ldv + hh * HD);
+    srd_words(row + 20, (bf16_t*)p.dq + ((int64_t)b * p.Nq + q0) * p.lddq + hh * HD, ((uint64_t)(nq - 1) * p.lddq + HD) * 2);
+  }
+  __syncthreads();
+  const uint32_t sk2 = __builtin_amdgcn_readfirstlane((uint32_t)(((p.Nk - 1) * (uint32_t)p.ldk + HD) * 2));
+  const uint32_t sv2 = __builtin_amdgcn_readfirstlane((uint32_t)(((p.Nk - 1) * (uint32_t)p.ldv + HD) * 2));
+  uint32_t vk[2], vv[2], vq[2], vo[2], vs[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
+    vk[i] = (uint32_t)(row * p.ldk + c * 8) * 2;
+    vv[i] = (uint32_t)(row * p.ldv + c * 8) * 2;
+    const int qr = wave * 64 + i * 32 + (lane & 31);  // the lane's query in query tile i
+    vq[i] = (uint32_t)(qr * p.ldq + 8 * h) * 2;
+    vo[i] = (uint32_t)(qr * p.lddo + 8 * h) * 2;
+    vs[i] = (uint32_t)qr * 4;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
+  const uint32_t tab = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DQ_W1P_TAB));
+  const uint32_t stg = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DQ_W1P_STG) + wave * 8192);
+  const uint32_t wq = __builtin_amdgcn_readfirstlane(wave * 2048);
+  const uint32_t kstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldk * 2));
+  const uint32_t vstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldv * 2));
+  const uint32_t iters = __builtin_amdgcn_readfirstlane((uint32_t)((p.Nk + 63) / 64 - 1));
+  const uint32_t nitems = __builtin_amdgcn_readfirstlane((uint32_t)nit);
+  const uint32_t s8dq = __builtin_amdgcn_readfirstlane((uint32_t)(16 * p.lddq));
+  const uint32_t vwd = (uint32_t)((lane & 31) * 128 + h * 8);
+  const uint32_t vrd = stg + (uint32_t)((lane >> 3) * 128 + (((lane & 7) ^ ((lane >> 3) & 7)) << 4));
+  const uint32_t vdq = (uint32_t)(((wave * 64 + (lane >> 3)) * p.lddq + (lane & 7) * 8) * 2);
+  const float c2 = p.scale * LOG2E, scale = p.scale;
+  uint64_t* stp = (uint64_t*)p.part + ((int64_t)blockIdx.x * 4 + wave) * 8;  // diagnostic builds only
+#define LTX_DQP_OPERANDS                                                                                       \
+  ::[sk2] "s"(sk2), [sv2] "s"(sv2), [kstep] "s"(kstep), [vstep] "s"(vstep), [lds0] "s"(lds0), [wq] "s"(wq),    \
+    [iters] "s"(iters), [c2] "s"(c2), [tab] "s"(tab), [nitems] "s"(nitems), [scale] "s"(scale), [s8dq] "s"(s8dq), \
+    [stg] "s"(stg), [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]), [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]), \
+    [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]), [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]),       \
+    [vk0] "v"(vk[0]), [vk1] "v"(vk[1]), [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), [vq0] "v"(vq[0]), [vq1] "v"(vq[1]),    \
+    [vo0] "v"(vo[0]), [vo1] "v"(vo[1]), [vs0] "v"(vs[0]), [vs1] "v"(vs[1]), [vwd] "v"(vwd), [vrd] "v"(vrd),        \
+    [vdq] "v"(vdq), [stp] "v"(stp)                                                                                \
+      : "memory", "scc", "vcc", LTX_DQ_W1P_CLOBBERS
+  if constexpr (V == 0) asm volatile(LTX_DQ_W1P_BODY LTX_DQP_OPERANDS);
+#ifdef LTX_DKDV_DIAG
+  if constexpr (V == 1) asm volatile(LTX_DQ_W1P_BODY_V1 LTX_DQP_OPERANDS);
+#endif
+#undef LTX_DQP_OPERANDS
+  if constexpr (V > 0) es.stop(p);
+}
+
+bool dq_w1p_applies(const AttnParams& p) {
+  const int64_t I = (int64_t)((p.Nq + 255) / 256) * p.H * p.B;
+  const uint64_t span = (uint64_t)p.Nk * (uint64_t)std::max<int64_t>(p.ldk, p.ldv) * 2;  // K / V descriptor sizes
+  return !p.dq_f32 && I <= (int64_t)W1P_MAXIT * cu_count() && span < 0xffffffffull;
+}
+
+int launch_dq_w1p(const AttnParams& p, hipStream_t s) {
+  const int I = ((p.Nq + 255) / 256) * p.H * p.B;
+  const dim3 g((unsigned)min(I, cu_count()));
+#ifdef LTX_DKDV_DIAG
+  if (dq_w1_mode() == 22) {
+    AttnParams q = p;
+    size_t ws = 0;
+    q.part = stream_workspace(s, &ws);
+    if (q.part == nullptr || ws < (size_t)g.x * 4 * 12 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
+    hipLaunchKernelGGL(attn_dq_w1p_kernel<1>, g, dim3(256), 0, s, q);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+#endif
+  hipLaunchKernelGGL(attn_dq_w1p_kernel<0>, g, dim3(256), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
 // LTX_ATTN_DQ_W1 (read per call): unset / 1 the one-wave kernel, 0 attn_dq_pipe_kernel, 12 / 13 the
 // stamped diagnostic variants (`make diag` builds)
 static int dq_w1_mode() {
@@ -575,6 +861,8 @@ static int dq_w1_mode() {
   return e ? std::atoi(e) : 1;
 }
 bool dq_w1_enabled() { return dq_w1_mode() != 0; }
+// LTX_ATTN_DQ_W1=2 (22: its stamped diagnostic variant): the persistent kernel
+bool dq_w1p_enabled() { return dq_w1_mode() == 2 || dq_w1_mode() == 22; }
 
 int launch_dq_w1(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nq + 255) / 256), (unsigned)p.H, (unsigned)p.B);
@@ -584,7 +872,7 @@ int launch_dq_w1(const AttnParams& p, hipStream_t s) {
     AttnParams q = p;
     size_t ws = 0;
     q.part = stream_workspace(s, &ws);
-    if (q.part == nullptr || ws < (size_t)g.x * g.y * g.z * 4 * 8 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
+    if (q.part == nullptr || ws < (size_t)g.x * g.y * g.z * 4 * 12 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
     if (mode == 12) hipLaunchKernelGGL(attn_dq_w1_kernel<1>, g, dim3(256), 0, s, q);
     else hipLaunchKernelGGL(attn_dq_w1_kernel<2>, g, dim3(256), 0, s, q);
     LTX_LAUNCH_CHECK();
