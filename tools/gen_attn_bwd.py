@@ -471,74 +471,55 @@ def clobbers(diag):
 # Persistent dK / dV (attn_dkdv_w1p_kernel): one workgroup per CU walks its key blocks ("items") in ONE
 # asm statement. Per item: the body of attn_dkdv_w1_kernel (A(0), half 0, the tile loop, the two tail
 # halves), then the dK / dV stores from the accumulators (a[0:127], fixed: ACC_REG) through a wave-
-# private LDS staging area. The next item's K / V fragments (into KF and v[0:31]) are loaded during
-# the first tail half and its first two Q / dO tiles are DMA'd into the ring right after the last
-# half, so item i+1's loads fly while item i finishes and stores: the ~10k-cycle load burst that opens
-# every workgroup of the non-persistent kernel (tools/dkdv_stamps.py: prologue 10.7k of 89k cycles)
-# is hidden, and the round-to-round skew of 1792 short-lived workgroups disappears.
-# Item parameters come from a table the kernel writes into LDS before the statement: one 96-B row
-# per item (K / V descriptors, Q / dO / lse / delta bases, dK / dV descriptors) plus a null row whose
-# K / V descriptors are empty, so the last item's prefetch loads zeros.
+# private LDS staging area. Every load an item starts with is issued while the previous item runs:
+#   * its K / V rows go by LDS-DMA into a dedicated region (each wave its own 64 keys) right after the
+#     previous item has read its own fragments out of it -- a whole item (~50 us) ahead;
+#   * its first two Q / dO tiles go into the two ring buffers the previous item's tail no longer
+#     reads (tile T-2's and the past-the-end one) before that tail's two halves and the stores.
+# The non-persistent kernel waits ~10k of its ~89k cycles per workgroup on these loads (stamps), and
+# 1792 short-lived workgroups add round-to-round skew.
+# Item parameters come from a table the kernel writes into LDS before the statement: one 96-B row per
+# item (K / V descriptors, Q / dO / lse / delta bases, dK / dV descriptors) plus a null row (empty
+# K / V descriptors: the last item's K / V prefetch writes zeros nobody reads).
 # =============================================================================================
-P_STG = NBUF * W_BUF                 # staging: 4 waves x 16 KiB ([kt][dK | dV], 4 KiB each)
-P_TAB = P_STG + 4 * 16384            # the item table
+P_KV = NBUF * W_BUF                  # K / V prefetch region: [256 keys][128 B] K, then V
+P_STG = P_KV + 2 * 32768             # staging: 4 waves x 8 KiB (dK | dV of one key tile)
+P_TAB = P_STG + 4 * 8192             # the item table
 ITEM_B = 96
-SK, SV, SDK, SDV = 40, 44, 48, 52    # descriptors: the item's K / V rows, its dK / dV block
-SLSE, SDLT = 56, 58                  # stats bases from the table (lse / delta: one per wave)
+SK, SV, SDK, SDV = 40, 44, 48, 52    # next item's K / V descriptors (then its Q / dO / lse / delta
+#                                      bases), this item's dK / dV descriptors
 SITEM = 39                           # items left
 TABV = 226                           # LDS address of the current item's table row (uniform)
-PRM = 66                             # v[66:81]: table reads (set 0's dP' tiles: free in the tail)
+PRM = 66                             # v[66:89]: table reads (free at an item's start)
 P_VLAST = 226
 
 
-def p_params_next(first):
-    """read a table row (the next one, or row 0 in the prologue) into K / V descriptors and the Q / dO /
-    stats descriptors' bases: [(reads as I)], [(readfirstlane + descriptor lines as I needing them)]"""
-    off = 0 if first else ITEM_B
-    rd = [I(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{off + 16 * i}", makes="PRM") for i in range(4)]
-    use = []
-    for i in range(4):
-        use.append(I(f"v_readfirstlane_b32 s{SK + i}, {v(PRM + i)}", needs=["PRM"]))
-        use.append(I(f"v_readfirstlane_b32 s{SV + i}, {v(PRM + 4 + i)}", needs=["PRM"]))
-    for srd, w in ((SRDQ, 8), (SRDO, 10), (SLSE, 12), (SDLT, 14)):
-        use.append(I(f"v_readfirstlane_b32 s{srd}, {v(PRM + w)}", needs=["PRM"]))
-        use.append(I(f"v_readfirstlane_b32 s{srd + 1}, {v(PRM + w + 1)}", needs=["PRM"]))
-    return rd, use
-
-
-def p_srd_reset():
-    """the Q / dO / stats descriptors' sizes (shrunk by the previous item's loop) and this wave's stats base"""
-    return [f"s_mov_b32 s{SRDQ + 2}, %[sq2]", f"s_mov_b32 s{SRDQ + 3}, 0x20000",
-            f"s_mov_b32 s{SRDO + 2}, %[so2]", f"s_mov_b32 s{SRDO + 3}, 0x20000",
-            f"s_mov_b32 s{SRDS + 2}, %[ss2]", f"s_mov_b32 s{SRDS + 3}, 0x20000",
-            "s_cmp_eq_u32 %[wodd], 0",
-            f"s_cselect_b64 s[{SRDS}:{SRDS + 1}], s[{SLSE}:{SLSE + 1}], s[{SDLT}:{SDLT + 1}]"]
-
-
-def p_kv_loads():
-    """the item's K fragments into KF, its V fragments into v[0:31] (negated into VF at the item start)"""
+def p_kv_dma():
+    """the next item's K / V rows of this wave (keys 64 w .. 64 w + 63, 8 pieces each) into the K / V
+    region: piece i = rows 8 i + (lane >> 3), chunk swizzled as the ring tiles (vkd / vvd: even / odd
+    pieces' lane offsets, rows stepped by soffset)"""
     out = []
-    for kt in range(2):
-        for ks in range(4):
-            out.append(f"buffer_load_dwordx4 {a_(KF(kt, ks), 4)}, %[vk{kt}], s[{SK}:{SK + 3}], 0 offen offset:{ks * 32}")
-            out.append(f"buffer_load_dwordx4 {v(16 * kt + 4 * ks, 4)}, %[vv{kt}], s[{SV}:{SV + 3}], 0 offen offset:{ks * 32}")
+    for which, srd, vo, s8, reg in (("k", SK, "%[vkd", "%[s8k]", 0), ("v", SV, "%[vvd", "%[s8v]", 32768)):
+        for i in range(8):
+            out += [f"s_mul_i32 s{STMP}, {s8}, {i}",
+                    f"s_add_u32 m0, %[kvw], {reg + 1024 * i}",
+                    "s_nop 0",
+                    f"buffer_load_dwordx4 {vo}{i & 1}], s[{srd}:{srd + 3}], s{STMP} offen lds"]
     return out
 
 
-def p_dma_first_tiles():
-    """the item's Q / dO tiles 0 and 1 into ring buffers 0 and 1 (descriptors advanced past them)"""
-    out = [f"s_mov_b32 s{SB0}, %[lds0]", f"s_add_u32 s{SB1}, %[lds0], {W_BUF}", f"s_add_u32 s{SBD}, %[lds0], {2 * W_BUF}"]
-    for buf in (SB0, SB1):
-        out.append(f"s_add_u32 s{STMP}, s{buf}, %[wq]")
-        for m0, ld in dma_pieces(buf):
-            out += [m0, "s_nop 0", ld]
-        out += advance_srds()
-    return out
+def p_tile_dma(buf, tile):
+    """the next item's Q / dO tile (0 or 1) into ring buffer `buf` (descriptors advanced past it)"""
+    out = [f"s_add_u32 s{STMP}, s{buf}, %[wq]"]
+    for m0, ld in dma_pieces(buf):
+        out += [m0, "s_nop 0", ld]
+    return out + advance_srds()
 
 
 def p_epilogue(E):
-    """dK (x scale) / dV of the item from the accumulators: bf16 rows through this wave's staging area
-    (16-B chunks XOR row & 7, as store_rows_lds), then buffer stores clipped to the block's valid keys"""
+    """dK (x scale) / dV of the item from the accumulators, one key tile per pass: bf16 rows through
+    this wave's staging area (16-B chunks XOR row & 7, as store_rows_lds), then buffer stores clipped
+    to the block's valid keys"""
     a = E.raw
     a("s_nop 15")
     a("s_nop 15")  # the last C MFMAs -> accvgpr reads
@@ -549,7 +530,7 @@ def p_epilogue(E):
     a(f"v_add_u32 {v(WB)}, %[stg], %[vwd]")
     for kt in range(2):
         for ti, kind in enumerate(("dk", "dv")):
-            stage = (2 * kt + ti) * 4096
+            stage = ti * 4096
             for d in range(2):
                 base = ACC_REG(kind, kt, d)
                 for r in range(16):
@@ -567,20 +548,15 @@ def p_epilogue(E):
                     a(f"v_xor_b32 {v(wt)}, {c}, {v(WX)}")
                     a(f"v_lshl_add_u32 {v(wt)}, {v(wt)}, 4, {v(WB)}")
                     a(f"ds_write_b64 {v(wt)}, {v(wd, 2)} offset:{stage}")
-    a("s_waitcnt lgkmcnt(0)")
-    for kt in range(2):
+        a("s_waitcnt lgkmcnt(0)")
         for ti in range(2):
-            stage = (2 * kt + ti) * 4096
-            dst = (32, 98)[ti] + 16 * kt
             for i in range(4):
-                a(f"ds_read_b128 {v(dst + 4 * i, 4)}, %[vrd] offset:{stage + 1024 * i}")
-    a("s_waitcnt lgkmcnt(0)")
-    for kt in range(2):
+                a(f"ds_read_b128 {v(32 + 16 * ti + 4 * i, 4)}, %[vrd] offset:{ti * 4096 + 1024 * i}")
+        a("s_waitcnt lgkmcnt(0)")
         for ti, (srd, vo, s8) in enumerate(((SDK, "%[vdk]", "%[s8dk]"), (SDV, "%[vdv]", "%[s8dv]"))):
-            dst = (32, 98)[ti] + 16 * kt
             for i in range(4):
                 a(f"s_mul_i32 s{STMP}, {s8}, {4 * kt + i}")
-                a(f"buffer_store_dwordx4 {v(dst + 4 * i, 4)}, {vo}, s[{srd}:{srd + 3}], s{STMP} offen")
+                a(f"buffer_store_dwordx4 {v(32 + 16 * ti + 4 * i, 4)}, {vo}, s[{srd}:{srd + 3}], s{STMP} offen")
 
 
 def dkdv_p_body():
@@ -594,39 +570,83 @@ def dkdv_p_body():
 def _dkdv_p_body():
     E = Emitter()
     a = E.raw
+
+    def rfl(dst, src):
+        a(f"v_readfirstlane_b32 s{dst}, {v(src)}")
+
     a("s_nop 4")
     a(f"s_mov_b32 s{SKEEP}, m0")
     a(f"v_mov_b32 {v(TABV)}, %[tab]")
     a(f"s_mov_b32 s{SITEM}, %[nitems]")
-    # ---- item 0: parameters, fragments, tiles 0 and 1 ----------------------------------------------
-    rd, use = p_params_next(True)
-    for ins in rd + use:
-        E.put(ins)
-    E.drain("s_waitcnt lgkmcnt(0)")
-    for i in range(2):  # item 0's dK / dV descriptors
-        a(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{64 + 16 * i}")
+    # ---- item 0: its K / V rows, its tiles 0 and 1 -------------------------------------------------
+    for i in range(4):
+        a(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{16 * i}")
     a("s_waitcnt lgkmcnt(0)")
     for i in range(4):
-        a(f"v_readfirstlane_b32 s{SDK + i}, {v(PRM + i)}")
-        a(f"v_readfirstlane_b32 s{SDV + i}, {v(PRM + 4 + i)}")
-    for t in p_srd_reset():
-        a(t)
+        rfl(SK + i, PRM + i)
+        rfl(SV + i, PRM + 4 + i)
+    for srd, w in ((SRDQ, 8), (SRDO, 10)):
+        rfl(srd, PRM + w)
+        rfl(srd + 1, PRM + w + 1)
+    rfl(SDK, PRM + 12)      # lse / delta bases (scratch: SDK is set at the item start)
+    rfl(SDK + 1, PRM + 13)
+    rfl(SDK + 2, PRM + 14)
+    rfl(SDK + 3, PRM + 15)
+    a(f"s_mov_b32 s{SRDQ + 2}, %[sq2]")
+    a(f"s_mov_b32 s{SRDQ + 3}, 0x20000")
+    a(f"s_mov_b32 s{SRDO + 2}, %[so2]")
+    a(f"s_mov_b32 s{SRDO + 3}, 0x20000")
+    a(f"s_mov_b32 s{SRDS + 2}, %[ss2]")
+    a(f"s_mov_b32 s{SRDS + 3}, 0x20000")
+    a("s_cmp_eq_u32 %[wodd], 0")
+    a(f"s_cselect_b64 s[{SRDS}:{SRDS + 1}], s[{SDK}:{SDK + 1}], s[{SDK + 2}:{SDK + 3}]")
     a("s_nop 4")  # SGPRs fresh from v_readfirstlane -> descriptors / M0
-    for t in p_kv_loads() + p_dma_first_tiles():
+    for t in p_kv_dma():
         a(t)
-    a("s_waitcnt vmcnt(5)")  # K, V and tile 0 landed (tile 1's five pieces may fly)
+    a(f"s_mov_b32 s{SB0}, %[lds0]")
+    a(f"s_add_u32 s{SB1}, %[lds0], {W_BUF}")
+    a(f"s_add_u32 s{SBD}, %[lds0], {2 * W_BUF}")
+    for t in p_tile_dma(SB0, 0) + p_tile_dma(SB1, 1):
+        a(t)
+    a("s_waitcnt vmcnt(0)")
     a("s_branch L_p_item_%=")
     a("L_p_next_%=:")
-    # the previous item left: K / V fragments (16), tiles 0, 1 (10 pieces), its dK / dV stores (16)
-    a("s_waitcnt vmcnt(21)")
+    # outstanding: the previous item's dK / dV stores (16) -- its K / V region fill (issued an item
+    # ago) and this item's tiles 0, 1 (issued at the previous tail) are older
+    a("s_waitcnt vmcnt(16)")
     a("L_p_item_%=:")
+    a("s_barrier")  # tiles 0, 1 complete in every wave
+    # ---- this item's K / V fragments from the region (the wave's own rows), its dK / dV
+    # descriptors, the next item's K / V descriptors and Q / dO / lse / delta bases --------------------
+    for ks in range(4):
+        a(f"v_add_u32 {v(RA[ks])}, %[kvw], %[vr{ks}]")
+    for kt in range(2):
+        for ks in range(4):
+            a(f"ds_read_b128 {a_(KF(kt, ks), 4)}, {v(RA[ks])} offset:{kt * 4096}")
+            a(f"ds_read_b128 {v(16 * kt + 4 * ks, 4)}, {v(RA[ks])} offset:{32768 + kt * 4096}")
+    for i in range(2):
+        a(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{64 + 16 * i}")
+    for i in range(4):
+        a(f"ds_read_b128 {v(PRM + 8 + 4 * i, 4)}, {v(TABV)} offset:{ITEM_B + 16 * i}")
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_nop 4")  # the previous item's stores read SDK / SDV at issue: rewrite after
+    for i in range(4):
+        rfl(SDK + i, PRM + i)
+        rfl(SDV + i, PRM + 4 + i)
+        rfl(SK + i, PRM + 8 + i)
+        rfl(SV + i, PRM + 12 + i)
+    a("s_nop 4")
+    for t in p_kv_dma():  # the next item's K / V rows (the null row's empty descriptors: zeros)
+        a(t)
+    a("s_nop 4")  # the DMA's descriptor reads before SK / SV take the next item's bases
+    for i in range(8):
+        rfl(SK + i, PRM + 16 + i)   # SK: Q base, dO base; SV: lse base, delta base
     for r in range(32):  # -V (sign flip, exact) into the accumulator file
         a(f"v_xor_b32 {v(r)}, 0x80008000, {v(r)}")
     for r in range(32):
         a(f"v_accvgpr_write_b32 {a_(160 + r)}, {v(r)}")
     for r in range(128):
         a(f"v_accvgpr_write_b32 {a_(r)}, 0")
-    a("s_barrier")
     for t in addr_regs("A", f"s{SB0}") + addr_regs("TN", f"s{SB0}"):
         a(t)
     for ins in a_reads(0) + lse_reads(0, LSEB[0]):
@@ -673,44 +693,34 @@ def _dkdv_p_body():
     a("L_p_tail_%=:")
     if "stamps" in VARIANT:
         a("s_memtime s[74:75]")
-    # ---- tail: half J-1 with the next item's parameters (slots 12-15, after B(J-2) freed set 0),
-    # descriptors (slots 20-23) and K / V fragment loads (slots 24-31) ------------------------------
-    plan = read_plan(None, TN, 1, None, None)
-    rd, use = p_params_next(False)
-    for i, x in enumerate(rd):
-        plan.setdefault(12 + i, []).append(x)
-    for i, x in enumerate(use):
-        plan.setdefault(20 + i // 6, []).append(x)
-    extra = {}
-    reset = p_srd_reset()
-    for i, t in enumerate(reset):
-        extra.setdefault(23 if i < 6 else 24, []).append(t)
-    extra.setdefault(24, []).append("s_nop 4")
-    for i, t in enumerate(p_kv_loads()):
-        extra.setdefault(25 + i // 3, []).append(t)
-    half(E, True, b_even, b_odd, None, plan, extra=extra)
-    half(E, True, b_odd, {}, None, {})
-    # ---- end of the item: ring free -> the next item's first tiles; the stores; the next dK / dV ----
-    E.drain("s_waitcnt lgkmcnt(0)")
+    # ---- tail start: the next item's tiles 0, 1 into SBD (the past-the-end DMA's buffer) and SB0
+    # (tile T-2: every wave past it after the barrier); the tail itself reads only SB1 -------------------
+    a("s_waitcnt vmcnt(0)")  # this wave's past-the-end tile DMA into SBD landed
+    E.drain("s_waitcnt lgkmcnt(15)", keep=15)
     a("s_barrier")
     a(f"s_cmp_eq_u32 s{SITEM}, 1")
     a("s_cbranch_scc1 L_p_nodma_%=")
-    # the loop's last (empty, past-the-end) tile DMA of this wave landed before its pieces of the
-    # next item's tiles 0 and 1 go into the same ring slots (the 16 fragment loads may fly)
-    a("s_waitcnt vmcnt(16)")
-    for t in p_dma_first_tiles():
+    for srd, w in ((SRDQ, SK), (SRDO, SK + 2)):
+        a(f"s_mov_b64 s[{srd}:{srd + 1}], s[{w}:{w + 1}]")
+    a(f"s_mov_b32 s{SRDQ + 2}, %[sq2]")
+    a(f"s_mov_b32 s{SRDO + 2}, %[so2]")
+    a(f"s_mov_b32 s{SRDS + 2}, %[ss2]")
+    a("s_cmp_eq_u32 %[wodd], 0")
+    a(f"s_cselect_b64 s[{SRDS}:{SRDS + 1}], s[{SV}:{SV + 1}], s[{SV + 2}:{SV + 3}]")
+    for t in p_tile_dma(SBD, 0) + p_tile_dma(SB0, 1):
         a(t)
     a("L_p_nodma_%=:")
+    half(E, True, b_even, b_odd, None, read_plan(None, TN, 1, None, None))
+    half(E, True, b_odd, {}, None, {})
+    E.drain("s_waitcnt lgkmcnt(0)")
     p_epilogue(E)
     a(f"s_cmp_eq_u32 s{SITEM}, 1")
     a("s_cbranch_scc1 L_p_done_%=")
-    a("s_nop 4")  # the stores' descriptor reads before the descriptors are rewritten
-    for i in range(2):
-        a(f"ds_read_b128 {v(PRM + 4 * i, 4)}, {v(TABV)} offset:{ITEM_B + 64 + 16 * i}")
-    a("s_waitcnt lgkmcnt(0)")
-    for i in range(4):
-        a(f"v_readfirstlane_b32 s{SDK + i}, {v(PRM + i)}")
-        a(f"v_readfirstlane_b32 s{SDV + i}, {v(PRM + 4 + i)}")
+    # the next item's ring: tile 0 in SBD, tile 1 in SB0, SB1 (tile T-1) free
+    a(f"s_mov_b32 s{STMP}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{STMP}")
     a(f"v_add_u32 {v(TABV)}, {ITEM_B}, {v(TABV)}")
     a(f"s_sub_u32 s{SITEM}, s{SITEM}, 1")
     a("s_branch L_p_next_%=")
@@ -996,65 +1006,50 @@ def dq_body():
 
 # =============================================================================================
 # Persistent dQ (attn_dq_w1p_kernel): one workgroup per CU walks its 256-query blocks in ONE asm
-# statement, as the persistent dK / dV kernel does: the next block's Q / dO fragments (into QF / OF),
-# lse and delta (v[0:3]) load in the first tail half, its first two K / V tiles right after the last
-# half, under the dQ stores of the block. Table row (96 B): Q, dO, lse, delta descriptors of the
-# block (sizes: its valid rows), K / V bases of the (batch, head), the dQ descriptor.
+# statement, as the persistent dK / dV kernel walks key blocks: each block's Q / dO rows, lse and delta
+# go by LDS-DMA into a dedicated region an item ahead (each wave its own 64 queries), its first two
+# K / V tiles into the ring buffers the previous block's tail no longer reads. Table row (96 B): the
+# Q, dO, lse, delta descriptors of the block (sizes: its valid rows), the K / V bases of the (batch,
+# head), the dQ descriptor.
 # =============================================================================================
-DP_STG = 3 * D_BUF                    # staging: 4 waves x 8 KiB ([qt] 4 KiB each)
-DP_TAB = DP_STG + 4 * 8192
+DP_QO = 3 * D_BUF                     # Q / dO prefetch region: [256][128 B] Q, then dO
+DP_ST = DP_QO + 2 * 32768             # lse [256] f32, then delta [256]
+DP_STG = DP_ST + 2048                 # staging: 4 waves x 4 KiB (dQ of one query tile)
+DP_TAB = DP_STG + 4 * 4096
 DNLR = 190                            # -lse of the lane's query in qt 0 / 1 (the B stream's fma)
 DP_TABV = 192
 DP_VLAST = 192
-DSQ, DSO, DSL, DSD_, DSDQ = 40, 44, 48, 52, 56   # descriptors of the block's Q, dO, lse, delta, dQ
+DSQ, DSO, DSL, DSD_, DSDQ = 40, 44, 48, 52, 56   # next block's Q, dO, lse, delta descriptors; this block's dQ
 DSITEM = 39
+DKB = 80                              # (the next block's K / V bases wait in SRDK / SRDV words 0, 1)
 
 
-def dqp_params_next(first):
-    """table row -> the Q / dO / lse / delta descriptors and the K / V descriptors' bases"""
-    off = 0 if first else ITEM_B
-    rd = [I(f"ds_read_b128 {v(66 + 4 * i, 4)}, {v(DP_TABV)} offset:{off + 16 * i}", makes="PRM") for i in range(5)]
-    use = []
-    for j, srd in enumerate((DSQ, DSO, DSL, DSD_)):
-        for i in range(4):
-            use.append(I(f"v_readfirstlane_b32 s{srd + i}, {v(66 + 4 * j + i)}", needs=["PRM"]))
-    for i in range(2):
-        use.append(I(f"v_readfirstlane_b32 s{SRDK + i}, {v(82 + i)}", needs=["PRM"]))
-        use.append(I(f"v_readfirstlane_b32 s{SRDV + i}, {v(84 + i)}", needs=["PRM"]))
-    return rd, use
-
-
-def dqp_loads():
-    """the block's Q / dO fragments into QF / OF, the lane's lse and delta per qt into v[0:3]"""
+def dqp_region_dma():
+    """the next block's Q / dO rows of this wave (queries 64 w .. + 63, 8 pieces each) into the Q / dO
+    region, its lse / delta words into the stats region (one dword piece each)"""
     out = []
-    for qt in range(2):
-        for ks in range(4):
-            out.append(f"buffer_load_dwordx4 {a_(DQF(qt, ks), 4)}, %[vq{qt}], s[{DSQ}:{DSQ + 3}], 0 offen offset:{ks * 32}")
-            out.append(f"buffer_load_dwordx4 {a_(DOF(qt, ks), 4)}, %[vo{qt}], s[{DSO}:{DSO + 3}], 0 offen offset:{ks * 32}")
-    for qt in range(2):
-        out.append(f"buffer_load_dword {v(qt)}, %[vs{qt}], s[{DSL}:{DSL + 3}], 0 offen")
-        out.append(f"buffer_load_dword {v(2 + qt)}, %[vs{qt}], s[{DSD_}:{DSD_ + 3}], 0 offen")
+    for srd, vo, s8, reg in ((DSQ, "%[vqd", "%[s8q]", 0), (DSO, "%[vod", "%[s8o]", 32768)):
+        for i in range(8):
+            out += [f"s_mul_i32 s{STMP}, {s8}, {i}",
+                    f"s_add_u32 m0, %[qow], {reg + 1024 * i}",
+                    "s_nop 0",
+                    f"buffer_load_dwordx4 {vo}{i & 1}], s[{srd}:{srd + 3}], s{STMP} offen lds"]
+    for srd, reg in ((DSL, 0), (DSD_, 1024)):
+        out += [f"s_add_u32 m0, %[stw], {reg}", "s_nop 0",
+                f"buffer_load_dword %[vsd], s[{srd}:{srd + 3}], 0 offen lds"]
     return out
 
 
-def dqp_kv_reset():
-    return [f"s_mov_b32 s{SRDK + 2}, %[sk2]", f"s_mov_b32 s{SRDK + 3}, 0x20000",
-            f"s_mov_b32 s{SRDV + 2}, %[sv2]", f"s_mov_b32 s{SRDV + 3}, 0x20000"]
-
-
-def dqp_dma_first_tiles():
-    out = [f"s_mov_b32 s{SB0}, %[lds0]", f"s_add_u32 s{SB1}, %[lds0], {D_BUF}", f"s_add_u32 s{SBD}, %[lds0], {2 * D_BUF}"]
-    for buf in (SB0, SB1):
-        out.append(f"s_add_u32 s{STMP}, s{buf}, %[wq]")
-        for m0, ld in dq_dma(buf):
-            out += [m0, "s_nop 0", ld]
-        out += dq_advance()
-    return out
+def dqp_tile_dma(buf):
+    out = [f"s_add_u32 s{STMP}, s{buf}, %[wq]"]
+    for m0, ld in dq_dma(buf):
+        out += [m0, "s_nop 0", ld]
+    return out + dq_advance()
 
 
 def dqp_epilogue(E):
-    """dQ (x scale) of the block: bf16 rows through this wave's staging area, buffer stores clipped
-    to the block's valid queries"""
+    """dQ (x scale) of the block, one query tile per pass: bf16 rows through this wave's staging area,
+    buffer stores clipped to the block's valid queries"""
     a = E.raw
     a("s_nop 15")
     a("s_nop 15")
@@ -1076,16 +1071,14 @@ def dqp_epilogue(E):
                 a(f"v_cvt_pk_bf16_f32 {v(wd + 1)}, {v(src + 2)}, {v(src + 3)}")
                 a(f"v_xor_b32 {v(wt)}, {c}, {v(WX)}")
                 a(f"v_lshl_add_u32 {v(wt)}, {v(wt)}, 4, {v(WB)}")
-                a(f"ds_write_b64 {v(wt)}, {v(wd, 2)} offset:{qt * 4096}")
-    a("s_waitcnt lgkmcnt(0)")
-    for qt in range(2):
+                a(f"ds_write_b64 {v(wt)}, {v(wd, 2)}")
+        a("s_waitcnt lgkmcnt(0)")
         for i in range(4):
-            a(f"ds_read_b128 {v(98 + 16 * qt + 4 * i, 4)}, %[vrd] offset:{qt * 4096 + 1024 * i}")
-    a("s_waitcnt lgkmcnt(0)")
-    for qt in range(2):
+            a(f"ds_read_b128 {v(98 + 4 * i, 4)}, %[vrd] offset:{1024 * i}")
+        a("s_waitcnt lgkmcnt(0)")
         for i in range(4):
             a(f"s_mul_i32 s{STMP}, %[s8dq], {4 * qt + i}")
-            a(f"buffer_store_dwordx4 {v(98 + 16 * qt + 4 * i, 4)}, %[vdq], s[{DSDQ}:{DSDQ + 3}], s{STMP} offen")
+            a(f"buffer_store_dwordx4 {v(98 + 4 * i, 4)}, %[vdq], s[{DSDQ}:{DSDQ + 3}], s{STMP} offen")
 
 
 def dq_p_body():
@@ -1096,45 +1089,83 @@ def dq_p_body():
         HARD_ACC[0] = False
 
 
-def dqp_item_setup(a):
-    """the block's -lse (DNLR) and -delta tuples (the dP chains' initial accumulator) from v[0:3]"""
+def _dq_p_body():
+    E = Emitter()
+    a = E.raw
+
+    def rfl(dst, src):
+        a(f"v_readfirstlane_b32 s{dst}, {v(src)}")
+
+    def kv_reset():
+        return [f"s_mov_b32 s{SRDK + 2}, %[sk2]", f"s_mov_b32 s{SRDK + 3}, 0x20000",
+                f"s_mov_b32 s{SRDV + 2}, %[sv2]", f"s_mov_b32 s{SRDV + 3}, 0x20000"]
+
+    a("s_nop 4")
+    a(f"s_mov_b32 s{SKEEP}, m0")
+    a(f"v_mov_b32 {v(DP_TABV)}, %[tab]")
+    a(f"s_mov_b32 s{DSITEM}, %[nitems]")
+    # ---- block 0: its region fill, its K / V tiles 0 and 1 -----------------------------------------
+    for i in range(5):
+        a(f"ds_read_b128 {v(66 + 4 * i, 4)}, {v(DP_TABV)} offset:{16 * i}")
+    a("s_waitcnt lgkmcnt(0)")
+    for j, srd in enumerate((DSQ, DSO, DSL, DSD_)):
+        for i in range(4):
+            rfl(srd + i, 66 + 4 * j + i)
+    for i in range(2):
+        rfl(SRDK + i, 82 + i)
+        rfl(SRDV + i, 84 + i)
+    for t in kv_reset():
+        a(t)
+    a("s_nop 4")
+    for t in dqp_region_dma():
+        a(t)
+    a(f"s_mov_b32 s{SB0}, %[lds0]")
+    a(f"s_add_u32 s{SB1}, %[lds0], {D_BUF}")
+    a(f"s_add_u32 s{SBD}, %[lds0], {2 * D_BUF}")
+    for t in dqp_tile_dma(SB0) + dqp_tile_dma(SB1):
+        a(t)
+    a("s_waitcnt vmcnt(0)")
+    a("s_branch L_qp_item_%=")
+    a("L_qp_next_%=:")
+    a("s_waitcnt vmcnt(8)")  # the previous block's dQ stores (8) may fly
+    a("L_qp_item_%=:")
+    a("s_barrier")
+    # ---- this block's fragments and stats from the region; its dQ descriptor; the next block's
+    # region descriptors and K / V bases ----------------------------------------------------------------
+    for ks in range(4):
+        a(f"v_add_u32 {v(DRK[ks])}, %[qow], %[vr{ks}]")
+    for qt in range(2):
+        for ks in range(4):
+            a(f"ds_read_b128 {a_(DQF(qt, ks), 4)}, {v(DRK[ks])} offset:{qt * 4096}")
+            a(f"ds_read_b128 {a_(DOF(qt, ks), 4)}, {v(DRK[ks])} offset:{32768 + qt * 4096}")
+    for qt in range(2):
+        a(f"ds_read_b32 {v(qt)}, %[vsl] offset:{qt * 128}")
+        a(f"ds_read_b32 {v(2 + qt)}, %[vsl] offset:{1024 + qt * 128}")
+    a(f"ds_read_b128 {v(86, 4)}, {v(DP_TABV)} offset:80")
+    for i in range(5):
+        a(f"ds_read_b128 {v(66 + 4 * i, 4)}, {v(DP_TABV)} offset:{ITEM_B + 16 * i}")
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_nop 4")  # the previous block's stores read DSDQ at issue: rewrite after
+    for i in range(4):
+        rfl(DSDQ + i, 86 + i)
+    for j, srd in enumerate((DSQ, DSO, DSL, DSD_)):
+        for i in range(4):
+            rfl(srd + i, 66 + 4 * j + i)
+    rfl(DSITEM - 1, 82)      # the next block's K / V bases: s[35:38] until its tiles are DMA'd
+    rfl(DSITEM - 2, 83)
+    rfl(DSITEM - 3, 84)
+    rfl(DSITEM - 4, 85)
+    a("s_nop 4")
+    for t in dqp_region_dma():  # the next block's rows (the null row's empty descriptors: zeros)
+        a(t)
+    # -lse (the B stream's fma), the -delta tuples (the dP chains' initial accumulator)
     for qt in range(2):
         a(f"v_xor_b32 {v(DNLR + qt)}, 0x80000000, {v(qt)}")
         a(f"v_xor_b32 {v(2 + qt)}, 0x80000000, {v(2 + qt)}")
         for r in range(16):
             a(f"v_mov_b32 {v(DNDL(qt) + r)}, {v(2 + qt)}")
-
-
-def _dq_p_body():
-    E = Emitter()
-    a = E.raw
-    a("s_nop 4")
-    a(f"s_mov_b32 s{SKEEP}, m0")
-    a(f"v_mov_b32 {v(DP_TABV)}, %[tab]")
-    a(f"s_mov_b32 s{DSITEM}, %[nitems]")
-    rd, use = dqp_params_next(True)
-    for ins in rd + use:
-        E.put(ins)
-    E.drain("s_waitcnt lgkmcnt(0)")
-    a(f"ds_read_b128 {v(86, 4)}, {v(DP_TABV)} offset:80")  # the block's dQ descriptor
-    a("s_waitcnt lgkmcnt(0)")
-    for i in range(4):
-        a(f"v_readfirstlane_b32 s{DSDQ + i}, {v(86 + i)}")
-    for t in dqp_kv_reset():
-        a(t)
-    a("s_nop 4")
-    for t in dqp_loads() + dqp_dma_first_tiles():
-        a(t)
-    a("s_waitcnt vmcnt(4)")  # Q, dO fragments, lse, delta and key tile 0 landed
-    a("s_branch L_qp_item_%=")
-    a("L_qp_next_%=:")
-    # the previous block left: fragments + stats (20), K / V tiles 0, 1 (8 pieces), its dQ stores (8)
-    a("s_waitcnt vmcnt(12)")
-    a("L_qp_item_%=:")
-    dqp_item_setup(a)
     for r in range(64):
         a(f"v_accvgpr_write_b32 {a_(r)}, 0")
-    a("s_barrier")
     for t in dq_addr("A", f"s{SB0}") + dq_addr("TN", f"s{SB0}"):
         a(t)
     for ins in dq_a_reads(0):
@@ -1181,35 +1212,29 @@ def _dq_p_body():
     a("L_qp_tail_%=:")
     if "stamps" in VARIANT:
         a("s_memtime s[74:75]")
-    # tail half J-1: the next block's parameters (slots 5-9, once B(J-2) freed set 0), descriptors
-    # (slots 11-14), fragment / stats loads (slots 16-22)
-    rd, use = dqp_params_next(False)
-    more = {}
-    for i, x in enumerate(rd):
-        more.setdefault(5 + i, []).append(x)
-    for i, x in enumerate(use):
-        more.setdefault(11 + i // 6, []).append(x)
-    extra = {15: dqp_kv_reset() + ["s_nop 4"]}
-    for i, t in enumerate(dqp_loads()):
-        extra.setdefault(16 + i // 3, []).append(t)
-    dq_half(E, True, b_even, b_odd, None, None, (DTN, 1), extra=extra, more=more)
-    dq_half(E, True, b_odd, {}, None, None, None)
-    E.drain("s_waitcnt lgkmcnt(0)")
+    # ---- tail start: the next block's K / V tiles 0, 1 into SBD and SB0 ------------------------------
+    a("s_waitcnt vmcnt(0)")
+    E.drain("s_waitcnt lgkmcnt(15)", keep=15)
     a("s_barrier")
     a(f"s_cmp_eq_u32 s{DSITEM}, 1")
     a("s_cbranch_scc1 L_qp_nodma_%=")
-    a("s_waitcnt vmcnt(20)")  # the loop's last (past-the-end) tile DMA landed; the 20 block loads may fly
-    for t in dqp_dma_first_tiles():
+    a(f"s_mov_b32 s{SRDK}, s{DSITEM - 1}")
+    a(f"s_mov_b32 s{SRDK + 1}, s{DSITEM - 2}")
+    a(f"s_mov_b32 s{SRDV}, s{DSITEM - 3}")
+    a(f"s_mov_b32 s{SRDV + 1}, s{DSITEM - 4}")
+    for t in kv_reset() + dqp_tile_dma(SBD) + dqp_tile_dma(SB0):
         a(t)
     a("L_qp_nodma_%=:")
+    dq_half(E, True, b_even, b_odd, None, None, (DTN, 1))
+    dq_half(E, True, b_odd, {}, None, None, None)
+    E.drain("s_waitcnt lgkmcnt(0)")
     dqp_epilogue(E)
     a(f"s_cmp_eq_u32 s{DSITEM}, 1")
     a("s_cbranch_scc1 L_qp_done_%=")
-    a("s_nop 4")
-    a(f"ds_read_b128 {v(66, 4)}, {v(DP_TABV)} offset:{ITEM_B + 80}")
-    a("s_waitcnt lgkmcnt(0)")
-    for i in range(4):
-        a(f"v_readfirstlane_b32 s{DSDQ + i}, {v(66 + i)}")
+    a(f"s_mov_b32 s{STMP}, s{SB0}")
+    a(f"s_mov_b32 s{SB0}, s{SBD}")
+    a(f"s_mov_b32 s{SBD}, s{SB1}")
+    a(f"s_mov_b32 s{SB1}, s{STMP}")
     a(f"v_add_u32 {v(DP_TABV)}, {ITEM_B}, {v(DP_TABV)}")
     a(f"s_sub_u32 s{DSITEM}, s{DSITEM}, 1")
     a("s_branch L_qp_next_%=")
@@ -1227,7 +1252,7 @@ def _dq_p_body():
 
 def dqp_clobbers(diag=False):
     regs = [f'"v{r}"' for r in range(DP_VLAST + 1)] + [f'"a{r}"' for r in range(240)] + \
-           [f'"s{r}"' for r in list(range(39, 60)) + list(range(80, 88)) + list(range(92, 98))]
+           [f'"s{r}"' for r in list(range(35, 60)) + list(range(80, 88)) + list(range(92, 98))]
     if diag:
         regs += [f'"s{r}"' for r in range(60, 76)]
     return ", ".join(regs)
@@ -1268,7 +1293,7 @@ def main():
         txt.append("#undef LTX_DKDV_W1_CLOBBERS")
     txt.append("#define LTX_DKDV_W1_CLOBBERS " + clobbers(diag) + "\n")
     VARIANT.clear()
-    txt += [f"#define LTX_DKDV_W1P_STG {P_STG}", f"#define LTX_DKDV_W1P_TAB {P_TAB}",
+    txt += [f"#define LTX_DKDV_W1P_KV {P_KV}", f"#define LTX_DKDV_W1P_STG {P_STG}", f"#define LTX_DKDV_W1P_TAB {P_TAB}",
             f"#define LTX_DKDV_W1P_ITEM {ITEM_B}", define("LTX_DKDV_W1P_BODY", dkdv_p_body())]
     if diag:
         VARIANT.update({"stamps"})
@@ -1287,7 +1312,8 @@ def main():
         txt.append("#undef LTX_DQ_W1_CLOBBERS")
     txt.append("#define LTX_DQ_W1_CLOBBERS " + dq_clobbers(diag) + "\n")
     VARIANT.clear()
-    txt += [f"#define LTX_DQ_W1P_STG {DP_STG}", f"#define LTX_DQ_W1P_TAB {DP_TAB}",
+    txt += [f"#define LTX_DQ_W1P_QO {DP_QO}", f"#define LTX_DQ_W1P_ST {DP_ST}", f"#define LTX_DQ_W1P_STG {DP_STG}",
+            f"#define LTX_DQ_W1P_TAB {DP_TAB}",
             define("LTX_DQ_W1P_BODY", dq_p_body())]
     if diag:
         VARIANT.update({"stamps"})

@@ -462,11 +462,12 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p
   if constexpr (V > 0) es.stop(p);
 }
 
-// LTX_ATTN_DKDV_W1 (read per call): unset / 1 the one-wave-per-SIMD kernel, 0 attn_dkdv_pipe_kernel,
-// 12..16 the stamped diagnostic variants (`make diag` builds)
+// LTX_ATTN_DKDV_W1 (read per call): unset / 2 the persistent one-wave kernel (attn_dkdv_w1p_kernel), 1
+// one workgroup per key block (attn_dkdv_w1_kernel), 0 attn_dkdv_pipe_kernel, 12..16 / 22 the stamped
+// diagnostic variants (`make diag` builds)
 static int dkdv_w1_mode() {
   const char* e = std::getenv("LTX_ATTN_DKDV_W1");
-  return e ? std::atoi(e) : 1;
+  return e ? std::atoi(e) : 2;
 }
 bool dkdv_w1_enabled() { return dkdv_w1_mode() != 0; }
 // LTX_ATTN_DKDV_W1=2 (22: its stamped diagnostic variant): the persistent kernel
@@ -568,20 +569,25 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1p_kernel(const AttnParams 
   const uint32_t so2 = __builtin_amdgcn_readfirstlane((uint32_t)(((p.Nq - 1) * (uint32_t)p.lddo + HD) * 2));
   const uint32_t ss2 = __builtin_amdgcn_readfirstlane((uint32_t)(p.Nq * 4));
   const uint32_t wst = __builtin_amdgcn_readfirstlane(2 * P_TILE + (wave < 2 ? wave * P_STAT : 2 * P_STAT));
-  uint32_t vq[2], vo[2], vk[2], vv[2];
+  uint32_t vq[2], vo[2], vkd[2], vvd[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
     vq[i] = (uint32_t)(row * p.ldq + c * 8) * 2;
     vo[i] = (uint32_t)(row * p.lddo + c * 8) * 2;
-    const int key = wave * 64 + i * 32 + (lane & 31);  // fragment rows of key tile i
-    vk[i] = (uint32_t)(key * p.ldk + 8 * h) * 2;
-    vv[i] = (uint32_t)(key * p.ldv + 8 * h) * 2;
+    // K / V region fill: even / odd 8-row pieces of the wave's 64 keys (the swizzle depends on the
+    // row's bits 1-3 only: piece j's rows 8 j + (lane >> 3) swizzle as piece j & 1's), the piece's
+    // 8 j rows added by its soffset
+    const int kr = wave * 64 + (lane >> 3), kc = (lane & 7) ^ swz<HD>(8 * i + (lane >> 3));
+    vkd[i] = (uint32_t)(kr * p.ldk + kc * 8) * 2;
+    vvd[i] = (uint32_t)(kr * p.ldv + kc * 8) * 2;
   }
   const uint32_t vl = (uint32_t)lane * 4, vs = (uint32_t)(16 * h);
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
   const uint32_t tab = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DKDV_W1P_TAB));
-  const uint32_t stg = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DKDV_W1P_STG) + wave * 16384);
+  const uint32_t stg = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DKDV_W1P_STG) + wave * 8192);
+  const uint32_t kvw = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DKDV_W1P_KV) + wave * 8192);
+  const uint32_t s8k = __builtin_amdgcn_readfirstlane((uint32_t)(16 * p.ldk)), s8v = __builtin_amdgcn_readfirstlane((uint32_t)(16 * p.ldv));
   const uint32_t wq = __builtin_amdgcn_readfirstlane(wave * 2048);
   const uint32_t qstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldq * 2));
   const uint32_t ostep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.lddo * 2));
@@ -599,11 +605,12 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1p_kernel(const AttnParams 
 #define LTX_W1P_OPERANDS                                                                                     \
   ::[sq2] "s"(sq2), [so2] "s"(so2), [ss2] "s"(ss2), [qstep] "s"(qstep), [ostep] "s"(ostep), [lds0] "s"(lds0),  \
     [wq] "s"(wq), [wst] "s"(wst), [iters] "s"(iters), [c2] "s"(c2), [tab] "s"(tab), [nitems] "s"(nitems),       \
-    [wodd] "s"(wodd), [scale] "s"(scale), [s8dk] "s"(s8dk), [s8dv] "s"(s8dv), [stg] "s"(stg),                   \
+    [wodd] "s"(wodd), [scale] "s"(scale), [s8dk] "s"(s8dk), [s8dv] "s"(s8dv), [stg] "s"(stg), [kvw] "s"(kvw),   \
+    [s8k] "s"(s8k), [s8v] "s"(s8v),                                                                             \
     [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]), [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]),             \
     [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]), [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]),     \
     [vs] "v"(vs), [vq0] "v"(vq[0]), [vq1] "v"(vq[1]), [vo0] "v"(vo[0]), [vo1] "v"(vo[1]), [vl] "v"(vl),         \
-    [vk0] "v"(vk[0]), [vk1] "v"(vk[1]), [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), [vwd] "v"(vwd), [vrd] "v"(vrd),      \
+    [vkd0] "v"(vkd[0]), [vkd1] "v"(vkd[1]), [vvd0] "v"(vvd[0]), [vvd1] "v"(vvd[1]), [vwd] "v"(vwd), [vrd] "v"(vrd), \
     [vdk] "v"(vdk), [vdv] "v"(vdv), [stp] "v"(stp)                                                              \
       : "memory", "scc", "vcc", LTX_DKDV_W1P_CLOBBERS
   if constexpr (V == 0) asm volatile(LTX_DKDV_W1P_BODY LTX_W1P_OPERANDS);
@@ -787,20 +794,26 @@ __global__ __launch_bounds__(256, 1) void attn_dq_w1p_kernel(const AttnParams p)
   __syncthreads();
   const uint32_t sk2 = __builtin_amdgcn_readfirstlane((uint32_t)(((p.Nk - 1) * (uint32_t)p.ldk + HD) * 2));
   const uint32_t sv2 = __builtin_amdgcn_readfirstlane((uint32_t)(((p.Nk - 1) * (uint32_t)p.ldv + HD) * 2));
-  uint32_t vk[2], vv[2], vq[2], vo[2], vs[2];
+  uint32_t vk[2], vv[2], vqd[2], vod[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
     vk[i] = (uint32_t)(row * p.ldk + c * 8) * 2;
     vv[i] = (uint32_t)(row * p.ldv + c * 8) * 2;
-    const int qr = wave * 64 + i * 32 + (lane & 31);  // the lane's query in query tile i
-    vq[i] = (uint32_t)(qr * p.ldq + 8 * h) * 2;
-    vo[i] = (uint32_t)(qr * p.lddo + 8 * h) * 2;
-    vs[i] = (uint32_t)qr * 4;
+    // Q / dO region fill: even / odd 8-row pieces of the wave's 64 queries (as the persistent dK / dV
+    // kernel's K / V fill), the piece's 8 j rows added by its soffset
+    const int qr = wave * 64 + (lane >> 3), qc = (lane & 7) ^ swz<HD>(8 * i + (lane >> 3));
+    vqd[i] = (uint32_t)(qr * p.ldq + qc * 8) * 2;
+    vod[i] = (uint32_t)(qr * p.lddo + qc * 8) * 2;
   }
+  const uint32_t vsd = (uint32_t)(wave * 64 + lane) * 4;  // the wave's lse / delta words
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
   const uint32_t tab = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DQ_W1P_TAB));
-  const uint32_t stg = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DQ_W1P_STG) + wave * 8192);
+  const uint32_t stg = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DQ_W1P_STG) + wave * 4096);
+  const uint32_t qow = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DQ_W1P_QO) + wave * 8192);
+  const uint32_t stw = __builtin_amdgcn_readfirstlane(lds_u32(smem + LTX_DQ_W1P_ST) + wave * 256);
+  const uint32_t vsl = stw + (uint32_t)(lane & 31) * 4;
+  const uint32_t s8q = __builtin_amdgcn_readfirstlane((uint32_t)(16 * p.ldq)), s8o = __builtin_amdgcn_readfirstlane((uint32_t)(16 * p.lddo));
   const uint32_t wq = __builtin_amdgcn_readfirstlane(wave * 2048);
   const uint32_t kstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldk * 2));
   const uint32_t vstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldv * 2));
@@ -815,10 +828,10 @@ __global__ __launch_bounds__(256, 1) void attn_dq_w1p_kernel(const AttnParams p)
 #define LTX_DQP_OPERANDS                                                                                       \
   ::[sk2] "s"(sk2), [sv2] "s"(sv2), [kstep] "s"(kstep), [vstep] "s"(vstep), [lds0] "s"(lds0), [wq] "s"(wq),    \
     [iters] "s"(iters), [c2] "s"(c2), [tab] "s"(tab), [nitems] "s"(nitems), [scale] "s"(scale), [s8dq] "s"(s8dq), \
-    [stg] "s"(stg), [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]), [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]), \
+    [stg] "s"(stg), [qow] "s"(qow), [stw] "s"(stw), [s8q] "s"(s8q), [s8o] "s"(s8o), [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]), [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]), \
     [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]), [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]),       \
-    [vk0] "v"(vk[0]), [vk1] "v"(vk[1]), [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), [vq0] "v"(vq[0]), [vq1] "v"(vq[1]),    \
-    [vo0] "v"(vo[0]), [vo1] "v"(vo[1]), [vs0] "v"(vs[0]), [vs1] "v"(vs[1]), [vwd] "v"(vwd), [vrd] "v"(vrd),        \
+    [vk0] "v"(vk[0]), [vk1] "v"(vk[1]), [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), [vqd0] "v"(vqd[0]), [vqd1] "v"(vqd[1]), \
+    [vod0] "v"(vod[0]), [vod1] "v"(vod[1]), [vsd] "v"(vsd), [vsl] "v"(vsl), [vwd] "v"(vwd), [vrd] "v"(vrd),        \
     [vdq] "v"(vdq), [stp] "v"(stp)                                                                                \
       : "memory", "scc", "vcc", LTX_DQ_W1P_CLOBBERS
   if constexpr (V == 0) asm volatile(LTX_DQ_W1P_BODY LTX_DQP_OPERANDS);
@@ -854,11 +867,11 @@ int launch_dq_w1p(const AttnParams& p, hipStream_t s) {
   return LTX_OK;
 }
 
-// LTX_ATTN_DQ_W1 (read per call): unset / 1 the one-wave kernel, 0 attn_dq_pipe_kernel, 12 / 13 the
-// stamped diagnostic variants (`make diag` builds)
+// LTX_ATTN_DQ_W1 (read per call): unset / 2 the persistent one-wave kernel (bf16 dQ), 1 one workgroup per
+// query block, 0 attn_dq_pipe_kernel, 12 / 13 / 22 the stamped diagnostic variants (`make diag` builds)
 static int dq_w1_mode() {
   const char* e = std::getenv("LTX_ATTN_DQ_W1");
-  return e ? std::atoi(e) : 1;
+  return e ? std::atoi(e) : 2;
 }
 bool dq_w1_enabled() { return dq_w1_mode() != 0; }
 // LTX_ATTN_DQ_W1=2 (22: its stamped diagnostic variant): the persistent kernel

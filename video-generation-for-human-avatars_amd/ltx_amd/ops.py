@@ -412,14 +412,19 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
         # LDS buffers of the pipelined kernels (attention_pipe.hip dq_nbuf / dkdv_nbuf: 4 unless "3")
         nq = "3" if os.environ.get("LTX_ATTN_DQ_NBUF", "4")[:1] == "3" else "4"
         nk = "3" if os.environ.get("LTX_ATTN_DKDV_NBUF", "4")[:1] == "3" else "4"
-        if kb == "false" and os.environ.get("LTX_ATTN_DQ_W1", "1").strip()[:1] != "0":
-            dqk = "ltx::attn_dq_w1_kernel"  # one wave per SIMD (attention_pipe.hip)
+        # one wave per SIMD, hand-scheduled loops (attention_pipe.hip): LTX_ATTN_DQ_W1 /
+        # LTX_ATTN_DKDV_W1 = 2 (default) the persistent kernels, 1 one workgroup per block
+        dq_mode = os.environ.get("LTX_ATTN_DQ_W1", "2").strip() or "2"
+        dk_mode = os.environ.get("LTX_ATTN_DKDV_W1", "2").strip() or "2"
+        if kb == "false" and dq_mode[:1] != "0":
+            dqk = ("ltx::attn_dq_w1p_kernel<0>" if dq_mode == "2" and dq.dtype != F32
+                   else "ltx::attn_dq_w1_kernel<0>")
         else:
             dqk = (f"ltx::attn_dq_pipe_kernel<{nq}>" if kb == "false" and _env_on("LTX_ATTN_DQ_PIPE")
                    else f"ltx::attn_q_kernel<{d}, 1, {kb}, 4>")
-        if kb == "false" and os.environ.get("LTX_ATTN_DKDV_W1", "1").strip() not in ("0", ""):
-            # one wave per SIMD, hand-scheduled loop (attention_pipe.hip attn_dkdv_w1_kernel)
-            kern = f"ltx::attn_dkdv_w1_kernel<0> + {dqk}"
+        if kb == "false" and dk_mode != "0":
+            dkk = "ltx::attn_dkdv_w1p_kernel<0>" if dk_mode == "2" else "ltx::attn_dkdv_w1_kernel<0>"
+            kern = f"{dkk} + {dqk}"
         else:
             kern = f"ltx::attn_dkdv_pipe_kernel<{kb}, {nk}> + {dqk}"
     else:
