@@ -837,6 +837,38 @@ def test_attention_dkdv_w1_matches_pipe_bitwise(B, H, Nq, Nk, monkeypatch):
         assert torch.equal(a, b_)
 
 
+@pytest.mark.parametrize("B,H,Nq,Nk,jump", [(8, 32, 1792, 1792, 0), (2, 3, 1000, 768, 0), (1, 2, 70, 320, 0),
+                                            (2, 4, 300, 256, 0), (2, 2, 1792, 1792, 4), (1, 2, 7488, 7488, 16),
+                                            (1, 3, 500, 1344, 1)])
+def test_attention_fwd_w1_matches_pipe_bitwise(B, H, Nq, Nk, jump, monkeypatch):
+    """attn_fwd_w1_kernel (one wave per SIMD, 64 queries per wave, hand-scheduled loop from
+    tools/gen_attn_fwd.py; LTX_ATTN_FWD_W1=1, opt-in) keeps attn_fwd_pipe_kernel<true>'s arithmetic,
+    deferred-max decisions and accumulation order: O and lse bitwise equal, ragged query blocks and odd
+    tile counts included. jump > 0: the keys' logits step up by ~17 log2 units every `jump` tiles, so
+    most rows take the out-of-line redo (the tile max, alpha, the O / l rescale) several times."""
+    from ltx_amd import ops
+    d = 64
+    scale = d ** -0.5
+    q = g(B * Nq, H * d, seed=61)
+    k = g(B * Nk, H * d, seed=62)
+    v = g(B * Nk, H * d, seed=63)
+    if jump:
+        gen = torch.Generator(device="cpu").manual_seed(64)
+        qh = q.float().view(B, Nq, H, d).cpu()
+        kh = k.float().view(B, Nk, H, d).cpu()
+        qh[..., 0] = torch.where(torch.rand(B, Nq, H, generator=gen) < 0.7, 4.0, -4.0)
+        t = torch.arange(Nk) // 64
+        kh[..., 0] = (-60.0 + 24.0 * (t // jump).float() + torch.rand(Nk, generator=gen) * 3.0).clamp(max=60.0).view(1, Nk, 1)
+        q = qh.reshape(B * Nq, H * d).cuda().bfloat16()
+        k = kh.reshape(B * Nk, H * d).cuda().bfloat16()
+    outs = {}
+    for w1 in ("0", "1"):
+        monkeypatch.setenv("LTX_ATTN_FWD_W1", w1)
+        outs[w1] = ops.attn_fwd(q, k, v, B, H, d, scale)
+    assert torch.equal(outs["1"][0], outs["0"][0])
+    assert torch.equal(outs["1"][1], outs["0"][1])
+
+
 # (8, 32, 1792, 1792): config A's self-attention, 7 blocks per workgroup; (4, 16, 7488, 7488): config
 # X-like, 30 blocks per workgroup; the small ones give every block its own workgroup
 @pytest.mark.parametrize("B,H,Nq,Nk", [(8, 32, 1792, 1792), (4, 16, 7488, 7488), (2, 3, 1000, 768), (1, 2, 70, 320),

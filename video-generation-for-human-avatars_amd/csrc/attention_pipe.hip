@@ -21,6 +21,7 @@
 
 #include "attention_common.h"
 #include "attn_bwd_body.h"
+#include "attn_fwd_body.h"
 #ifdef LTX_DKDV_DIAG  // `make diag`: timing-only variants of the loop (tools/gen_attn_bwd.py --diag)
 #include "attn_bwd_body_diag.h"
 #endif
@@ -1317,6 +1318,109 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (qi < p.Nq && h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
 }
 
+// =============================================================================================
+// Forward at ONE wave per SIMD (self-attention shapes: no key bias, head dim 64, Nk % 64 == 0, >= 4
+// key tiles): 4 waves x 64 queries (two 32-query tiles per wave) = 256 queries per workgroup, the
+// loop one hand-scheduled asm statement (attn_fwd_body.h, tools/gen_attn_fwd.py: the unit schedule,
+// the out-of-line redo of the deferred max). Same arithmetic, decisions and accumulation order as
+// attn_fwd_pipe_kernel<true>: O and lse bitwise equal to it.
+// =============================================================================================
+__global__ __launch_bounds__(256, 1) void attn_fwd_w1_kernel(const AttnParams p) {
+  constexpr int HD = PHD;
+  __shared__ __attribute__((aligned(16))) char smem[LTX_FWD_W1_NBUF * LTX_FWD_W1_BUF];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  int bx, hh, b;
+  xcd_block(p.xcd_order, bx, hh, b);
+  const int q0 = bx * 256 + wave * 64;
+  const bf16_t* qp[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qc = min(q0 + qt * 32 + (lane & 31), p.Nq - 1);
+    qp[qt] = p.q + ((int64_t)b * p.Nq + qc) * p.ldq + hh * HD + 8 * h;
+  }
+  const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  const bf16_t* vbase = p.v + (int64_t)b * p.kvb * p.ldv + hh * HD;
+  const u32x4 srdk = raw_srd(kbase, ((uint64_t)(p.Nk - 1) * p.ldk + HD) * 2);
+  const u32x4 srdv = raw_srd(vbase, ((uint64_t)(p.Nk - 1) * p.ldv + HD) * 2);
+  // DMA: wave w moves K rows 16 w .. 16 w + 15 (pieces 2w, 2w+1) and the same V rows of every tile
+  uint32_t vk[2], vv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3), c = (lane & 7) ^ swz<HD>(row);
+    vk[i] = (uint32_t)(row * p.ldk + c * 8) * 2;
+    vv[i] = (uint32_t)(row * p.ldv + c * 8) * 2;
+  }
+  const uint32_t wq0 = __builtin_amdgcn_readfirstlane(wave * 2048), wq1 = __builtin_amdgcn_readfirstlane(wave * 2048 + 1024);
+  const uint32_t wqv0 = __builtin_amdgcn_readfirstlane(8192 + wave * 2048), wqv1 = __builtin_amdgcn_readfirstlane(8192 + wave * 2048 + 1024);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_u32(smem));
+  const uint32_t kstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldk * 2));
+  const uint32_t vstep = __builtin_amdgcn_readfirstlane((uint32_t)(64 * p.ldv * 2));
+  const int U = p.Nk / 64;
+  const uint32_t iters = __builtin_amdgcn_readfirstlane((uint32_t)((U - 2) / 2));
+  const uint32_t uodd = __builtin_amdgcn_readfirstlane((uint32_t)(U & 1));
+  const float c2 = p.scale * LOG2E;
+  f32x16 a00 = {}, a01 = {}, a10 = {}, a11 = {};
+  float m0 = -1e30f, m1 = -1e30f, l0 = 0.f, l1 = 0.f;
+  uint64_t* stp = (uint64_t*)p.part +  // diagnostic bodies only (tools/build_fwd_variant.sh stamps)
+                  ((blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z)) * 4 + wave) * 8;
+  asm volatile(LTX_FWD_W1_BODY
+               : "+a"(a00), "+a"(a01), "+a"(a10), "+a"(a11), "+v"(m0), "+v"(m1), "+v"(l0), "+v"(l1)
+               : [sk0] "s"(srd_half(srdk, 0)), [sk1] "s"(srd_half(srdk, 1)), [sv0] "s"(srd_half(srdv, 0)),
+                 [sv1] "s"(srd_half(srdv, 1)), [kstep] "s"(kstep), [vstep] "s"(vstep), [lds0] "s"(lds0),
+                 [wq0] "s"(wq0), [wq1] "s"(wq1), [wqv0] "s"(wqv0), [wqv1] "s"(wqv1), [iters] "s"(iters),
+                 [uodd] "s"(uodd), [c2] "s"(c2), [vr0] "v"(lofs.row[0]), [vr1] "v"(lofs.row[1]),
+                 [vr2] "v"(lofs.row[2]), [vr3] "v"(lofs.row[3]), [vt0] "v"(lofs.tr[0][0]), [vt1] "v"(lofs.tr[0][1]),
+                 [vt2] "v"(lofs.tr[1][0]), [vt3] "v"(lofs.tr[1][1]), [vk0] "v"(vk[0]), [vk1] "v"(vk[1]),
+                 [vv0] "v"(vv[0]), [vv1] "v"(vv[1]), [qp0] "v"(qp[0]), [qp1] "v"(qp[1]), [stp] "v"(stp)
+               : "memory", "scc", "vcc", LTX_FWD_W1_CLOBBERS);
+  // attn_fwd_pipe_kernel's epilogue per query tile (every DMA retired inside the statement)
+  const f32x16 acc[2][2] = {{a00, a01}, {a10, a11}};
+  const float mr[2] = {m0, m1}, lr[2] = {l0, l1};
+  __syncthreads();
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const float l_tot = xor32_sum(lr[qt]);
+    const float inv = 1.0f / l_tot;
+    const int qb = q0 + qt * 32;
+    if (qb < p.Nq)
+      store_rows_lds<HD>(smem + wave * 8192 + qt * 4096, acc[qt], inv, p.o_out + (int64_t)b * p.Nq * p.ldo + hh * HD,
+                         p.ldo, qb, min(32, p.Nq - qb), lane);
+    const int qi = qb + (lane & 31);
+    if (qi < p.Nq && h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = mr[qt] + log2f(l_tot);
+  }
+}
+
+// LTX_ATTN_FWD_W1 (read per call): 1 the one-wave forward where it applies; unset / 0 the pipelined
+// kernel (12: the diagnostic bodies of tools/build_fwd_variant.sh, stamps into the stream's workspace).
+// Not the default: its loop measures 2008 cycles per 64-key unit against 1024 of MFMA (1284 without
+// the softmax VALU, profiles/r05d_fwd_w1_stamps.txt) -- at two exponentials per MFMA the one-wave
+// schedule adds the VALU to the MFMA time almost linearly, and the eight-wave kernel is faster
+// (220 vs 236 us per layer at config A)
+bool fwd_w1_enabled(const AttnParams& p) {
+  const char* e = std::getenv("LTX_ATTN_FWD_W1");
+  const bool on = e && e[0] != '0';
+  return on && p.Nk % 64 == 0 && p.Nk >= 256;
+}
+
+int launch_fwd_w1(const AttnParams& p, hipStream_t s) {
+  const dim3 g((unsigned)((p.Nq + 255) / 256), (unsigned)p.H, (unsigned)p.B);
+  const char* e = std::getenv("LTX_ATTN_FWD_W1");
+  if (e && std::atoi(e) == 12) {
+    AttnParams q = p;
+    size_t ws = 0;
+    q.part = stream_workspace(s, &ws);
+    if (q.part == nullptr || ws < (size_t)g.x * g.y * g.z * 4 * 8 * 8) return fail(LTX_ERR_BAD_ARG, "stamps: workspace");
+    hipLaunchKernelGGL(attn_fwd_w1_kernel, g, dim3(256), 0, s, q);
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+  hipLaunchKernelGGL(attn_fwd_w1_kernel, g, dim3(256), 0, s, p);
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
 bool fwd_pipe_enabled() {  // LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8> (A/B switch)
   const char* e = std::getenv("LTX_ATTN_FWD_PIPE");  // read per call: tests compare paths in one process
   const int v = e ? std::atoi(e) : 1;
@@ -1329,6 +1433,7 @@ static bool fwd_f32sum() {  // LTX_ATTN_FWD_F32SUM=0: row sums by v_dot2c over t
 }
 
 int launch_fwd_pipe(const AttnParams& p, hipStream_t s) {
+  if (fwd_w1_enabled(p)) return launch_fwd_w1(p, s);
   const dim3 g((unsigned)((p.Nq + F_QUERIES - 1) / F_QUERIES), (unsigned)p.H, (unsigned)p.B);
   if (fwd_f32sum())
     hipLaunchKernelGGL(attn_fwd_pipe_kernel<true>, g, dim3(512), 0, s, p);
