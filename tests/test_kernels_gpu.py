@@ -608,7 +608,7 @@ def test_timestep_silu_transpose_colsum():
     assert rel(cs, x.float().sum(0)) < 5e-3
 
 
-@pytest.mark.parametrize("M,r", [(1000, 16), (2048, 16), (333, 8), (517, 32)])
+@pytest.mark.parametrize("M,r", [(1000, 16), (2048, 16), (333, 8), (517, 32), (4480, 8), (14336, 16)])
 def test_lora_kernels(M, r):
     from ltx_amd import ops
     K, N = 2048, 2048

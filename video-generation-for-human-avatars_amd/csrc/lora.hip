@@ -329,6 +329,10 @@ __global__ __launch_bounds__(64 * NW) void lora_rows_kernel(const bf16_t* __rest
 // per row), and MFMA t (t = 0..7) takes element t, so its output column c stands for
 // n0 + 8c + t (a fixed permutation undone at the store). Block = 8 waves on the same 128
 // columns, interleaved row quads; the wave partials are reduced through LDS in wave order.
+// the token-sized path of ltx_lora_wgrad (lora_dy.hip)
+bool lora_wgrad_rows(const bf16_t* y, int64_t ldy, const float* u, int64_t ldu, float* dw, int64_t on, int64_t oj,
+                     int64_t M, int64_t N, int64_t r, float alpha, int accumulate, hipStream_t s);
+
 template <int R>
 __global__ __launch_bounds__(512) void lora_wgrad_kernel(const bf16_t* __restrict__ y, int64_t ldy,
                                                          const float* __restrict__ u, int64_t ldu,
@@ -570,6 +574,10 @@ extern "C" int ltx_lora_wgrad_grouped(const void* y, int64_t ldy, const float* u
   LTX_CHECK_ARG(groups >= 1 && groups <= 65535 && gy % 8 == 0 && (groups == 1 || gd >= N * r),
                 "lora_wgrad: groups in [1, 65535], 16-B aligned y groups, disjoint outputs");
   hipStream_t s = (hipStream_t)stream;
+  if (groups == 1 && lora_wgrad_rows((const bf16_t*)y, ldy, u, ldu, dw, on, oj, M, N, r, alpha, accumulate, s)) {
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
   // ~512 blocks of 128 columns x >= 512 rows (8 waves x 4-quad steps): enough waves to stream y.
   // ~512 blocks (two per CU): 17.9 us vs 20.0 us with 256 at M = 14336, N = 2048, r = 16. Splits
   // of >= 256 rows in multiples of 32 (a wave's row quads stay aligned; the last 128-row step of a

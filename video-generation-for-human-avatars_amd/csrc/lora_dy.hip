@@ -34,7 +34,9 @@ constexpr int DY_COLS = 512; // columns per block
 constexpr int DY_UPAD = DY_G * 32 + 4;  // u^T row length in LDS (floats; +4 spreads the banks)
 }  // namespace
 
-template <int R>
+// WP = false: the dB product alone (ltx_lora_wgrad's token-sized path: dw = alpha . Y^T . u on the
+// bf16 matrix core with u's exact three-piece split, where lora_wgrad_kernel runs f32 MFMAs)
+template <int R, bool WP>
 __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__ y, int64_t ldy,
                                                       const float* __restrict__ u, int64_t ldu,
                                                       const bf16_t* __restrict__ w3, int64_t ldw,
@@ -55,24 +57,6 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
   const int cs = blockIdx.x, rs = blockIdx.y;
   const int c0 = cs * DY_COLS + wave * 64;
   const int mb = rs * DY_G * 32;
-
-  // u^T of rows mb .. mb + 32G (zero past M)
-  for (int e = tid; e < DY_G * 32 * RP; e += 512) {
-    const int rr = e / RP, j = e % RP;
-    const int m = mb + rr;
-    ut[j * DY_UPAD + rr] = (m < M && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
-  }
-  // B^T pieces of this wave's 64 columns: [k half][piece x JT] (ltx_lora_rows' fragment layout)
-  s16x8 bp[2][NF];
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-#pragma unroll
-    for (int t = 0; t < JT; ++t) {
-      const bf16_t* src = w3 + (int64_t)(p * RP + t * 16 + (lane & 15)) * ldw + c0 + (lane >> 4) * 8;
-      bp[0][p * JT + t] = *(const s16x8*)src;
-      bp[1][p * JT + t] = *(const s16x8*)(src + 32);
-    }
-  __syncthreads();  // u^T staged; every ordinary load retired before the DMA stream starts
 
   // DMA: piece i of a slot = rows 8i .. 8i+7; lane -> row 8i + (lane >> 3), physical chunk lane & 7
   uint32_t yo[4];
@@ -96,6 +80,27 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
         : "memory", "scc");
   };
   const int ng = min(DY_G, (M - mb + 31) / 32);  // row groups of this block
+  // the first slots' DMA goes out ahead of the u^T staging loads, so their latencies overlap
+  for (int g = 0; g < DY_NR - 1; ++g)
+    if (g < ng) dma(g);
+
+  // u^T of rows mb .. mb + 32G (zero past M)
+  for (int e = tid; e < DY_G * 32 * RP; e += 512) {
+    const int rr = e / RP, j = e % RP;
+    const int m = mb + rr;
+    ut[j * DY_UPAD + rr] = (m < M && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
+  }
+  // B^T pieces of this wave's 64 columns: [k half][piece x JT] (ltx_lora_rows' fragment layout)
+  s16x8 bp[2][NF];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int t = 0; t < JT && WP; ++t) {
+      const bf16_t* src = w3 + (int64_t)(p * RP + t * 16 + (lane & 15)) * ldw + c0 + (lane >> 4) * 8;
+      bp[0][p * JT + t] = *(const s16x8*)src;
+      bp[1][p * JT + t] = *(const s16x8*)(src + 32);
+    }
+  __syncthreads();  // u^T staged; every ordinary load retired before the counted waits below
 
   // row reads (w product): rows 16q + (lane & 15), logical chunk 4h + (lane >> 4)
   int roff[2][2];
@@ -122,8 +127,6 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) bacc[t][nb] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  for (int g = 0; g < DY_NR - 1; ++g)
-    if (g < ng) dma(g);
 #pragma unroll
   for (int g = 0; g < DY_G; ++g) {
 #pragma unroll
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
     const char* sl = smem + wave * (DY_NR * 4096) + (g % DY_NR) * 4096;
     s16x8 xf[2][2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < 2 && WP; ++q)
 #pragma unroll
       for (int h = 0; h < 2; ++h) xf[q][h] = *(const s16x8*)(sl + roff[q][h]);
     s16x8 yb[4];
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot g read: its ring slot may be refilled
     if (g + DY_NR - 1 < ng) dma(g + DY_NR - 1);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2 && WP; ++h)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -197,6 +200,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
       const int n = c0 + 16 * nb + (lane & 15);
       *(f32x4*)(part_b + ((int64_t)rs * N + n) * RP + 16 * t + 4 * g4) = bacc[t][nb];
     }
+  if constexpr (!WP) return;
   // w partial: the 8 waves' [32G rows][RP] sums through LDS (the ring is free once all waves are
   // past their last slot), then one column-split partial per row
   __syncthreads();
@@ -268,6 +272,40 @@ __global__ __launch_bounds__(256) void lora_dy_finish_kernel(const float* __rest
   }
 }
 
+// ltx_lora_wgrad's token-sized path (called from lora.hip): dw (+)= alpha . Y^T . u through the
+// dB product of lora_dy_kernel (bf16 matrix core, u split into exact hi / mid / lo pieces) and the
+// dB half of the finish kernel. lora_wgrad_kernel spends ~9 us of f32 MFMA issue on the same
+// product at M = 14336, N = 2048, r = 16. Returns false (nothing launched) where it does not apply;
+// LTX_LORA_WGRAD_ROWS=0 at load keeps lora_wgrad_kernel everywhere.
+bool lora_wgrad_rows(const bf16_t* y, int64_t ldy, const float* u, int64_t ldu, float* dw, int64_t on, int64_t oj,
+                     int64_t M, int64_t N, int64_t r, float alpha, int accumulate, hipStream_t s) {
+  static const int enabled = [] {
+    const char* e = getenv("LTX_LORA_WGRAD_ROWS");
+    return e ? atoi(e) : 1;
+  }();
+  if (!enabled || M < 2048 || M % 32 != 0 || N % DY_COLS != 0 || (r != 8 && r != 16)) return false;
+  if (ldy % 8 != 0 || ((uintptr_t)y % 16) != 0 || ldy * 2 * 32 >= ((int64_t)1 << 32) || ldu < r) return false;
+  const int64_t RP = r >= 16 ? r : 16;
+  const int RS = (int)((M + DY_G * 32 - 1) / (DY_G * 32));
+  size_t ws = 0;
+  float* pb = stream_workspace(s, &ws);
+  if (pb == nullptr || (size_t)RS * N * RP * sizeof(float) > ws) return false;
+  const dim3 grid((unsigned)(N / DY_COLS), (unsigned)RS);
+  const dim3 g2((unsigned)((N * r + 63) / 64));
+#define LTX_LORA_WG(RR)                                                                                       \
+  hipLaunchKernelGGL((lora_dy_kernel<RR, false>), grid, dim3(512), 0, s, y, ldy, u, ldu, nullptr, (int64_t)0, \
+                     nullptr, pb, (int)M, (int)N);                                                            \
+  hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, nullptr, 0, pb, RS, (int)M, (int)N,    \
+                     alpha, nullptr, (int64_t)0, nullptr, (int64_t)0, 0, dw, on, oj, accumulate, 0);
+  if (r == 8) {
+    LTX_LORA_WG(8)
+  } else {
+    LTX_LORA_WG(16)
+  }
+#undef LTX_LORA_WG
+  return true;
+}
+
 extern "C" int ltx_lora_dy_workspace(int64_t M, int64_t N, int64_t r, int64_t* floats) {
   LTX_CHECK_ARG(floats && M > 0 && N > 0 && (r == 8 || r == 16), "lora_dy_workspace: bad args");
   const int64_t RP = r >= 16 ? r : 16;
@@ -297,7 +335,7 @@ extern "C" int ltx_lora_dy(const void* y, int64_t ldy, const float* u, int64_t l
   const int nwb = (int)((M * K2 + 255) / 256);
   const dim3 g2((unsigned)(nwb + (N * r + 63) / 64));
 #define LTX_LORA_DY(RR)                                                                                          \
-  hipLaunchKernelGGL((lora_dy_kernel<RR>), grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu,                \
+  hipLaunchKernelGGL((lora_dy_kernel<RR, true>), grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu,                \
                      (const bf16_t*)w3, ldw3, pw, pb, (int)M, (int)N);                                           \
   LTX_LAUNCH_CHECK();                                                                                            \
   hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, pw, CS, pb, RS, (int)M, (int)N, alpha, w, \

@@ -709,6 +709,7 @@ def lora_wgrad(y, u, alpha=1.0, transpose_out=False, out=None, accumulate=False,
     assert tuple(out.shape) == shape and out.dtype == F32 and out.is_contiguous()
     on, oj = (1, N) if transpose_out else (r, 1)
     gy, gu = group_strides
+    _gemm_workspace(y.device)  # the row-split partials live in the stream's workspace
     call("ltx_lora_wgrad_grouped", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(out), on, oj, M,
          N, r, float(alpha), 1 if accumulate else 0, groups, gy, gu, N * r, _s())
     return out
