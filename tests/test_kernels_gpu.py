@@ -658,6 +658,25 @@ def test_lora_dy_one_pass(M, N, r):
     assert rel(buf2, ops.lora_wgrad(dy, u, alpha=0.5)) < 1e-6
 
 
+@pytest.mark.parametrize("M,K,r", [(14336, 2048, 16), (4480, 1024, 8), (2048, 512, 16)])
+def test_lora_rows_token_sized(M, K, r):
+    """ltx_lora_rows at token-sized M (the column-split lora_dy_kernel path + its finish): u against
+    fp32, the split operand exactly lora_split of its own u, and a strided out / split_out view."""
+    from ltx_amd import ops
+    x = g(M, K, seed=7)
+    A = torch.randn(r, K, device=DEV) / K ** 0.5
+    pieces = ops.lora_pieces(A)
+    u, su = ops.lora_rows(x, pieces, r, alpha=0.5, split=True)
+    assert rel(u, 0.5 * x.float() @ A.t()) < 1e-5
+    assert torch.equal(su, ops.lora_split(u, "act"))
+    K2 = ops.lora_k2(r)
+    big = torch.full((M, 2 * K2), 7.0, dtype=torch.bfloat16, device=DEV)
+    outb = torch.full((M, 2 * r), 3.0, device=DEV)
+    u2, _ = ops.lora_rows(x, pieces, r, alpha=0.5, out=outb[:, r:], split=True, split_out=big[:, K2:])
+    assert torch.equal(u2, u) and torch.equal(big[:, K2:], su)
+    assert float((big[:, :K2] - 7.0).abs().max()) == 0 and float((outb[:, :r] - 3.0).abs().max()) == 0
+
+
 def test_mse_and_adamw():
     from ltx_amd import ops
     o, v = g(2, 64, 128, seed=1), g(2, 64, 128, seed=2)

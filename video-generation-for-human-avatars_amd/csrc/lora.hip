@@ -329,7 +329,9 @@ __global__ __launch_bounds__(64 * NW) void lora_rows_kernel(const bf16_t* __rest
 // per row), and MFMA t (t = 0..7) takes element t, so its output column c stands for
 // n0 + 8c + t (a fixed permutation undone at the store). Block = 8 waves on the same 128
 // columns, interleaved row quads; the wave partials are reduced through LDS in wave order.
-// the token-sized path of ltx_lora_wgrad (lora_dy.hip)
+// the token-sized paths of ltx_lora_rows and ltx_lora_wgrad (lora_dy.hip)
+bool lora_rows_dy(const bf16_t* x, int64_t ldx, const bf16_t* w3, int64_t ldw, float* out, int64_t ldo, int64_t M,
+                  int64_t K, int64_t r, float alpha, bf16_t* split, int64_t ld_split, int64_t K2, hipStream_t s);
 bool lora_wgrad_rows(const bf16_t* y, int64_t ldy, const float* u, int64_t ldu, float* dw, int64_t on, int64_t oj,
                      int64_t M, int64_t N, int64_t r, float alpha, int accumulate, hipStream_t s);
 
@@ -545,9 +547,13 @@ extern "C" int ltx_lora_rows(const void* x, int64_t ldx, const void* w3, int64_t
   LTX_CHECK_ARG((int64_t)ldx * 2 * (M - 1) + 2 * K < ((int64_t)1 << 32) && (int64_t)ldw * 2 * 3 * 32 < ((int64_t)1 << 32),
                 "lora_rows: 32-bit DMA offsets");
   LTX_CHECK_ARG(!split || (K2 >= 3 * r && K2 % 64 == 0 && ld_split >= K2), "lora_rows: split needs K2 >= 3r, %64");
-  const dim3 grid((unsigned)((M + 31) / 32));
   hipStream_t s = (hipStream_t)stream;
   bf16_t* sp = (bf16_t*)split;
+  if (lora_rows_dy((const bf16_t*)x, ldx, (const bf16_t*)w3, ldw, out, ldo, M, K, r, alpha, sp, ld_split, K2, s)) {
+    LTX_LAUNCH_CHECK();
+    return LTX_OK;
+  }
+  const dim3 grid((unsigned)((M + 31) / 32));
   // 4 waves x K/4 per 32-row block, 4-slot ring: 16.3 us at M = 14336, K = 2048, r = 16 against
   // 19.9 us for lora_down_kernel (8 waves x K/8 with a 3-slot ring: 17.8 us)
 #define LTX_LORA_ROWS(RR)                                                                             \

@@ -27,6 +27,9 @@
 
 namespace ltx {
 
+#ifndef LTX_LORA_DIAG  // diagnostic builds only (timing of the kernel's parts): 0 = the kernel
+#define LTX_LORA_DIAG 0
+#endif
 namespace {
 constexpr int DY_G = 7;      // row groups of 32 per block (14336 = 64 x 7 x 32)
 constexpr int DY_NR = 4;     // ring slots per wave
@@ -34,9 +37,10 @@ constexpr int DY_COLS = 512; // columns per block
 constexpr int DY_UPAD = DY_G * 32 + 4;  // u^T row length in LDS (floats; +4 spreads the banks)
 }  // namespace
 
-// WP = false: the dB product alone (ltx_lora_wgrad's token-sized path: dw = alpha . Y^T . u on the
-// bf16 matrix core with u's exact three-piece split, where lora_wgrad_kernel runs f32 MFMAs)
-template <int R, bool WP>
+// MODE: bit 0 the w product, bit 1 the dB product. MODE 2 is ltx_lora_wgrad's token-sized path
+// (dw = alpha . Y^T . u on the bf16 matrix core with u's exact three-piece split, where
+// lora_wgrad_kernel runs f32 MFMAs); MODE 1 is ltx_lora_rows' (u = x . A^T from A's pieces).
+template <int R, int MODE>
 __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__ y, int64_t ldy,
                                                       const float* __restrict__ u, int64_t ldu,
                                                       const bf16_t* __restrict__ w3, int64_t ldw,
@@ -84,18 +88,26 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
   for (int g = 0; g < DY_NR - 1; ++g)
     if (g < ng) dma(g);
 
-  // u^T of rows mb .. mb + 32G (zero past M)
-  for (int e = tid; e < DY_G * 32 * RP; e += 512) {
-    const int rr = e / RP, j = e % RP;
-    const int m = mb + rr;
-    ut[j * DY_UPAD + rr] = (m < M && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
+  // u^T of rows mb .. mb + 32G (zero past M): all loads in flight before the first LDS write (a
+  // rolled loop waited out one load round trip per element, ~2 us per block)
+  constexpr int UPT = (DY_G * 32 * RP + 511) / 512;
+  float uv[UPT];
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    const int e = tid + 512 * i, rr = e / RP, j = e % RP, m = mb + rr;
+    uv[i] = ((MODE & 2) && e < DY_G * 32 * RP && m < M && j < R && !(LTX_LORA_DIAG & 1)) ? u[(int64_t)m * ldu + j] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < UPT; ++i) {
+    const int e = tid + 512 * i;
+    if ((MODE & 2) && e < DY_G * 32 * RP) ut[(e % RP) * DY_UPAD + e / RP] = uv[i];
   }
   // B^T pieces of this wave's 64 columns: [k half][piece x JT] (ltx_lora_rows' fragment layout)
   s16x8 bp[2][NF];
 #pragma unroll
   for (int p = 0; p < 3; ++p)
 #pragma unroll
-    for (int t = 0; t < JT && WP; ++t) {
+    for (int t = 0; t < JT && (MODE & 1); ++t) {
       const bf16_t* src = w3 + (int64_t)(p * RP + t * 16 + (lane & 15)) * ldw + c0 + (lane >> 4) * 8;
       bp[0][p * JT + t] = *(const s16x8*)src;
       bp[1][p * JT + t] = *(const s16x8*)(src + 32);
@@ -142,12 +154,12 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
     const char* sl = smem + wave * (DY_NR * 4096) + (g % DY_NR) * 4096;
     s16x8 xf[2][2];
 #pragma unroll
-    for (int q = 0; q < 2 && WP; ++q)
+    for (int q = 0; q < 2 && (MODE & 1); ++q)
 #pragma unroll
       for (int h = 0; h < 2; ++h) xf[q][h] = *(const s16x8*)(sl + roff[q][h]);
     s16x8 yb[4];
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
+    for (int nb = 0; nb < 4 && (MODE & 2); ++nb) {
       const s16x4 b0 = tr4(sl + toffs[nb]), b1 = tr4(sl + toffs[nb] + 16 * 128);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -158,7 +170,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
     // u pieces of this group's rows in the k-slot order: [piece][t]
     s16x8 up[3][JT];
 #pragma unroll
-    for (int t = 0; t < JT; ++t) {
+    for (int t = 0; t < JT && (MODE & 2); ++t) {
       const float* ur = ut + (16 * t + (lane & 15)) * DY_UPAD + 32 * g + 4 * g4;
       const f32x4 lo4 = *(const f32x4*)ur, hi4 = *(const f32x4*)(ur + 16);
 #pragma unroll
@@ -176,7 +188,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot g read: its ring slot may be refilled
     if (g + DY_NR - 1 < ng) dma(g + DY_NR - 1);
 #pragma unroll
-    for (int h = 0; h < 2 && WP; ++h)
+    for (int h = 0; h < 2 && (MODE & 1); ++h)
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
           for (int q = 0; q < 2; ++q)
             wacc[g][q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[q][h], bp[h][p * JT + t], wacc[g][q][t], 0, 0, 0);
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
+    for (int p = 0; p < 3 && (MODE & 2) && !(LTX_LORA_DIAG & 2); ++p)
 #pragma unroll
       for (int t = 0; t < JT; ++t)
 #pragma unroll
@@ -194,35 +206,38 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
   }
   // dB partial: C[j][n] -> part_b[rs][n][j], lane: n = c0 + 16 nb + (lane & 15), j = 16t + 4 g4 + 0..3
 #pragma unroll
-  for (int t = 0; t < JT; ++t)
+  for (int t = 0; t < JT && (MODE & 2); ++t)
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       const int n = c0 + 16 * nb + (lane & 15);
-      *(f32x4*)(part_b + ((int64_t)rs * N + n) * RP + 16 * t + 4 * g4) = bacc[t][nb];
+      if (!(LTX_LORA_DIAG & 4)) *(f32x4*)(part_b + ((int64_t)rs * N + n) * RP + 16 * t + 4 * g4) = bacc[t][nb];
     }
-  if constexpr (!WP) return;
-  // w partial: the 8 waves' [32G rows][RP] sums through LDS (the ring is free once all waves are
-  // past their last slot), then one column-split partial per row
+  if constexpr (!(MODE & 1)) return;
+  // w partial: the 8 waves' [j][32G rows] sums through LDS (the ring is free once all waves are
+  // past their last slot; a C fragment's 4 values are 4 consecutive rows of one j: one 16-B write),
+  // then one column-split partial part_w[cs][j][m] per row quad (16-B reads and stores)
   __syncthreads();
-  float(*part)[DY_G * 32][RP + 1] = (float(*)[DY_G * 32][RP + 1])smem;
+  constexpr int WROW = DY_G * 32 + 4;  // floats per (wave, j) row; +4 spreads the banks
+  float* part = (float*)smem;
+  static_assert(8 * RP * WROW * 4 <= RING, "w partials fit the ring");
 #pragma unroll
   for (int g = 0; g < DY_G; ++g)
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int t = 0; t < JT; ++t)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
-          part[wave][32 * g + 16 * q + 4 * g4 + rr][16 * t + (lane & 15)] = wacc[g][q][t][rr];
+        *(f32x4*)(part + (wave * RP + 16 * t + (lane & 15)) * WROW + 32 * g + 16 * q + 4 * g4) = wacc[g][q][t];
   __syncthreads();
-  for (int e = tid; e < DY_G * 32 * RP; e += 512) {
-    const int rr = e / RP, j = e % RP;
-    const int m = mb + rr;
-    if (m >= M) continue;
-    float sum = 0.f;
+  for (int e = tid; e < RP * DY_G * 8; e += 512) {  // (j, row quad)
+    const int j = e / (DY_G * 8), r4 = 4 * (e % (DY_G * 8));
+    if (mb + r4 >= M) continue;  // M % 32 == 0: a quad is all in or all out
+    f32x4 sum = *(const f32x4*)(part + j * WROW + r4);
 #pragma unroll
-    for (int w = 0; w < 8; ++w) sum += part[w][rr][j];
-    part_w[((int64_t)cs * M + m) * RP + j] = sum;
+    for (int w = 1; w < 8; ++w) {
+      const f32x4 v = *(const f32x4*)(part + (w * RP + j) * WROW + r4);
+      sum[0] += v[0]; sum[1] += v[1]; sum[2] += v[2]; sum[3] += v[3];
+    }
+    *(f32x4*)(part_w + ((int64_t)cs * RP + j) * M + mb + r4) = sum;
   }
 }
 
@@ -239,20 +254,46 @@ __global__ __launch_bounds__(256) void lora_dy_finish_kernel(const float* __rest
                                                              int accumulate, int nwb) {
   constexpr int RP = R >= 16 ? R : 16;
   if ((int)blockIdx.x < nwb) {
+    // thread (j quad q, row m), m fastest (the partial reads coalesce): w[m][4q..4q+3],
+    // split[m][4q..] = split[m][R + 4q..] = hi, split[m][2R + 4q..] = lo, and the zero padding
+    // columns 3R + 4q + kR < K2 (the R / 4 quads of a row cover 3R .. K2 between them)
+    constexpr int NQ = R / 4;
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= (int64_t)M * K2) return;
-    const int m = (int)(e / K2), c = (int)(e % K2);
-    if (c >= 3 * R) {
-      split[(int64_t)m * lds + c] = (bf16_t)0;
-      return;
+    if (e >= (int64_t)M * NQ) return;
+    const int q = (int)(e / M), m = (int)(e % M);
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    int c = 0;
+    for (; c + 4 <= CS; c += 4) {  // 16 loads in flight, summed in split order
+      float t[4][4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[cc][k] = part_w[((int64_t)(c + cc) * RP + 4 * q + k) * M + m];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] += t[cc][k];
     }
-    const int j = c % R;
-    float sum = 0.f;
-    for (int s = 0; s < CS; ++s) sum += part_w[((int64_t)s * M + m) * RP + j];
-    const float v = sum * alpha;
-    const bf16_t hi = f2bf(v);
-    if (c < R) w[(int64_t)m * ldw_out + j] = v;
-    split[(int64_t)m * lds + c] = c < 2 * R ? hi : f2bf(v - bf2f(hi));
+    for (; c < CS; ++c)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] += part_w[((int64_t)c * RP + 4 * q + k) * M + m];
+    f32x4 wv;
+    uint32_t hi[2], lo[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wv[k] = v[k] * alpha;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bf16_t h0 = f2bf(wv[2 * k]), h1 = f2bf(wv[2 * k + 1]);
+      hi[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      lo[k] = (uint32_t)f2bf(wv[2 * k] - bf2f(h0)) | ((uint32_t)f2bf(wv[2 * k + 1] - bf2f(h1)) << 16);
+    }
+    *(f32x4*)(w + (int64_t)m * ldw_out + 4 * q) = wv;
+    if (split == nullptr) return;
+    bf16_t* sr = split + (int64_t)m * lds;
+    *(u32x2*)(sr + 4 * q) = (u32x2){hi[0], hi[1]};
+    *(u32x2*)(sr + R + 4 * q) = (u32x2){hi[0], hi[1]};
+    *(u32x2*)(sr + 2 * R + 4 * q) = (u32x2){lo[0], lo[1]};
+    for (int c = 3 * R + 4 * q; c < K2; c += R) *(u32x2*)(sr + c) = (u32x2){0u, 0u};
     return;
   }
   __shared__ float red[4][64];
@@ -293,7 +334,7 @@ bool lora_wgrad_rows(const bf16_t* y, int64_t ldy, const float* u, int64_t ldu, 
   const dim3 grid((unsigned)(N / DY_COLS), (unsigned)RS);
   const dim3 g2((unsigned)((N * r + 63) / 64));
 #define LTX_LORA_WG(RR)                                                                                       \
-  hipLaunchKernelGGL((lora_dy_kernel<RR, false>), grid, dim3(512), 0, s, y, ldy, u, ldu, nullptr, (int64_t)0, \
+  hipLaunchKernelGGL((lora_dy_kernel<RR, 2>), grid, dim3(512), 0, s, y, ldy, u, ldu, nullptr, (int64_t)0, \
                      nullptr, pb, (int)M, (int)N);                                                            \
   hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, nullptr, 0, pb, RS, (int)M, (int)N,    \
                      alpha, nullptr, (int64_t)0, nullptr, (int64_t)0, 0, dw, on, oj, accumulate, 0);
@@ -303,6 +344,44 @@ bool lora_wgrad_rows(const bf16_t* y, int64_t ldy, const float* u, int64_t ldu, 
     LTX_LORA_WG(16)
   }
 #undef LTX_LORA_WG
+  return true;
+}
+
+// ltx_lora_rows' token-sized path (called from lora.hip): out = alpha . x . A^T (and its split
+// operand) through the w product of lora_dy_kernel (MODE 1: eight waves x 64 columns per block,
+// column-split partials in the stream's workspace) and the w half of the finish kernel. Returns
+// false (nothing launched) where it does not apply; LTX_LORA_ROWS_DY=0 at load keeps
+// lora_rows_kernel.
+bool lora_rows_dy(const bf16_t* x, int64_t ldx, const bf16_t* w3, int64_t ldw, float* out, int64_t ldo, int64_t M,
+                  int64_t K, int64_t r, float alpha, bf16_t* split, int64_t ld_split, int64_t K2, hipStream_t s) {
+  static const int enabled = [] {
+    const char* e = getenv("LTX_LORA_ROWS_DY");
+    return e ? atoi(e) : 1;
+  }();
+  if (!enabled || M < 2048 || M % 32 != 0 || K % DY_COLS != 0 || (r != 8 && r != 16)) return false;
+  if (ldx % 8 != 0 || ((uintptr_t)x % 16) != 0 || ldx * 2 * 32 >= ((int64_t)1 << 32)) return false;
+  if (ldw % 8 != 0 || ((uintptr_t)w3 % 16) != 0 || ldw < K) return false;
+  if (ldo % 4 != 0 || ((uintptr_t)out % 16) != 0) return false;
+  if (split && (ld_split % 4 != 0 || ((uintptr_t)split % 8) != 0 || K2 < 3 * r || (K2 - 3 * r) % 4 != 0)) return false;
+  const int64_t RP = r >= 16 ? r : 16;
+  const int CS = (int)(K / DY_COLS), RS = (int)((M + DY_G * 32 - 1) / (DY_G * 32));
+  size_t ws = 0;
+  float* pw = stream_workspace(s, &ws);
+  if (pw == nullptr || (size_t)CS * M * RP * sizeof(float) > ws) return false;
+  const dim3 grid((unsigned)CS, (unsigned)RS);
+  const dim3 g2((unsigned)((M * (r / 4) + 255) / 256));
+  const int nwb = (int)g2.x;
+#define LTX_LORA_RW(RR)                                                                                      \
+  hipLaunchKernelGGL((lora_dy_kernel<RR, 1>), grid, dim3(512), 0, s, x, ldx, nullptr, (int64_t)0, w3, ldw, pw, \
+                     nullptr, (int)M, (int)K);                                                              \
+  hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, pw, CS, nullptr, 0, (int)M, (int)K,    \
+                     alpha, out, ldo, split, ld_split, (int)K2, nullptr, (int64_t)0, (int64_t)0, 0, nwb);
+  if (r == 8) {
+    LTX_LORA_RW(8)
+  } else {
+    LTX_LORA_RW(16)
+  }
+#undef LTX_LORA_RW
   return true;
 }
 
@@ -325,6 +404,8 @@ extern "C" int ltx_lora_dy(const void* y, int64_t ldy, const float* u, int64_t l
                 "lora_dy: 16-B aligned rows of dY and of the pieces");
   LTX_CHECK_ARG(ldy * 2 * 32 < ((int64_t)1 << 32), "lora_dy: 32-bit DMA offsets");
   LTX_CHECK_ARG(ldw_out >= r && ldu >= r && K2 >= 3 * r && K2 % 64 == 0 && ld_split >= K2, "lora_dy: output strides");
+  LTX_CHECK_ARG(ldw_out % 4 == 0 && ((uintptr_t)w % 16) == 0 && ld_split % 4 == 0 && ((uintptr_t)split % 8) == 0,
+                "lora_dy: 16-B aligned w rows, 8-B aligned split rows");
   LTX_CHECK_ARG((on == r && oj == 1) || (on == 1 && oj == N), "lora_dy: dB must be a dense [N,r] or [r,N]");
   const int64_t RP = r >= 16 ? r : 16;
   const int CS = (int)(N / DY_COLS), RS = (int)((M + DY_G * 32 - 1) / (DY_G * 32));
@@ -332,10 +413,10 @@ extern "C" int ltx_lora_dy(const void* y, int64_t ldy, const float* u, int64_t l
   float* pb = workspace + (int64_t)CS * M * RP;
   hipStream_t s = (hipStream_t)stream;
   const dim3 grid((unsigned)CS, (unsigned)RS);
-  const int nwb = (int)((M * K2 + 255) / 256);
+  const int nwb = (int)((M * (r / 4) + 255) / 256);
   const dim3 g2((unsigned)(nwb + (N * r + 63) / 64));
 #define LTX_LORA_DY(RR)                                                                                          \
-  hipLaunchKernelGGL((lora_dy_kernel<RR, true>), grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu,                \
+  hipLaunchKernelGGL((lora_dy_kernel<RR, 3>), grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu,                \
                      (const bf16_t*)w3, ldw3, pw, pb, (int)M, (int)N);                                           \
   LTX_LAUNCH_CHECK();                                                                                            \
   hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, pw, CS, pb, RS, (int)M, (int)N, alpha, w, \

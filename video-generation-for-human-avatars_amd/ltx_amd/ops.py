@@ -653,6 +653,7 @@ def lora_rows(x, w3, r, alpha=1.0, out=None, split=False, split_out=None):
         K2 = lora_k2(r)
         sp = torch.empty(M, K2, dtype=BF16, device=x.device) if split_out is None else split_out
         lds = _rows(sp, "split_out")
+    _gemm_workspace(x.device)  # token-sized calls keep column-split partials in the workspace
     call("ltx_lora_rows", _p(x), _rows(x, "x"), _p(w3), _rows(w3, "w3"), _p(out), _rows(out, "out"),
          M, K, r, float(alpha), _p(sp), lds, K2, _s())
     return (out, sp) if split else out
