@@ -286,6 +286,18 @@ def test_attention_bwd_one_pass(B, H, Nq, Nk, masked, shared, valid, monkeypatch
         assert torch.equal(outs["1"][0], outs["0"][0])  # dQ: per query tile, unaffected
         for a, b_ in zip(outs["1"][1:], outs["0"][1:]):  # dK / dV: f32 partials summed in order
             assert rel(a, b_) < 1e-3
+    if masked:  # every unmasked key in one 32-key block: per-wave sub-tiles (bwd1_few_keys) against
+        # the 8 x 32-key schedule: dQ bitwise, dK / dV to the order of the 8 waves' partial sums
+        monkeypatch.setenv("LTX_ATTN_BWD1", "1")
+        outs = {}
+        for few in ("1", "0"):
+            monkeypatch.setenv("LTX_ATTN_BWD1_FEW", few)
+            outs[few] = ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, kv_shared=shared)
+        assert torch.equal(outs["1"][0], outs["0"][0])
+        for a, b_, r32, er in zip(outs["1"][1:], outs["0"][1:], refs32[1:], e16[1:]):
+            assert rel(a, b_) < 1e-2
+            assert rel(batch_summed(a), r32) <= 1.25 * er + 1e-3, (rel(batch_summed(a), r32), er)
+        monkeypatch.delenv("LTX_ATTN_BWD1_FEW")
     if Nk <= 128:  # the query-split one-pass kernel (QS) against the 8 x 32-key one: dQ bitwise
         monkeypatch.setenv("LTX_ATTN_BWD1", "1")
         outs = {}
@@ -349,6 +361,7 @@ def test_attention_padding_blocks_skipped_exactly(B, H, Nq, Nk, valid, shared, m
     bias = ((1 - keep.to(torch.bfloat16)) * -10000.0).float()
     res = {}
     monkeypatch.setenv("LTX_ATTN_BWD1_QS", "0")  # the 8 x 32-key kernel: bitwise skip invariance
+    monkeypatch.setenv("LTX_ATTN_BWD1_FEW", "0")
     for mode in ("1", "0"):
         monkeypatch.setenv("LTX_ATTN_SKIP", mode)
         o, lse = ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias, kv_shared=shared)
@@ -356,6 +369,18 @@ def test_attention_padding_blocks_skipped_exactly(B, H, Nq, Nk, valid, shared, m
         res[mode] = (o, lse, dq, dk, dv)
     for a, b_ in zip(res["1"], res["0"]):
         assert torch.equal(a, b_)
+    # one active 32-key block (bwd1_few_keys, the default there): dQ bitwise, dK / dV to the order
+    # of the waves' partial sums, every padding key's rows exactly 0
+    monkeypatch.setenv("LTX_ATTN_BWD1_FEW", "1")
+    monkeypatch.setenv("LTX_ATTN_SKIP", "1")
+    dq3, dk3, dv3 = ops.attn_bwd(q, k, v, res["1"][0], do, res["1"][1], B, H, d, scale, key_bias=bias,
+                                 kv_shared=shared)
+    assert torch.equal(dq3, res["1"][2])
+    assert rel(dk3, res["1"][3]) < 1e-2 and rel(dv3, res["1"][4]) < 1e-2
+    pad3 = ~(keep.repeat(B, 1) if shared else keep).reshape(-1)
+    assert float(dk3.view(-1, H * d)[pad3].abs().max()) == 0.0
+    assert float(dv3.view(-1, H * d)[pad3].abs().max()) == 0.0
+    monkeypatch.setenv("LTX_ATTN_BWD1_FEW", "0")
     # the query-split backward (every unmasked key below 128 here): dQ bitwise, dK / dV to the
     # order of two partial sums, padding rows exactly 0
     monkeypatch.setenv("LTX_ATTN_SKIP", "1")

@@ -648,6 +648,268 @@ __global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BI
 // consecutive image rows, which the row swizzle keeps conflict-free.
 // =============================================================================================
 
+// Few unmasked keys (the caption's padded prompt: 16 valid tokens of 256): when every unmasked
+// key of the (batch, head) lies in ONE 32-key block kb, the 8-wave kernel below leaves 7 waves with
+// only a dQ share of each tile and the whole S / dP / dV / dK chain on one wave, behind a barrier
+// per 64-query tile (~2.5 us per tile at config A). Here each wave instead takes its own 32-query
+// sub-tiles (w, w + 8, ...) end to end with no workgroup barrier in the loop:
+//   * Q / dO rows (and the lse / delta words) of a sub-tile by LDS-DMA into a wave-private
+//     2-slot ring, the next sub-tile's DMA in flight while this one computes;
+//   * S, dP, P, dS, dV^T += dO^T.P and dK^T += Q^T.dS exactly as one u-half of attn_bwd1_kernel
+//     (this lane's key = kb * 32 + (lane & 31) in every wave);
+//   * dS (bf16) into a wave-private [32 keys][32 queries] image, dQ^T = K^T.dS^T of the sub-tile
+//     (4 head-dim blocks x 2 query blocks, v_mfma_f32_16x16x32_bf16 over the block's 32 keys: the
+//     same single k-step as the 8-wave kernel's, so dQ is bitwise its dQ);
+//   * the 8 waves' dK / dV partials summed through LDS in wave order at the end (f32 rounding away
+//     from the 8-wave kernel, whose one wave summed every tile in sequence); all other keys' dK /
+//     dV rows are stored as zeros, as there.
+namespace {
+constexpr int FK_SLOT = 2 * 32 * 128 + 256;      // Q | dO (32 rows x 128 B each) | lse | delta
+constexpr int FK_RING = 8 * 2 * FK_SLOT;          // 8 waves x 2 slots
+constexpr int FK_SIMG = 32 * 64;                  // dS image [32 keys][32 queries] bf16, per wave
+constexpr int FK_KIMG = 32 * 128;                 // K rows of the active block
+constexpr int FK_LDS = FK_RING + 8 * FK_SIMG + FK_KIMG;
+static_assert(8 * 4 * 16 * 64 * 4 <= FK_RING, "the dK / dV partials fit the ring");
+}  // namespace
+
+template <int HD>
+__device__ __forceinline__ void bwd1_few_keys(const AttnParams& p, char* smem, int kb, int b, int hh) {
+  static_assert(HD == 64, "head dim 64");
+  constexpr int KS = HD / 16, DS = HD / 32;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const LaneOfs<HD> lofs(lane);
+  char* ring = smem + wave * (2 * FK_SLOT);
+  char* simg = smem + FK_RING + wave * FK_SIMG;
+  char* kimg = smem + FK_RING + 8 * FK_SIMG;
+  const int kl = kb * 32 + (lane & 31);  // this lane's key (the same in every wave)
+  const int kc = min(kl, p.Nk - 1);
+  const float c2 = p.scale * LOG2E;
+  float kbias = -INFINITY;
+  if (kl < p.Nk) kbias = p.key_bias ? p.key_bias[(int64_t)b * p.kvb + kl] * LOG2E : 0.f;
+  const bf16_t* kbase = p.k + (int64_t)b * p.kvb * p.ldk + hh * HD;
+  // sub-tiles of this wave: st = wave + 8 i (32 queries each)
+  const int nsub = (p.Nq + 31) / 32;
+  const int nmine = nsub > wave ? (nsub - wave + 7) / 8 : 0;
+  const bf16_t* qbase = p.q + (int64_t)b * p.Nq * p.ldq + hh * HD;
+  const bf16_t* obase = p.dout + (int64_t)b * p.Nq * p.lddo + hh * HD;
+  const float* lbase = p.lse + ((int64_t)b * p.H + hh) * p.Nq;
+  const float* dbase = p.delta + ((int64_t)b * p.H + hh) * p.Nq;
+  // DMA piece i of a sub-tile: rows 8i + (lane >> 3), physical chunk lane & 7 (the source chunk
+  // swizzled as toff expects); rows past Nq re-read the last row (their lse is set to +inf)
+  auto dma = [&](int i) {
+    const int q0 = (wave + 8 * i) * 32;
+    char* slot = ring + (i & 1) * FK_SLOT;
+#pragma unroll
+    for (int pc = 0; pc < 4; ++pc) {
+      const int row = 8 * pc + (lane >> 3);
+      const int qr = min(q0 + row, p.Nq - 1);
+      const int ch = (lane & 7) ^ swz<HD>(row);
+      dma16s((uint32_t)(qr * p.ldq + ch * 8) * 2, qbase, lds_u32(slot + pc * 1024));
+      dma16s((uint32_t)(qr * p.lddo + ch * 8) * 2, obase, lds_u32(slot + 4096 + pc * 1024));
+    }
+    const int qs = min(q0 + (lane & 31), p.Nq - 1);
+    dma4((lane < 32 ? lbase : dbase) + qs, lds_u32(slot + 8192));
+  };
+  // the first two sub-tiles' DMA goes out ahead of this lane's K / V fragments and the K image
+  // (their latencies overlap); everything retired before the counted waits below
+  if (nmine > 0) dma(0);
+  if (nmine > 1) dma(1);
+  s16x8 kf[KS], vf[KS];
+  {
+    const bf16_t* kr = kbase + (int64_t)kc * p.ldk;
+    const bf16_t* vr = p.v + ((int64_t)b * p.kvb + kc) * p.ldv + hh * HD;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = *(const s16x8*)(kr + ks * 16 + 8 * h);
+      vf[ks] = *(const s16x8*)(vr + ks * 16 + 8 * h);
+    }
+  }
+  if (tid < 256) {  // K image of the block's 32 rows (the dQ product's A operand, swizzled)
+    const int r = tid >> 3, c = tid & 7;
+    const int key = min(kb * 32 + r, p.Nk - 1);
+    *(u32x4*)(kimg + toff<HD>(r, c)) = *(const u32x4*)(kbase + (int64_t)key * p.ldk + c * 8);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  f32x16 dka[DS], dva[DS];
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      dka[d][r] = 0.f;
+      dva[d][r] = 0.f;
+    }
+  // dQ operand offsets: K^T (head-dim block db) and dS^T (query block qb) by transposed reads
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  int offk[4], offs[2];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) offk[db] = toff<HD>(4 * g4 + qq, 2 * db + (pp >> 1)) + 8 * (pp & 1);
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) offs[qb] = toff<32>(4 * g4 + qq, 2 * qb + (pp >> 1)) + 8 * (pp & 1);
+  auto tr4 = [](const char* a) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a);
+  };
+  const int srow = (lane & 31) * 64 + 8 * h;  // this lane's dS image row (+ chunk ^ swizzle)
+  const int sw4 = swz<32>(lane & 31);
+  for (int i = 0; i < nmine; ++i) {
+    // this sub-tile's 9 DMA instructions landed: younger than them are the next sub-tile's 9 (issued
+    // in iteration i - 1) and iteration i - 1's 8 dQ stores (inline asm, so exactly 8; CDNA4's
+    // vmcnt counts stores too)
+    if (i + 1 < nmine && i >= 1) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+    else if (i + 1 < nmine) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else if (i >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int q0 = (wave + 8 * i) * 32;
+    char* slot = ring + (i & 1) * FK_SLOT;
+    const char* qtile = slot;
+    const char* otile = slot + 4096;
+    float* sl = (float*)(slot + 8192);
+    const float* sd = sl + 32;
+    if (q0 + 32 > p.Nq && lane < 32 && q0 + lane >= p.Nq) sl[lane] = INFINITY;  // P = dS = 0 there
+    f32x16 s, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = 0.f;
+      dp[r] = 0.f;
+    }
+    s16x8 qfr[KS], ofr[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qfr[ks] = row_frag<HD>(qtile, 0, ks, lofs);
+      ofr[ks] = row_frag<HD>(otile, 0, ks, lofs);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      s = mfma32(qfr[ks], kf[ks], s);
+      dp = mfma32(ofr[ks], vf[ks], dp);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 l4 = *(const f32x4*)&sl[8 * g + 4 * h];
+      const f32x4 dl4 = *(const f32x4*)&sd[8 * g + 4 * h];
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int r = 4 * g + ii;
+        const float pr = fast_exp2(fmaf(s[r], c2, kbias - l4[ii]));
+        s[r] = pr;
+        dp[r] = pr * (dp[r] - dl4[ii]);
+      }
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      const s16x8 pb = acc_frag(s, ss);
+      const s16x8 sb = acc_frag(dp, ss);
+#pragma unroll
+      for (int d = 0; d < DS; ++d) {
+        dva[d] = mfma32(tr_frag<HD>(otile, 0, ss, d, lofs), pb, dva[d]);
+        dka[d] = mfma32(tr_frag<HD>(qtile, 0, ss, d, lofs), sb, dka[d]);
+      }
+      // registers 8ss + 4gg + ii are queries 16ss + 8gg + 4h + ii: chunk 2ss + gg, half h
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        u32x2 w;
+        w[0] = (unsigned)(unsigned short)sb[4 * gg] | ((unsigned)(unsigned short)sb[4 * gg + 1] << 16);
+        w[1] = (unsigned)(unsigned short)sb[4 * gg + 2] | ((unsigned)(unsigned short)sb[4 * gg + 3] << 16);
+        *(u32x2*)(simg + srow + (((2 * ss + gg) ^ sw4) << 4)) = w;
+      }
+    }
+    // every read of this slot and the dS image writes done: the slot takes sub-tile i + 2
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (i + 2 < nmine) dma(i + 2);
+    // dQ^T (16 dims x 16 queries per MFMA) over the block's 32 keys
+    f32x4 dqa[4][2];
+    s16x8 bv[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const s16x4 b0 = tr4(simg + offs[qb]), b1 = tr4(simg + offs[qb] + 16 * 64);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bv[qb][j] = b0[j];
+        bv[qb][4 + j] = b1[j];
+      }
+    }
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const s16x4 a0 = tr4(kimg + offk[db]), a1 = tr4(kimg + offk[db] + 16 * (HD * 2));
+      s16x8 av;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        av[j] = a0[j];
+        av[4 + j] = a1[j];
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        dqa[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[qb], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
+    // the stores: 8 asm instructions while another sub-tile follows (only the last sub-tile of
+    // the (batch, head) can be ragged, and it is its wave's last)
+    const bool last = i + 1 == nmine;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q = q0 + 16 * qb + (lane & 15);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int64_t off = ((int64_t)b * p.Nq + min(q, p.Nq - 1)) * p.lddq + (int64_t)hh * HD + 16 * db + 4 * g4;
+        if (p.dq_f32) {
+          const f32x4 w = {dqa[db][qb][0] * p.scale, dqa[db][qb][1] * p.scale, dqa[db][qb][2] * p.scale,
+                           dqa[db][qb][3] * p.scale};
+          float* dst = (float*)p.dq + off;
+          if (!last) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(dst), "v"(w) : "memory");
+          else if (q < p.Nq) *(f32x4*)dst = w;
+        } else {
+          u32x2 w;
+          w[0] = pack2(dqa[db][qb][0] * p.scale, dqa[db][qb][1] * p.scale);
+          w[1] = pack2(dqa[db][qb][2] * p.scale, dqa[db][qb][3] * p.scale);
+          bf16_t* dst = (bf16_t*)p.dq + off;
+          if (!last) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(dst), "v"(w) : "memory");
+          else if (q < p.Nq) *(u32x2*)dst = w;
+        }
+      }
+    }
+  }
+  // dK / dV partials of the 8 waves through LDS (the ring is free once every wave is done), summed
+  // in wave order: wave 0 dK, wave 1 dV; waves 2-7 store the zero rows of every other key
+  __syncthreads();
+  float* part = (float*)smem;  // [wave][acc a][r][lane], a = 2 d + (0: dK, 1: dV)
+#pragma unroll
+  for (int d = 0; d < DS; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      part[((wave * 4 + 2 * d) * 16 + r) * 64 + lane] = dka[d][r];
+      part[((wave * 4 + 2 * d + 1) * 16 + r) * 64 + lane] = dva[d][r];
+    }
+  __syncthreads();
+  if (wave < 2) {
+    f32x16 acc[DS];
+#pragma unroll
+    for (int d = 0; d < DS; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float sum = part[((0 * 4 + 2 * d + wave) * 16 + r) * 64 + lane];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) sum += part[((w * 4 + 2 * d + wave) * 16 + r) * 64 + lane];
+        acc[d][r] = sum;
+      }
+    const bool kin = kl < p.Nk;
+    if (wave == 0)
+      store_row_swap<HD>(acc, p.scale, kin ? p.dk + ((int64_t)b * p.Nk + kl) * p.lddk + hh * HD : nullptr, lane);
+    else
+      store_row_swap<HD>(acc, 1.0f, kin ? p.dv + ((int64_t)b * p.Nk + kl) * p.lddv + hh * HD : nullptr, lane);
+  } else {
+    // zero rows: keys outside the block, 16 B per lane-store (8 per 128-B row), dK then dV
+    const int nz = p.Nk - min(32, p.Nk - kb * 32);
+    for (int e = (wave - 2) * 64 + lane; e < 2 * nz * 8; e += 6 * 64) {
+      const int t = e / (nz * 8), rem = e % (nz * 8);
+      int key = rem / 8;
+      if (key >= kb * 32) key += 32;
+      const int c = rem % 8;
+      bf16_t* row = t == 0 ? p.dk + ((int64_t)b * p.Nk + key) * p.lddk : p.dv + ((int64_t)b * p.Nk + key) * p.lddv;
+      *(u32x4*)(row + hh * HD + c * 8) = (u32x4){0u, 0u, 0u, 0u};
+    }
+  }
+}
+
 // QS (biased key ranges): when every unmasked key lies below 128 (the caption's padded prompt),
 // waves w and w + 4 hold the same 32 keys and take the two 32-query halves of each tile (instead
 // of the padding-key waves idling and the others running both halves); their dK / dV partials
@@ -669,7 +931,8 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
   constexpr int STAT = QT * 4;
   constexpr int SLOT = 2 * TILE + 2 * STAT;  // Q | dO | lse | delta
   constexpr int NSLOT = 3;
-  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT + KIMG + 2 * SIMG];
+  constexpr int OLD_LDS = NSLOT * SLOT + KIMG + 2 * SIMG;
+  __shared__ __attribute__((aligned(16))) char smem[(BIAS && !QS && HD == 64 && FK_LDS > OLD_LDS) ? FK_LDS : OLD_LDS];
   char* kimg = smem + NSLOT * SLOT;
   char* simg0 = kimg + KIMG;
 
@@ -691,6 +954,13 @@ __global__ __launch_bounds__(BWD1_THREADS, 1) void attn_bwd1_kernel(const AttnPa
       if (__any(kbv > KEY_MASKED)) kact |= 1u << kb;
     }
     if (kact == 0u) kact = 0xffu;  // no unmasked key at all: keep everything
+  }
+  if constexpr (BIAS && !QS && HD == 64) {
+    // one active 32-key block: every wave takes its own query sub-tiles (bwd1_few_keys)
+    if (p.few_keys && p.qsplit == 1 && __builtin_popcount(kact) == 1) {
+      bwd1_few_keys<HD>(p, smem, __builtin_ctz(kact), b, hh);
+      return;
+    }
   }
   const bool qs = QS && (kact & 0xf0u) == 0u;  // every active key below 128: split the queries
   const int kl = (qs ? (wave & 3) : wave) * 32 + (lane & 31);  // this lane's key
@@ -1083,6 +1353,13 @@ static int bwd1_qs_flag() {
   return (e && e[0] == '1') ? 1 : 0;
 }
 
+// LTX_ATTN_BWD1_FEW=0: the one-pass cross backward keeps the 8 x 32-key schedule when all unmasked
+// keys lie in one 32-key block (read per call; bwd1_few_keys is the default there)
+static int bwd1_few_flag() {
+  const char* e = std::getenv("LTX_ATTN_BWD1_FEW");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 // LTX_ATTN_QSPLIT=0: the one-pass cross backward keeps one workgroup per (batch, head) at any
 // H * B (read per call)
 static int qsplit_flag() {
@@ -1141,6 +1418,7 @@ static int launch_bwd(AttnParams p, float* delta, int delta_ready, hipStream_t s
   p.delta = delta;
   p.xcd_order = xcd_order_flag();
   p.skip_masked = skip_flag();
+  p.few_keys = p.skip_masked && bwd1_few_flag();
   if constexpr (HD == 64) {  // (head dim 32, the tiny config, keeps the split kernels)
     if (p.Nk <= BWD1_KEYS && bwd1_flag()) {  // every key in one workgroup: one-pass backward
       // under 128 (batch, head) pairs the queries are split over S workgroups each (f32 dK / dV

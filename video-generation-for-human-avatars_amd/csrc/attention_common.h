@@ -163,6 +163,9 @@ struct AttnParams {
   // partials [2][qsplit][B][Nk][H*HD] to `part`, summed in order by attn_bwd1_finish_kernel
   int qsplit;
   float* part;
+  // one-pass cross backward: a (batch, head) whose unmasked keys all lie in one 32-key block takes
+  // the per-wave sub-tile schedule (attention.hip bwd1_few_keys)
+  int few_keys;
 };
 
 // per-key additive term in log2 units for keys key0..key0+63 -> LDS
