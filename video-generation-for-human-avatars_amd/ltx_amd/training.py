@@ -24,6 +24,7 @@ from .patchifier import SymmetricPatchifier
 
 
 _LOGN_PARAMS = {}  # (mu, sigma, device) -> the LogNormal's 0-dim device loc / scale
+_QUANTILES = {}  # (q_min, q_max, device, dtype) -> the two quantile levels as one device tensor
 
 
 def sample_timesteps(batch, config, device):
@@ -47,8 +48,14 @@ def sample_timesteps(batch, config, device):
     z = torch.empty(batch, dtype=loc.dtype, device=device).normal_(0.0, 1.0)
     raw = z.mul_(scale).add_(loc).exp_()
     t_raw = raw / (1 + raw)
-    t_low = torch.quantile(t_raw, config.rf_quantile_min)
-    t_high = torch.quantile(t_raw, config.rf_quantile_max)
+    # both bounds from one sort: quantile with a q tensor runs the scalar form's arithmetic per q
+    # (q as an f32 tensor, rank q (n - 1), the same lerp), so the values are those of two calls
+    qkey = (float(config.rf_quantile_min), float(config.rf_quantile_max), str(torch.device(device)), t_raw.dtype)
+    qs = _QUANTILES.get(qkey)
+    if qs is None:
+        qs = torch.tensor([qkey[0], qkey[1]], dtype=t_raw.dtype, device=device)
+        _QUANTILES[qkey] = qs
+    t_low, t_high = torch.quantile(t_raw, qs).unbind(0)
     # clamp against the 0-dim f32 bounds: the reference's float(t_low) is the same f32 value
     # (exact in double, cast back to f32 by clamp), so only the host sync differs
     return t_raw.clamp(min=t_low, max=t_high)
