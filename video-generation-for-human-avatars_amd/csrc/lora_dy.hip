@@ -27,9 +27,6 @@
 
 namespace ltx {
 
-#ifndef LTX_LORA_DIAG  // diagnostic builds only (timing of the kernel's parts): 0 = the kernel
-#define LTX_LORA_DIAG 0
-#endif
 namespace {
 constexpr int DY_G = 7;      // row groups of 32 per block (14336 = 64 x 7 x 32)
 constexpr int DY_NR = 4;     // ring slots per wave
@@ -95,7 +92,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
 #pragma unroll
   for (int i = 0; i < UPT; ++i) {
     const int e = tid + 512 * i, rr = e / RP, j = e % RP, m = mb + rr;
-    uv[i] = ((MODE & 2) && e < DY_G * 32 * RP && m < M && j < R && !(LTX_LORA_DIAG & 1)) ? u[(int64_t)m * ldu + j] : 0.f;
+    uv[i] = ((MODE & 2) && e < DY_G * 32 * RP && m < M && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
   }
 #pragma unroll
   for (int i = 0; i < UPT; ++i) {
@@ -197,7 +194,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
           for (int q = 0; q < 2; ++q)
             wacc[g][q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[q][h], bp[h][p * JT + t], wacc[g][q][t], 0, 0, 0);
 #pragma unroll
-    for (int p = 0; p < 3 && (MODE & 2) && !(LTX_LORA_DIAG & 2); ++p)
+    for (int p = 0; p < 3 && (MODE & 2); ++p)
 #pragma unroll
       for (int t = 0; t < JT; ++t)
 #pragma unroll
@@ -210,7 +207,7 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       const int n = c0 + 16 * nb + (lane & 15);
-      if (!(LTX_LORA_DIAG & 4)) *(f32x4*)(part_b + ((int64_t)rs * N + n) * RP + 16 * t + 4 * g4) = bacc[t][nb];
+      *(f32x4*)(part_b + ((int64_t)rs * N + n) * RP + 16 * t + 4 * g4) = bacc[t][nb];
     }
   if constexpr (!(MODE & 1)) return;
   // w partial: the 8 waves' [j][32G rows] sums through LDS (the ring is free once all waves are
