@@ -280,11 +280,20 @@ STAMP_BODY = 10  # "stamps": the loop body (counted down from ntiles - 1) whose 
 
 def stamp(E, k):
     """s_memtime into s[60 + 2k : 61 + 2k] when the loop counter is STAMP_BODY (diagnostic only)"""
-    if "stamps" not in VARIANT:
+    if "stamps" not in VARIANT or "itemstamps" in VARIANT:
         return
     for t in (f"s_cmp_eq_u32 s{SITER}, {STAMP_BODY}", f"s_cbranch_scc0 L_st{k}_%=",
               f"s_memtime s[{60 + 2 * k}:{61 + 2 * k}]", f"L_st{k}_%=:"):
         E.raw(t)
+
+
+def istamp(E, k):
+    """"itemstamps" (diagnostic): s_memtime into s[60 + 2k : 61 + 2k] at an item-phase boundary of the
+    persistent dK / dV body, every item (the last item's values are stored), retired at once so the
+    generator's counted lgkmcnt waits stay exact"""
+    if "itemstamps" in VARIANT:
+        E.raw(f"s_memtime s[{60 + 2 * k}:{61 + 2 * k}]")
+        E.raw("s_waitcnt lgkmcnt(0)")
 
 
 def half(E, c, b_prev, b_cur, a_set, reads, dma=(), extra=None):
@@ -611,11 +620,13 @@ def _dkdv_p_body():
     a("s_waitcnt vmcnt(0)")
     a("s_branch L_p_item_%=")
     a("L_p_next_%=:")
+    istamp(E, 0)
     # outstanding: the previous item's dK / dV stores (16) -- its K / V region fill (issued an item
     # ago) and this item's tiles 0, 1 (issued at the previous tail) are older
     a("s_waitcnt vmcnt(16)")
     a("L_p_item_%=:")
     a("s_barrier")  # tiles 0, 1 complete in every wave
+    istamp(E, 1)
     # ---- this item's K / V fragments from the region (the wave's own rows), its dK / dV
     # descriptors, the next item's K / V descriptors and Q / dO / lse / delta bases --------------------
     for ks in range(4):
@@ -649,6 +660,7 @@ def _dkdv_p_body():
         a(f"v_accvgpr_write_b32 {a_(r)}, 0")
     for t in addr_regs("A", f"s{SB0}") + addr_regs("TN", f"s{SB0}"):
         a(t)
+    istamp(E, 2)
     for ins in a_reads(0) + lse_reads(0, LSEB[0]):
         E.put(ins)
     a("s_nop 1")
@@ -657,6 +669,7 @@ def _dkdv_p_body():
     a("s_nop 7")
     a("s_nop 7")
     a("s_nop 3")
+    istamp(E, 3)
     b_even, b_odd = b_stream(0, LSEB[0]), b_stream(1, LSEB[1])
     half(E, False, {}, b_even, 1, read_plan(1, TN, 0, 1, LSEB[1]))
     a(f"s_mov_b32 s{STMP}, s{SBD}")
@@ -666,6 +679,8 @@ def _dkdv_p_body():
     a(f"s_mov_b32 s{SITER}, %[iters]")
     if "stamps" in VARIANT:
         a("s_memtime s[72:73]")
+        if "itemstamps" in VARIANT:
+            a("s_waitcnt lgkmcnt(0)")
     a(f"s_cmp_eq_u32 s{SITER}, 0")
     a("s_cbranch_scc1 L_p_tail_%=")
     a("L_p_loop_%=:")
@@ -693,6 +708,8 @@ def _dkdv_p_body():
     a("L_p_tail_%=:")
     if "stamps" in VARIANT:
         a("s_memtime s[74:75]")
+        if "itemstamps" in VARIANT:
+            a("s_waitcnt lgkmcnt(0)")
     # ---- tail start: the next item's tiles 0, 1 into SBD (the past-the-end DMA's buffer) and SB0
     # (tile T-2: every wave past it after the barrier); the tail itself reads only SB1 -------------------
     a("s_waitcnt vmcnt(0)")  # this wave's past-the-end tile DMA into SBD landed
@@ -713,7 +730,9 @@ def _dkdv_p_body():
     half(E, True, b_even, b_odd, None, read_plan(None, TN, 1, None, None))
     half(E, True, b_odd, {}, None, {})
     E.drain("s_waitcnt lgkmcnt(0)")
+    istamp(E, 4)
     p_epilogue(E)
+    istamp(E, 5)
     a(f"s_cmp_eq_u32 s{SITEM}, 1")
     a("s_cbranch_scc1 L_p_done_%=")
     # the next item's ring: tile 0 in SBD, tile 1 in SB0, SB1 (tile T-1) free
@@ -1296,7 +1315,7 @@ def main():
     txt += [f"#define LTX_DKDV_W1P_KV {P_KV}", f"#define LTX_DKDV_W1P_STG {P_STG}", f"#define LTX_DKDV_W1P_TAB {P_TAB}",
             f"#define LTX_DKDV_W1P_ITEM {ITEM_B}", define("LTX_DKDV_W1P_BODY", dkdv_p_body())]
     if diag:
-        VARIANT.update({"stamps"})
+        VARIANT.update({"stamps", "itemstamps"})  # item-phase stamps (tools/dkdv_item_stamps.py)
         txt.append(define("LTX_DKDV_W1P_BODY_V1", dkdv_p_body()))
         VARIANT.clear()
         txt.append("#undef LTX_DKDV_W1P_CLOBBERS")
