@@ -568,6 +568,13 @@ def p_epilogue(E):
                 a(f"buffer_store_dwordx4 {v(32 + 16 * ti + 4 * i, 4)}, {vo}, s[{srd}:{srd + 3}], s{STMP} offen")
 
 
+def zero_acc_mfma(n, z=130):
+    """zero n accumulator tiles a[16 i : 16 i + 15] with one 0 x 0 + 0 MFMA each (v[z : z + 3] = 0): the
+    idle matrix core does what 16 n v_accvgpr_write would cost the wave's issue (+0.0, as those)"""
+    out = [f"v_mov_b32 {v(z + i)}, 0" for i in range(4)] + ["s_nop 2"]
+    return out + [f"v_mfma_f32_32x32x16_bf16 {a_(16 * i, 16)}, {v(z, 4)}, {v(z, 4)}, 0" for i in range(n)]
+
+
 def dkdv_p_body():
     HARD_ACC[0] = True
     try:
@@ -640,6 +647,8 @@ def _dkdv_p_body():
     for i in range(4):
         a(f"ds_read_b128 {v(PRM + 8 + 4 * i, 4)}, {v(TABV)} offset:{ITEM_B + 16 * i}")
     a("s_waitcnt lgkmcnt(0)")
+    for t in zero_acc_mfma(8):  # dV / dK accumulators a[0:127] (read out by the previous epilogue)
+        a(t)
     a("s_nop 4")  # the previous item's stores read SDK / SDV at issue: rewrite after
     for i in range(4):
         rfl(SDK + i, PRM + i)
@@ -656,8 +665,6 @@ def _dkdv_p_body():
         a(f"v_xor_b32 {v(r)}, 0x80008000, {v(r)}")
     for r in range(32):
         a(f"v_accvgpr_write_b32 {a_(160 + r)}, {v(r)}")
-    for r in range(128):
-        a(f"v_accvgpr_write_b32 {a_(r)}, 0")
     for t in addr_regs("A", f"s{SB0}") + addr_regs("TN", f"s{SB0}"):
         a(t)
     istamp(E, 2)
@@ -1164,6 +1171,8 @@ def _dq_p_body():
     for i in range(5):
         a(f"ds_read_b128 {v(66 + 4 * i, 4)}, {v(DP_TABV)} offset:{ITEM_B + 16 * i}")
     a("s_waitcnt lgkmcnt(0)")
+    for t in zero_acc_mfma(4):  # dQ accumulators a[0:63]
+        a(t)
     a("s_nop 4")  # the previous block's stores read DSDQ at issue: rewrite after
     for i in range(4):
         rfl(DSDQ + i, 86 + i)
@@ -1183,8 +1192,6 @@ def _dq_p_body():
         a(f"v_xor_b32 {v(2 + qt)}, 0x80000000, {v(2 + qt)}")
         for r in range(16):
             a(f"v_mov_b32 {v(DNDL(qt) + r)}, {v(2 + qt)}")
-    for r in range(64):
-        a(f"v_accvgpr_write_b32 {a_(r)}, 0")
     for t in dq_addr("A", f"s{SB0}") + dq_addr("TN", f"s{SB0}"):
         a(t)
     for ins in dq_a_reads(0):
