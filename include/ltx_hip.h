@@ -34,7 +34,8 @@ enum {
 /* GEMM epilogues (ltx_gemm_bf16_nt `epilogue`). y = bf16(acc + bias) first, then: */
 enum {
   LTX_EPI_STORE = 0,            /* C = y                                        nn.Linear */
-  LTX_EPI_GELU = 1,             /* aux0 <- y (pre-act, optional); C = bf16(gelu_tanh(y))
+  LTX_EPI_GELU = 1,             /* aux0 <- int16 rint(32767 gelu_tanh'(y) / 2) (optional, the backward's factor);
+                                   C = bf16(gelu_tanh(y)), y = bf16(acc + bias)
                                    attention.py:1237-1238 (diffusers GELU tanh), PixArt proj */
   LTX_EPI_GATED_RESIDUAL = 2,   /* C = bf16(R + bf16(gate[b] * y)); R = aux0, gate = aux1 row b =
                                    m / rows_per_batch (row stride ld1); aux2 <- y (optional, ld2:
@@ -42,7 +43,7 @@ enum {
   LTX_EPI_LORA = 3,             /* C = bf16(y + alpha * U[m,:].Lb[n,:]); U = aux1 f32 [M,rank],
                                    Lb = aux2 f32 [N,rank]      peft lora.Linear, training.py:50-68 */
   LTX_EPI_LORA_RESIDUAL = 4,    /* C = bf16(R + bf16(LORA)); R = aux0        attention.py:285 */
-  LTX_EPI_GELU_BWD = 5,         /* C = bf16(bf16(acc) * gelu_tanh'(F)); F = aux0 (pre-act) */
+  LTX_EPI_GELU_BWD = 5,         /* C = bf16(bf16(acc) * q * 2 / 32767); q = aux0 (int16, as LTX_EPI_GELU stores it) */
   LTX_EPI_ACCUM = 6,            /* C = bf16(R + bf16(acc)); R = aux0 (may alias C); with aux1 (gate
                                    rows, one per batch) also aux2 = bf16(C * gate[m / rows_per_batch])
                                    (the backward's gate multiply, bitwise ltx_gate_mul_bf16) */

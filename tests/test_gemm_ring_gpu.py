@@ -85,8 +85,9 @@ def test_gemm_ring_epilogues_bitwise(M, N, K, B, variant=20):
     b = torch.randn(N, device="cuda", generator=g).bfloat16()
     R = torch.randn(M, N, device="cuda", generator=g).bfloat16()
     gate = torch.randn(B, N, device="cuda", generator=g).bfloat16()
-    pre0, pre1 = torch.empty(M, N, device="cuda").bfloat16(), torch.empty(M, N, device="cuda").bfloat16()
-    # GELU with the pre-activation store (two separate aux buffers)
+    pre0 = torch.empty(M, N, device="cuda", dtype=torch.int16)
+    pre1 = torch.empty(M, N, device="cuda", dtype=torch.int16)
+    # GELU with the store of its derivative (int16 snorm; two separate aux buffers)
     _set(REF)
     o0 = ops.gemm(a, w, bias=b, epilogue="gelu", aux0=pre0)
     _set(variant)
@@ -97,7 +98,7 @@ def test_gemm_ring_epilogues_bitwise(M, N, K, B, variant=20):
     r0, r1 = _both(lambda: ops.gemm(a, w, bias=b, epilogue="gated_residual", aux0=R, aux1=gate,
                                     rows_per_batch=M // B), variant)
     assert _same(r0, r1)
-    r0, r1 = _both(lambda: ops.gemm(a, w, epilogue="gelu_bwd", aux0=R), variant)
+    r0, r1 = _both(lambda: ops.gemm(a, w, epilogue="gelu_bwd", aux0=pre0), variant)
     assert _same(r0, r1)
     acc0, acc1 = R.clone(), R.clone()
     d0, d1 = torch.empty_like(R), torch.empty_like(R)

@@ -76,12 +76,18 @@ def test_gemm_epilogues(M, N, K):
     r, B = 16, 4
     a, w, b = g(M, K, seed=6), g(N, K, seed=7, scale=K ** -0.5), g(N, seed=8)
     y = (a.float() @ w.float().t() + b.float()).to(torch.bfloat16)
-    # GELU + pre-activation store
-    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    # GELU + the backward's factor gelu_tanh'(y) (int16 snorm of d / 2): against ATen at the build's own bf16
+    # y (recovered from the plain store; y itself differs from the fp32-accumulated reference by ulps)
+    pre = torch.empty(M, N, dtype=torch.int16, device=DEV)
     out = ops.gemm(a, w, bias=b, epilogue="gelu", aux0=pre)
-    assert ulps_bad(pre, y, 2) < 1e-3
-    ref = F.gelu(pre.float(), approximate="tanh").to(torch.bfloat16)
+    yb = ops.gemm(a, w, bias=b)
+    assert ulps_bad(yb, y, 2) < 1e-3
+    ref = F.gelu(yb.float(), approximate="tanh").to(torch.bfloat16)
     assert ulps_bad(out, ref, 1) < 1e-3
+    dq = ops.gelu_grad_q(yb)
+    assert int((pre.int() - dq.int()).abs().max()) <= 1  # rint(32767 d / 2) up to the f32 rounding of d
+    assert float((pre.float() / ops.GELU_Q - torch.ops.aten.gelu_backward(
+        torch.ones_like(yb, dtype=torch.float32), yb.float(), approximate="tanh")).abs().max()) < 2 ** -14
     # gated residual
     R = g(M, N, seed=9)
     gate = g(B, N, seed=10)
@@ -97,12 +103,15 @@ def test_gemm_epilogues(M, N, K):
     assert ulps_bad(out, ref, 2) < 2e-3
     out = ops.gemm(a, w, bias=b, epilogue="lora_residual", aux0=R, aux1=u, aux2=lb, alpha=0.5, rank=r)
     assert rel(out, R.float() + ref.float()) < 1e-2
-    # GELU backward
+    # GELU backward: dF = bf16((bf16(acc) * q) * 2 / 32767), q the int16 factor the forward epilogue
+    # keeps (acc * q is exact in f32); end to end against ATen's gelu_backward at F
     Fpre = g(M, N, seed=11)
-    out = ops.gemm(a, w, epilogue="gelu_bwd", aux0=Fpre)
+    q = ops.gelu_grad_q(Fpre)
+    out = ops.gemm(a, w, epilogue="gelu_bwd", aux0=q)
     acc = (a.float() @ w.float().t()).to(torch.bfloat16).float()
-    x = Fpre.float()
-    ref = torch.ops.aten.gelu_backward(acc, x, approximate="tanh")
+    accb = ops.gemm(a, w).float()  # the build's own bf16(acc)
+    assert torch.equal(out, ((accb * q.float()) * (2.0 / 32767.0)).to(torch.bfloat16))
+    ref = torch.ops.aten.gelu_backward(acc, Fpre.float(), approximate="tanh")
     assert rel(out, ref) < 1e-2
     # accumulate (in place on R)
     R2 = R.clone()

@@ -27,7 +27,7 @@ for n in (8192, 2048):
             x = torch.randn(M, k, device="cuda").bfloat16()
             w = (torch.randn(n, k, device="cuda") / k ** 0.5).bfloat16()
             bias = torch.randn(n, device="cuda").bfloat16()
-            pre = torch.empty(M, n, device="cuda", dtype=torch.bfloat16) if epi == "gelu" else None
+            pre = torch.empty(M, n, device="cuda", dtype=torch.int16) if epi == "gelu" else None
             c = torch.empty(M, n, device="cuda", dtype=torch.bfloat16)
             t_l, t_t = [], []
             for _ in range(3):

@@ -36,10 +36,12 @@ for name, n, k, epi in SHAPES:
     bias = torch.randn(n, device="cuda").bfloat16()
     aux0 = aux1 = None
     if epi == "gelu":
-        aux0 = torch.empty(M, n, device="cuda", dtype=torch.bfloat16)
+        aux0 = torch.empty(M, n, device="cuda", dtype=torch.int16)
     aux2, rank = None, 0
     if epi in ("gated_residual", "gelu_bwd", "accum", "store_rowdot"):
         aux0 = torch.randn(M, n, device="cuda").bfloat16()
+    if epi == "gelu_bwd":  # the GELU derivative (int16 snorm)
+        aux0 = (aux0.float().clamp(-1, 1) * 16384).to(torch.int16)
     if epi in ("gated_residual", "accum"):
         aux1 = torch.randn(8, n, device="cuda").bfloat16()
     if epi == "accum":

@@ -90,13 +90,32 @@ __device__ __forceinline__ f32x2 sigmoid2u_pk(f32x2 x, f32x2 x2) {
   return s;
 }
 __device__ __forceinline__ f32x2 gelu_tanh_pk(f32x2 x) { return x * sigmoid2u_pk(x, x * x); }
-// d gelu / dx = s + x s (1 - s) 2u'  (s = sigmoid(2u); 0.5(1 + tanh) = s, 1 - tanh^2 = 4 s (1 - s))
-__device__ __forceinline__ f32x2 gelu_tanh_grad_pk(f32x2 x) {
-  const f32x2 x2 = x * x;
-  const f32x2 s = sigmoid2u_pk(x, x2);
+// d gelu / dx = s + x s (1 - s) 2u'  (s = sigmoid(2u); 0.5(1 + tanh) = s, 1 - tanh^2 = 4 s (1 - s)),
+// from the forward's s: 5 packed ops per pair on top of the GELU itself
+__device__ __forceinline__ f32x2 gelu_tanh_grad_s_pk(f32x2 x, f32x2 x2, f32x2 s) {
   const f32x2 du = __builtin_elementwise_fma(x2, (f32x2)gelu_k::C1, (f32x2)gelu_k::C0);
   return __builtin_elementwise_fma(s * (x * (1.0f - s)), du, s);
 }
+// the same from the GELU output g = x s: s + g (1 - s) 2u' (3 packed ops)
+__device__ __forceinline__ f32x2 gelu_tanh_grad_g_pk(f32x2 x2, f32x2 s, f32x2 g) {
+  const f32x2 du = __builtin_elementwise_fma(x2, (f32x2)gelu_k::C1, (f32x2)gelu_k::C0);
+  return __builtin_elementwise_fma(__builtin_elementwise_fma(-g, s, g), du, s);
+}
+__device__ __forceinline__ f32x2 gelu_tanh_grad_pk(f32x2 x) {
+  const f32x2 x2 = x * x;
+  return gelu_tanh_grad_s_pk(x, x2, sigmoid2u_pk(x, x2));
+}
+// The GELU derivative the forward keeps for the backward, as 16-bit snorm of d / 2 (gelu_tanh' lies
+// in (-0.17, 1.13)): q = rint(32767 clamp(d / 2, -1, 1)), one v_cvt_pknorm_i16_f32 per pair;
+// absolute error <= 2^-15, against fp16's 2^-11 relative near 1. The backward's g * q is exact in f32
+// (8 + 15 significant bits), so dF = bf16((g * q) * 2 / 32767) rounds twice only at the 2^-24 level.
+constexpr float GELU_DQ = 2.0f / 32767.0f;
+__device__ __forceinline__ uint32_t pack_gelu_q(f32x2 d) {
+  const f32x2 h = d * 0.5f;
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pknorm_i16(h[0], h[1]));
+}
+__device__ __forceinline__ float gelu_qlo(uint32_t w) { return (float)(int16_t)(uint16_t)w; }
+__device__ __forceinline__ float gelu_qhi(uint32_t w) { return (float)((int32_t)w >> 16); }
 
 // d gelu_tanh / dx, same association as ATen's GeluBackward (approximate="tanh"); the caller
 // multiplies by dy

@@ -131,20 +131,27 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       ((float*)p.aux1)[((int64_t)(m / rpb) * H + n0 / hd) * rpb + m % rpb] = s;
     }
   } else if constexpr (EPI == LTX_EPI_GELU) {
-    // aux0: optional pre-activation store (bf16, ld0) for the backward
+    // aux0 (optional, int16 snorm of d / 2, ld0): the backward's factor d = gelu_tanh'(y) at the bf16
+    // pre-activation y, from the GELU's own sigmoid (the backward then multiplies: no transcendental)
     if (p.aux0) {
       u32x4 pk;
-      pk[0] = (unsigned)cvals[0] | ((unsigned)cvals[1] << 16);
-      pk[1] = (unsigned)cvals[2] | ((unsigned)cvals[3] << 16);
-      pk[2] = (unsigned)cvals[4] | ((unsigned)cvals[5] << 16);
-      pk[3] = (unsigned)cvals[6] | ((unsigned)cvals[7] << 16);
-      *(u32x4*)((bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0) = pk;
-    }
 #pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const f32x2 g = gelu_tanh_pk((f32x2){v[j], v[j + 1]});
-      out8[j] = g[0];
-      out8[j + 1] = g[1];
+      for (int j = 0; j < 8; j += 2) {
+        const f32x2 x = {v[j], v[j + 1]}, x2 = x * x;
+        const f32x2 s = sigmoid2u_pk(x, x2);
+        const f32x2 g = x * s, d = gelu_tanh_grad_g_pk(x2, s, g);
+        out8[j] = g[0];
+        out8[j + 1] = g[1];
+        pk[j >> 1] = pack_gelu_q(d);
+      }
+      *(u32x4*)((uint16_t*)p.aux0 + (int64_t)m * p.ld0 + n0) = pk;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const f32x2 g = gelu_tanh_pk((f32x2){v[j], v[j + 1]});
+        out8[j] = g[0];
+        out8[j + 1] = g[1];
+      }
     }
   } else if constexpr (EPI == LTX_EPI_GATED_RESIDUAL) {
     // out = R + bf16(gate[b] * y): aux0 = R [M,N] (ld0), aux1 = gate rows (batch stride ld1);
@@ -187,14 +194,13 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
       for (int j = 0; j < 8; ++j) out8[j] = bf2f((bf16_t)(r4[j >> 1] >> ((j & 1) * 16))) + rbf(out8[j]);
     }
   } else if constexpr (EPI == LTX_EPI_GELU_BWD) {
-    // dF = bf16(bf16(acc) * gelu'(F)), F = aux0 pre-activation bf16 (ld0)
-    const u32x4 f4 = pre ? pre->a : *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
+    // dF = bf16(bf16(acc) * q * 2 / 32767), q = aux0 (int16, ld0): gelu_tanh'(F) as the LTX_EPI_GELU
+    // forward kept it (acc * q is exact in f32)
+    const u32x4 f4 = pre ? pre->a : *(const u32x4*)((const uint16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const f32x2 f = {bf2f((bf16_t)f4[j >> 1]), bf2f((bf16_t)(f4[j >> 1] >> 16))};
-      const f32x2 g = (f32x2){v[j], v[j + 1]} * gelu_tanh_grad_pk(f);
-      out8[j] = g[0];
-      out8[j + 1] = g[1];
+      out8[j] = (v[j] * gelu_qlo(f4[j >> 1])) * GELU_DQ;
+      out8[j + 1] = (v[j + 1] * gelu_qhi(f4[j >> 1])) * GELU_DQ;
     }
   } else if constexpr (EPI == LTX_EPI_ACCUM) {
     // out = R + bf16(acc): R = aux0 (ld0); C may alias R. With aux1 (gate rows of the batch,

@@ -550,6 +550,8 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
         raise ValueError(f"gemm: K mismatch {K} vs {K2}")
     out = torch.empty(M, N, dtype=BF16, device=a.device) if out is None else out
     ld0 = _rows(aux0, "aux0") if aux0 is not None else 0
+    if epilogue in ("gelu", "gelu_bwd") and aux0 is not None:  # the GELU derivative, int16 snorm
+        _need(aux0, torch.int16, f"gemm {epilogue} aux0 (int16 snorm of gelu_tanh' / 2)")
     if epilogue == "store_rowdot":  # aux1: the dense f32 [B, N / head_dim, rows_per_batch] delta
         _need(aux1, F32, "gemm store_rowdot delta")
         if not aux1.is_contiguous() or aux1.numel() != M * (N // max(rank, 1)):
@@ -579,15 +581,25 @@ def gemm(a, w, bias=None, epilogue="store", out=None, aux0=None, aux1=None, aux2
 _AUX_ROW_READ = {"gated_residual", "gelu_bwd", "accum", "store_rowdot", "lora_residual"}
 
 
+GELU_Q = 32767.0 / 2.0  # the GELU epilogue's derivative store: int16 q = rint(GELU_Q * gelu_tanh'(y))
+
+
+def gelu_grad_q(y):
+    """the GELU epilogue's aux0 for a pre-activation y (torch statement of what the kernel stores):
+    int16 rint(32767 * clamp(gelu_tanh'(y) / 2, -1, 1)); the backward multiplies by q / GELU_Q"""
+    d = torch.ops.aten.gelu_backward(torch.ones_like(y, dtype=torch.float32), y.float(), approximate="tanh")
+    return torch.round((d * 0.5).clamp(-1, 1) * 32767.0).to(torch.int16)
+
+
 def gemm_algorithmic_bytes(M, N, K, K2, epilogue, has_aux0, has_aux2):
     """Bytes one ltx_gemm launch must move at minimum: A, W (and the K-extension A2, W2) read once,
-    C written once, plus the epilogue's [M, N] bf16 aux rows (residual / GELU pre-activation /
+    C written once, plus the epilogue's [M, N] 2-byte aux rows (residual / GELU derivative /
     accumulator / attention output for delta) read or written once."""
     b = 2.0 * (M * K + N * K + M * N) + 2.0 * (M + N) * K2
     if epilogue in _AUX_ROW_READ or (epilogue == "lora_dgrad_accum" and has_aux0):
         b += 2.0 * M * N
     if (epilogue == "gelu" and has_aux0) or (epilogue in ("gated_residual", "accum") and has_aux2):
-        b += 2.0 * M * N  # pre-activation / pre-gate store, or the accumulate's gated copy
+        b += 2.0 * M * N  # GELU-derivative / pre-gate store, or the accumulate's gated copy
     return b
 
 

@@ -508,7 +508,9 @@ class _BlockFn(torch.autograd.Function):
             h2 = ops.gemm(o2, wo, bias=bo, epilogue="accum", aux0=h1)
         # ---- 3. norm2 + AdaLN(mlp) -> FF (tanh-GELU fused) -> gated residual
         x2, rstd2 = ops.rmsnorm_modulate_fwd(h2, mods[:, 3], onep[:, 4], ldm, rpm, blk.norm_eps)
-        fpre = torch.empty(M, ff.net[0].proj.out_features, dtype=torch.bfloat16, device=h.device)
+        # fpre: rint(32767 gelu_tanh'(pre-activation) / 2) (int16), kept by the GELU epilogue for the
+        # backward's multiply (ltx_hip.h LTX_EPI_GELU)
+        fpre = torch.empty(M, ff.net[0].proj.out_features, dtype=torch.int16, device=h.device)
         act = ops.gemm(x2, ff.net[0].proj.weight, bias=ff.net[0].proj.bias, epilogue="gelu",
                        aux0=fpre)
         del x2
@@ -757,7 +759,7 @@ class _CaptionProjFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, enc, w1, b1, w2, b2):
-        pre = torch.empty(enc.shape[0], w1.shape[0], dtype=torch.bfloat16, device=enc.device)
+        pre = torch.empty(enc.shape[0], w1.shape[0], dtype=torch.int16, device=enc.device)  # gelu' / 2 as int16 snorm
         act = ops.gemm(enc, w1, bias=b1, epilogue="gelu", aux0=pre)
         out = ops.gemm(act, w2, bias=b2)
         ctx.save_for_backward(enc, pre, act, w2)
