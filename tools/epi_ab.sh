@@ -1,6 +1,9 @@
 #!/bin/bash
-# attention tests, the dK/dV item stamps (diag library), then an interleaved A/B of the baseline
-# library (libltxhip_base.so, built from the previous commit) against the tree's libltxhip.so
+# attention tests, the dK/dV item stamps (diag library, tools/build_diag.sh), then an interleaved A/B
+# of a baseline library against the tree's libltxhip.so. The baseline is built by hand beforehand:
+#   git stash; make -C video-generation-for-human-avatars_amd/csrc ARCH=gfx950;
+#   cp video-generation-for-human-avatars_amd/ltx_amd/libltxhip{,_base}.so; git stash pop; make ... again
+# env ATTN_ONLY=1 (attention microbench only), ROUNDS (default 2)
 R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
 L=$R/video-generation-for-human-avatars_amd/ltx_amd
 timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_attention_large_logits_gpu.py -m gpu -x -q \
