@@ -81,6 +81,26 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
         : "memory", "scc");
   };
   const int ng = min(DY_G, (M - mb + 31) / 32);  // row groups of this block
+  // B^T pieces of this wave's 64 columns: [k half][piece x JT] (ltx_lora_rows' fragment layout).
+  // Loaded first and retired, then handed to hipcc as asm outputs: its own waits for these loads
+  // are counted without the asm DMA, and inside the slot loop they drained the prefetched slots
+  // (vmcnt(5) .. vmcnt(0) before every slot's MFMAs)
+  s16x8 bp[2][NF];
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+#pragma unroll
+    for (int t = 0; t < JT && (MODE & 1); ++t) {
+      const bf16_t* src = w3 + (int64_t)(p * RP + t * 16 + (lane & 15)) * ldw + c0 + (lane >> 4) * 8;
+      bp[0][p * JT + t] = *(const s16x8*)src;
+      bp[1][p * JT + t] = *(const s16x8*)(src + 32);
+    }
+  if constexpr ((MODE & 1) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bp[h][f]));
+  }
   // the first slots' DMA goes out ahead of the u^T staging loads, so their latencies overlap
   for (int g = 0; g < DY_NR - 1; ++g)
     if (g < ng) dma(g);
@@ -99,16 +119,6 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
     const int e = tid + 512 * i;
     if ((MODE & 2) && e < DY_G * 32 * RP) ut[(e % RP) * DY_UPAD + e / RP] = uv[i];
   }
-  // B^T pieces of this wave's 64 columns: [k half][piece x JT] (ltx_lora_rows' fragment layout)
-  s16x8 bp[2][NF];
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-#pragma unroll
-    for (int t = 0; t < JT && (MODE & 1); ++t) {
-      const bf16_t* src = w3 + (int64_t)(p * RP + t * 16 + (lane & 15)) * ldw + c0 + (lane >> 4) * 8;
-      bp[0][p * JT + t] = *(const s16x8*)src;
-      bp[1][p * JT + t] = *(const s16x8*)(src + 32);
-    }
   __syncthreads();  // u^T staged; every ordinary load retired before the counted waits below
 
   // row reads (w product): rows 16q + (lane & 15), logical chunk 4h + (lane >> 4)
