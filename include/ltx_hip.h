@@ -195,6 +195,9 @@ int ltx_attn_fwd(const void* q, int64_t ldq, const void* k, int64_t ldk, const v
                  int64_t ldv, void* o, int64_t ldo, float* lse, const float* key_bias, int64_t B,
                  int64_t H, int64_t Nq, int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale,
                  void* stream);
+/* The attention path's LTX_ATTN_* A/B switches are read from the environment once, at the first
+ * attention launch; this re-reads them (tests comparing two kernel paths in one process). */
+int ltx_attn_reload_switches(void);
 /* Backward (deterministic, no atomics): delta[b,h,i] = sum_d dO*O (f32, caller workspace
  * [B,H,Nq]); dQ [B,Nq,H,d] (f32 if dq_is_f32 else bf16, row stride lddq), dK/dV bf16. lse as
  * written by ltx_attn_fwd (log2 units). */

@@ -171,8 +171,10 @@ def test_attention_large_logits(B, Bk, H, Nq, Nk, valid, jump_every):
         e_ref = rel(x16, x32)
         e = rel(a, x32)
         assert e <= 1.25 * e_ref + 1e-3, (n, e, e_ref)
-        if tau0 is not None:
+        if tau0 is not None:  # without the build the comparison is reported as skipped below
             a0 = tau0[i]
             e0 = rel(a0, x32)
             assert e0 <= 1.25 * e_ref + 1e-3, (n, e0, e_ref)
             assert rel(a, a0) <= 2.0 * e_ref + 1e-3, (n, rel(a, a0), e_ref)
+    if tau0 is None:
+        pytest.skip("libltxhip_tau0.so not built: the fp32 checks passed, the RESCALE_TAU = 0 comparison did not run")

@@ -152,6 +152,22 @@ def test_two_blocks_b8_shared_prompt():
     _compare_model("A 2-block B8", cfg, params, d)
 
 
+@pytest.mark.timeout(600)
+def test_config_a_exact_28_layers_b8():
+    """Config A's benched shape in ONE comparison (VERDICT r05 #5a): the full 28-layer LTX-2B at
+    B = 8, N = 1792 (7x16x16), one shared 256-token prompt with 16 valid tokens (bench.py's
+    text_shared path), one train_step against the oracle in fp32 and bf16 on the same inputs and
+    weights: out.sample, the loss and every trainable gradient (28 x 8 LoRA tensors + the caption
+    projection) under SURVEY 8(c)-4's noise criterion."""
+    from ltx_amd.transformer3d import OURS_TRANSFORMER_CONFIG
+    cfg = dict(OURS_TRANSFORMER_CONFIG)
+    assert cfg["num_layers"] == 28
+    params = O.make_params(cfg, 61, lora_rank=16, requires_grad=False)
+    d = _inputs(8, 7, 16, 16, 256, 16, seed=29)
+    _compare_model("A 28-layer B8", cfg, params, d)
+    torch.cuda.empty_cache()
+
+
 def test_ltx2b_loss_curve_shared_prompt():
     """SURVEY 8(c)-5 at LTX-2B widths: 20 optimizer steps (2 blocks, LoRA r=16, B=8 with one
     shared prompt, lr 1e-4): train_step + FusedAdamW vs the oracle + torch AdamW in bf16 and
@@ -246,9 +262,11 @@ def test_ltx2b_28_layers_loss_curve_50_steps():
             ropt.zero_grad(set_to_none=True)
             curves[dt].append(l32)
             del r
-        log.write(f"step {step}: build {curves['build'][-1]:.6f} | oracle trajectories bf16 "
+        b_, h_, f_ = curves["build"][-1], curves["at16"][-1], curves["at32"][-1]
+        margin = abs(b_ - f_) / abs(f_) - 1.25 * abs(h_ - f_) / abs(f_)
+        log.write(f"step {step}: build {b_:.6f} | oracle trajectories bf16 "
                   f"{curves[torch.bfloat16][-1]:.6f} fp32 {curves[torch.float32][-1]:.6f} | oracle at the "
-                  f"build's weights bf16 {curves['at16'][-1]:.6f} fp32 {curves['at32'][-1]:.6f}\n")
+                  f"build's weights bf16 {h_:.6f} fp32 {f_:.6f} | margin {margin:+.3e}\n")
         log.flush()
     log.close()
     # Over 50 optimizer steps the bf16 and fp32 trajectories drift apart (~2 % by step 33) and cross,
@@ -259,15 +277,34 @@ def test_ltx2b_28_layers_loss_curve_50_steps():
     # (b) per step, the noise criterion at a fixed point: the build's loss against the oracle's fp32
     #     loss AT THE BUILD'S OWN WEIGHTS and inputs, within 1.25 x the oracle's bf16 distance from
     #     it at those same weights, + 2e-4 relative (SURVEY 8(c)-4 on one forward; the trajectory
-    #     divergence drops out, since all three evaluate the same weights).
+    #     divergence drops out, since all three evaluate the same weights);
+    # (c) the same fixed-point distances pooled over the 50 steps (VERDICT r05 #5b): the build's mean
+    #     and RMS distance to the fp32 loss at its weights within 1.1 x the oracle-bf16's. A
+    #     per-step margin err - 1.25 ref <= 1e-4 is logged but cannot be the bar: ref is ONE draw of
+    #     the reference's rounding noise per step (it lands within 7.4e-6 of fp32 at one step), and
+    #     with the roles swapped the oracle's own bf16 loss misses that bar against the build at 6
+    #     of r05's 50 steps, the build against the oracle at 4 (r05: build mean 2.49e-4 / RMS
+    #     3.21e-4 vs reference 2.66e-4 / 3.38e-4; worst per-step margin +1.27e-4, the reference's
+    #     against the build +2.9e-4). A systematic
+    #     gradient error moves every step's distance, so it shows in the pooled figures first;
+    # (d) per step, the build's trajectory within 2e-3 relative of the oracle-bf16 trajectory
+    #     (step-level drift of the gradients stays pinned; r05's worst 8.3e-4).
     l32 = curves[torch.float32]
     e_b = [abs(b - f) / abs(f) for b, f in zip(curves["build"], l32)]
     e_r = [abs(h - f) / abs(f) for h, f in zip(curves[torch.bfloat16], l32)]
     rms = lambda v: (sum(x * x for x in v) / len(v)) ** 0.5  # noqa: E731
+    mean = lambda v: sum(v) / len(v)  # noqa: E731
     assert rms(e_b) <= 1.25 * rms(e_r) + 1e-4, (rms(e_b), rms(e_r))
+    fb, fr = [], []
     for i, (b, h, f) in enumerate(zip(curves["build"], curves["at16"], curves["at32"])):
         eb, er = abs(b - f) / abs(f), abs(h - f) / abs(f)
+        fb.append(eb)
+        fr.append(er)
         assert eb <= 1.25 * er + 2e-4, f"28-layer step {i}: build {b}, oracle at its weights bf16 {h} fp32 {f}"
+    assert mean(fb) <= 1.1 * mean(fr), f"pooled fixed-point distance: build {mean(fb):.3e} vs bf16 {mean(fr):.3e}"
+    assert rms(fb) <= 1.1 * rms(fr), f"pooled fixed-point RMS: build {rms(fb):.3e} vs bf16 {rms(fr):.3e}"
+    for i, (b, h) in enumerate(zip(curves["build"], curves[torch.bfloat16])):
+        assert abs(b - h) <= 2e-3 * abs(h), f"28-layer step {i}: build {b} vs oracle-bf16 trajectory {h}"
 
 
 def test_text_stack_matches_per_block():

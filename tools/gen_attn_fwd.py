@@ -1,4 +1,6 @@
-"""Generates video-generation-for-human-avatars_amd/csrc/attn_fwd_body.h: the hand-scheduled main loop of
+"""Generates tools/experiments/attn_fwd_body.h (or the path given as the first argument; `make fwdw1` in
+csrc builds the opt-in library with it -- the kernel is measured slower than the default and is not
+in the shipping build): the hand-scheduled main loop of
 attn_fwd_w1_kernel (attention_pipe.hip), the self-attention forward of F.scaled_dot_product_attention
 (attention.py:1057-1064) for head dim 64 and no key bias, as ONE inline-asm statement.
 
@@ -488,7 +490,8 @@ def clobbers():
 
 def main():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = os.path.join(root, "video-generation-for-human-avatars_amd", "csrc", "attn_fwd_body.h")
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    out = args[0] if args else os.path.join(root, "tools", "experiments", "attn_fwd_body.h")
 
     def define(name, lines):
         return f"#define {name} \\\n" + " \\\n".join(f'  "{l}\\n\\t"' for l in lines) + "\n"

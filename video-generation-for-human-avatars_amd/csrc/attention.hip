@@ -1305,67 +1305,71 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const AttnParams p, flo
 
 static inline bool needs_bias(const AttnParams& p) { return p.key_bias != nullptr || (p.Nk % 64) != 0; }
 
-static int xcd_order_flag() {  // LTX_ATTN_XCD=0: hardware block order (A/B measurement switch)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("LTX_ATTN_XCD");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v;
-}
-
-// LTX_ATTN_BWD1=0: the split dQ + dK/dV kernels for every key range (read per call, so a test
-// can compare both paths in one process)
-static int bwd1_flag() {
-  const char* e = getenv("LTX_ATTN_BWD1");
-  return (e && e[0] == '0') ? 0 : 1;
-}
-
-// LTX_ATTN_W8 (A/B switch, read per call): bit 0 = 8-wave (256-query) tiled forward, bit 1 =
-// 8-wave (256-key) dK/dV kernel; the default is LTX_ATTN_W8_DEFAULT (forward only: self-attention
-// forward 297-305 vs 310-316 us, dK/dV 881-889 vs 857-862 us with 8 waves, tools/attn_bench.py)
 #ifndef LTX_ATTN_W8_DEFAULT
 #define LTX_ATTN_W8_DEFAULT 1
 #endif
-static int waves8_flag(int bit) {
-  const char* e = getenv("LTX_ATTN_W8");
-  const int v = e ? atoi(e) : LTX_ATTN_W8_DEFAULT;
-  return (v >> bit) & 1;
+
+static AttnSwitches read_attn_switches() {
+  AttnSwitches w;
+  auto num = [](const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return (e && e[0]) ? std::atoi(e) : dflt;
+  };
+  auto off0 = [](const char* name) {  // "0..." switches a default-on path off
+    const char* e = std::getenv(name);
+    return (e && e[0] == '0') ? 0 : 1;
+  };
+  w.xcd = off0("LTX_ATTN_XCD");
+  w.bwd1 = off0("LTX_ATTN_BWD1");
+  // bit 0 = 8-wave (256-query) tiled forward, bit 1 = 8-wave (256-key) dK/dV kernel; the default
+  // is the forward only (self-attention forward 297-305 vs 310-316 us, dK/dV 881-889 vs 857-862 us
+  // with 8 waves, tools/attn_bench.py)
+  w.w8 = num("LTX_ATTN_W8", LTX_ATTN_W8_DEFAULT);
+  w.skip = off0("LTX_ATTN_SKIP");
+  w.fwd1 = off0("LTX_ATTN_FWD1");
+  {  // off by default: its step A/B was neutral, and with it dK / dV of the unmasked keys are the sum
+     // of two partials (f32 rounding away from the 8 x 32-key kernel; dQ stays bitwise)
+    const char* e = std::getenv("LTX_ATTN_BWD1_QS");
+    w.bwd1_qs = (e && e[0] == '1') ? 1 : 0;
+  }
+  w.bwd1_few = off0("LTX_ATTN_BWD1_FEW");
+  w.qsplit = off0("LTX_ATTN_QSPLIT");
+  w.dkdv_w1 = num("LTX_ATTN_DKDV_W1", 2);
+  w.dq_w1 = num("LTX_ATTN_DQ_W1", 2);
+  w.dq_pipe = num("LTX_ATTN_DQ_PIPE", 1) != 0;
+  {
+    const char* e = std::getenv("LTX_ATTN_DQ_NBUF");
+    w.dq_nbuf = (e && e[0] == '3') ? 3 : 4;
+  }
+  {
+    const char* e = std::getenv("LTX_ATTN_FWD_W1");
+    w.fwd_w1 = (e && e[0] && e[0] != '0') ? std::atoi(e) : 0;
+  }
+  w.fwd_pipe = num("LTX_ATTN_FWD_PIPE", 1) != 0;
+  w.fwd_f32sum = off0("LTX_ATTN_FWD_F32SUM");
+  w.dkdv_pipe = num("LTX_ATTN_DKDV_PIPE", 1) != 0;
+  {
+    const char* e = std::getenv("LTX_ATTN_DKDV_NBUF");
+    w.dkdv_nbuf = (e && e[0] == '3') ? 3 : 4;
+  }
+  return w;
 }
 
-// LTX_ATTN_SKIP=0: the one-pass kernels keep all-padding key blocks (A/B and exactness tests)
-static int skip_flag() {
-  const char* e = getenv("LTX_ATTN_SKIP");
-  return (e && e[0] == '0') ? 0 : 1;
+static AttnSwitches& switch_table() {
+  static AttnSwitches w = read_attn_switches();
+  return w;
 }
 
-// LTX_ATTN_FWD1=0: the tiled forward (attn_q_kernel) for every key range
-static int fwd1_flag() {
-  const char* e = getenv("LTX_ATTN_FWD1");
-  return (e && e[0] == '0') ? 0 : 1;
-}
+const AttnSwitches& attn_switches() { return switch_table(); }
 
-// LTX_ATTN_BWD1_QS=1: biased key ranges take the query-split one-pass backward (read per call).
-// Off by default: its step A/B was neutral, and with it dK / dV of the unmasked keys are the sum
-// of two partials (f32 rounding away from the 8 x 32-key kernel; dQ stays bitwise)
-static int bwd1_qs_flag() {
-  const char* e = std::getenv("LTX_ATTN_BWD1_QS");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-
-// LTX_ATTN_BWD1_FEW=0: the one-pass cross backward keeps the 8 x 32-key schedule when all unmasked
-// keys lie in one 32-key block (read per call; bwd1_few_keys is the default there)
-static int bwd1_few_flag() {
-  const char* e = std::getenv("LTX_ATTN_BWD1_FEW");
-  return (e && e[0] == '0') ? 0 : 1;
-}
-
-// LTX_ATTN_QSPLIT=0: the one-pass cross backward keeps one workgroup per (batch, head) at any
-// H * B (read per call)
-static int qsplit_flag() {
-  const char* e = std::getenv("LTX_ATTN_QSPLIT");
-  return (e && e[0] == '0') ? 0 : 1;
-}
+static int xcd_order_flag() { return attn_switches().xcd; }
+static int bwd1_flag() { return attn_switches().bwd1; }
+static int waves8_flag(int bit) { return (attn_switches().w8 >> bit) & 1; }
+static int skip_flag() { return attn_switches().skip; }
+static int fwd1_flag() { return attn_switches().fwd1; }
+static int bwd1_qs_flag() { return attn_switches().bwd1_qs; }
+static int bwd1_few_flag() { return attn_switches().bwd1_few; }
+static int qsplit_flag() { return attn_switches().qsplit; }
 
 template <int HD>
 static int launch_fwd(AttnParams p, hipStream_t s) {
@@ -1561,4 +1565,9 @@ extern "C" int ltx_attn_bwd(const void* q, int64_t ldq, const void* k, int64_t l
                             int64_t Nk, int64_t kv_batch_rows, int64_t d, float scale, void* stream) {
   return ltx_attn_bwd_ex(q, ldq, k, ldk, v, ldv, o, ldo, dout, lddo, lse, key_bias, delta_ws, 0, dq, lddq, dq_is_f32,
                          dk, lddk, dv, lddv, B, H, Nq, Nk, kv_batch_rows, d, scale, stream);
+}
+
+extern "C" int ltx_attn_reload_switches(void) {
+  ltx::switch_table() = ltx::read_attn_switches();
+  return LTX_OK;
 }

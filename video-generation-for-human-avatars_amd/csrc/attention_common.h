@@ -140,6 +140,31 @@ __device__ __forceinline__ void dma4(const void* gsrc, uint32_t lds) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds) : "memory");
 }
 
+// The attention path's A/B switches (LTX_ATTN_*), read from the environment ONCE (first launch)
+// into this table; ltx_attn_reload_switches() re-reads them (tests that compare two paths in one
+// process; ops.py calls it when it sees an LTX_ATTN_* variable change). Defaults are the shipping
+// configuration. Defined in attention.hip.
+struct AttnSwitches {
+  int xcd = 1;          // LTX_ATTN_XCD=0: hardware block order
+  int bwd1 = 1;         // LTX_ATTN_BWD1=0: split dQ + dK/dV kernels for every key range
+  int w8 = 1;           // LTX_ATTN_W8: bit 0 8-wave tiled forward, bit 1 8-wave dK/dV
+  int skip = 1;         // LTX_ATTN_SKIP=0: one-pass kernels keep all-padding key blocks
+  int fwd1 = 1;         // LTX_ATTN_FWD1=0: tiled forward for every key range
+  int bwd1_qs = 0;      // LTX_ATTN_BWD1_QS=1: query-split one-pass backward for biased ranges
+  int bwd1_few = 1;     // LTX_ATTN_BWD1_FEW=0: keep the 8 x 32-key schedule for few unmasked keys
+  int qsplit = 1;       // LTX_ATTN_QSPLIT=0: one workgroup per (batch, head) at any H * B
+  int dkdv_w1 = 2;      // LTX_ATTN_DKDV_W1: 2 persistent, 1 per block, 0 pipe, 12..16 / 22 diagnostic
+  int dq_w1 = 2;        // LTX_ATTN_DQ_W1: likewise for dQ
+  int dq_pipe = 1;      // LTX_ATTN_DQ_PIPE=0: the plain dQ kernel
+  int dq_nbuf = 4;      // LTX_ATTN_DQ_NBUF=3: 3-buffer ring
+  int fwd_w1 = 0;       // LTX_ATTN_FWD_W1 (only in `make fwdw1` builds)
+  int fwd_pipe = 1;     // LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8>
+  int fwd_f32sum = 1;   // LTX_ATTN_FWD_F32SUM=0: row sums by v_dot2c over the bf16 weights
+  int dkdv_pipe = 1;    // LTX_ATTN_DKDV_PIPE=0: the plain dK/dV kernel
+  int dkdv_nbuf = 4;    // LTX_ATTN_DKDV_NBUF=3: 3-buffer ring
+};
+const AttnSwitches& attn_switches();
+
 struct AttnParams {
   const bf16_t* q; int64_t ldq;
   const bf16_t* k; int64_t ldk;

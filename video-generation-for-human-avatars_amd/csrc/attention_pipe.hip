@@ -21,7 +21,9 @@
 
 #include "attention_common.h"
 #include "attn_bwd_body.h"
+#ifdef LTX_FWD_W1  // `make fwdw1`: the one-wave forward (measured slower, not in the shipping build)
 #include "attn_fwd_body.h"
+#endif
 #ifdef LTX_DKDV_DIAG  // `make diag`: timing-only variants of the loop (tools/gen_attn_bwd.py --diag)
 #include "attn_bwd_body_diag.h"
 #endif
@@ -463,13 +465,10 @@ __global__ __launch_bounds__(256, 1) void attn_dkdv_w1_kernel(const AttnParams p
   if constexpr (V > 0) es.stop(p);
 }
 
-// LTX_ATTN_DKDV_W1 (read per call): unset / 2 the persistent one-wave kernel (attn_dkdv_w1p_kernel), 1
+// LTX_ATTN_DKDV_W1 (attn_switches()): unset / 2 the persistent one-wave kernel (attn_dkdv_w1p_kernel), 1
 // one workgroup per key block (attn_dkdv_w1_kernel), 0 attn_dkdv_pipe_kernel, 12..16 / 22 the stamped
 // diagnostic variants (`make diag` builds)
-static int dkdv_w1_mode() {
-  const char* e = std::getenv("LTX_ATTN_DKDV_W1");
-  return e ? std::atoi(e) : 2;
-}
+static int dkdv_w1_mode() { return attn_switches().dkdv_w1; }
 bool dkdv_w1_enabled() { return dkdv_w1_mode() != 0; }
 // LTX_ATTN_DKDV_W1=2 (22: its stamped diagnostic variant): the persistent kernel
 bool dkdv_w1p_enabled() { return dkdv_w1_mode() == 2 || dkdv_w1_mode() == 22; }
@@ -868,12 +867,9 @@ int launch_dq_w1p(const AttnParams& p, hipStream_t s) {
   return LTX_OK;
 }
 
-// LTX_ATTN_DQ_W1 (read per call): unset / 2 the persistent one-wave kernel (bf16 dQ), 1 one workgroup per
+// LTX_ATTN_DQ_W1 (attn_switches()): unset / 2 the persistent one-wave kernel (bf16 dQ), 1 one workgroup per
 // query block, 0 attn_dq_pipe_kernel, 12 / 13 / 22 the stamped diagnostic variants (`make diag` builds)
-static int dq_w1_mode() {
-  const char* e = std::getenv("LTX_ATTN_DQ_W1");
-  return e ? std::atoi(e) : 2;
-}
+static int dq_w1_mode() { return attn_switches().dq_w1; }
 bool dq_w1_enabled() { return dq_w1_mode() != 0; }
 // LTX_ATTN_DQ_W1=2 (22: its stamped diagnostic variant): the persistent kernel
 bool dq_w1p_enabled() { return dq_w1_mode() == 2 || dq_w1_mode() == 22; }
@@ -1124,16 +1120,9 @@ __global__ __launch_bounds__(256, 2) void attn_dq_pipe_kernel(const AttnParams p
   }
 }
 
-bool dq_pipe_enabled() {  // LTX_ATTN_DQ_PIPE=0: the plain dQ kernel (A/B switch)
-  const char* e = std::getenv("LTX_ATTN_DQ_PIPE");  // read per call: tests compare paths in one process
-  const int v = e ? std::atoi(e) : 1;
-  return v != 0;
-}
+bool dq_pipe_enabled() { return attn_switches().dq_pipe != 0; }  // LTX_ATTN_DQ_PIPE=0: the plain dQ kernel
 
-static int dq_nbuf() {  // LTX_ATTN_DQ_NBUF=3: the 3-buffer ring (read per call: A/B in one process)
-  const char* e = std::getenv("LTX_ATTN_DQ_NBUF");
-  return (e && e[0] == '3') ? 3 : 4;
-}
+static int dq_nbuf() { return attn_switches().dq_nbuf; }  // LTX_ATTN_DQ_NBUF=3: the 3-buffer ring
 
 int launch_dq_pipe(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nq + D_QUERIES - 1) / D_QUERIES), (unsigned)p.H, (unsigned)p.B);
@@ -1318,6 +1307,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
   if (qi < p.Nq && h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
 }
 
+#ifdef LTX_FWD_W1
 // =============================================================================================
 // Forward at ONE wave per SIMD (self-attention shapes: no key bias, head dim 64, Nk % 64 == 0, >= 4
 // key tiles): 4 waves x 64 queries (two 32-query tiles per wave) = 256 queries per workgroup, the
@@ -1392,22 +1382,20 @@ __global__ __launch_bounds__(256, 1) void attn_fwd_w1_kernel(const AttnParams p)
   }
 }
 
-// LTX_ATTN_FWD_W1 (read per call): 1 the one-wave forward where it applies; unset / 0 the pipelined
+// LTX_ATTN_FWD_W1 (attn_switches(), `make fwdw1` builds only): 1 the one-wave forward where it applies; unset / 0 the pipelined
 // kernel (12: the diagnostic bodies of tools/build_fwd_variant.sh, stamps into the stream's workspace).
 // Not the default: its loop measures 2008 cycles per 64-key unit against 1024 of MFMA (1284 without
 // the softmax VALU, profiles/r05d_fwd_w1_stamps.txt) -- at two exponentials per MFMA the one-wave
 // schedule adds the VALU to the MFMA time almost linearly, and the eight-wave kernel is faster
 // (220 vs 236 us per layer at config A)
 bool fwd_w1_enabled(const AttnParams& p) {
-  const char* e = std::getenv("LTX_ATTN_FWD_W1");
-  const bool on = e && e[0] != '0';
-  return on && p.Nk % 64 == 0 && p.Nk >= 256;
+  const int on = attn_switches().fwd_w1;
+  return on != 0 && p.Nk % 64 == 0 && p.Nk >= 256;
 }
 
 int launch_fwd_w1(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nq + 255) / 256), (unsigned)p.H, (unsigned)p.B);
-  const char* e = std::getenv("LTX_ATTN_FWD_W1");
-  if (e && std::atoi(e) == 12) {
+  if (attn_switches().fwd_w1 == 12) {
     AttnParams q = p;
     size_t ws = 0;
     q.part = stream_workspace(s, &ws);
@@ -1421,16 +1409,14 @@ int launch_fwd_w1(const AttnParams& p, hipStream_t s) {
   return LTX_OK;
 }
 
-bool fwd_pipe_enabled() {  // LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8> (A/B switch)
-  const char* e = std::getenv("LTX_ATTN_FWD_PIPE");  // read per call: tests compare paths in one process
-  const int v = e ? std::atoi(e) : 1;
-  return v != 0;
-}
+#else
+static bool fwd_w1_enabled(const AttnParams&) { return false; }
+static int launch_fwd_w1(const AttnParams&, hipStream_t) { return LTX_OK; }
+#endif  // LTX_FWD_W1
 
-static bool fwd_f32sum() {  // LTX_ATTN_FWD_F32SUM=0: row sums by v_dot2c over the bf16 weights
-  const char* e = std::getenv("LTX_ATTN_FWD_F32SUM");  // read per call: tests compare paths in one process
-  return !(e && e[0] == '0');
-}
+bool fwd_pipe_enabled() { return attn_switches().fwd_pipe != 0; }  // LTX_ATTN_FWD_PIPE=0: attn_q_kernel<64, 0, false, 8>
+
+static bool fwd_f32sum() { return attn_switches().fwd_f32sum != 0; }  // LTX_ATTN_FWD_F32SUM=0: v_dot2c row sums
 
 int launch_fwd_pipe(const AttnParams& p, hipStream_t s) {
   if (fwd_w1_enabled(p)) return launch_fwd_w1(p, s);
@@ -1443,16 +1429,9 @@ int launch_fwd_pipe(const AttnParams& p, hipStream_t s) {
   return LTX_OK;
 }
 
-bool dkdv_pipe_enabled() {  // LTX_ATTN_DKDV_PIPE=0: the plain dK/dV kernel (A/B switch)
-  const char* e = std::getenv("LTX_ATTN_DKDV_PIPE");  // read per call: tests compare paths in one process
-  const int v = e ? std::atoi(e) : 1;
-  return v != 0;
-}
+bool dkdv_pipe_enabled() { return attn_switches().dkdv_pipe != 0; }  // LTX_ATTN_DKDV_PIPE=0: the plain dK/dV kernel
 
-static int dkdv_nbuf() {  // LTX_ATTN_DKDV_NBUF=3: the 3-buffer ring (read per call: A/B in one process)
-  const char* e = std::getenv("LTX_ATTN_DKDV_NBUF");
-  return (e && e[0] == '3') ? 3 : 4;
-}
+static int dkdv_nbuf() { return attn_switches().dkdv_nbuf; }  // LTX_ATTN_DKDV_NBUF=3: the 3-buffer ring
 
 int launch_dkdv_pipe(const AttnParams& p, hipStream_t s) {
   const dim3 g((unsigned)((p.Nk + P_KEYS - 1) / P_KEYS), (unsigned)p.H, (unsigned)p.B);

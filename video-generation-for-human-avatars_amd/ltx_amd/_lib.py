@@ -51,6 +51,7 @@ _SIGNATURES = {
                      _i64, _f32, _p],
     "ltx_attn_bwd": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _p, _i64, _i32,
                      _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _p],
+    "ltx_attn_reload_switches": [],
     "ltx_attn_bwd_ex": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p, _p, _i32, _p,
                         _i64, _i32, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32,
                         _p],

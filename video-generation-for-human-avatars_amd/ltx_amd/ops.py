@@ -356,11 +356,29 @@ def _env_on(var):
     return v is None or v.strip() not in ("0", "")
 
 
+_ATTN_ENV = ("LTX_ATTN_XCD", "LTX_ATTN_BWD1", "LTX_ATTN_W8", "LTX_ATTN_SKIP", "LTX_ATTN_FWD1",
+             "LTX_ATTN_BWD1_QS", "LTX_ATTN_BWD1_FEW", "LTX_ATTN_QSPLIT", "LTX_ATTN_DKDV_W1",
+             "LTX_ATTN_DQ_W1", "LTX_ATTN_DQ_PIPE", "LTX_ATTN_DQ_NBUF", "LTX_ATTN_FWD_W1",
+             "LTX_ATTN_FWD_PIPE", "LTX_ATTN_FWD_F32SUM", "LTX_ATTN_DKDV_PIPE", "LTX_ATTN_DKDV_NBUF")
+_attn_env_seen = [None]
+
+
+def _attn_env_sync():
+    """The library reads its LTX_ATTN_* switches once (attention_common.h AttnSwitches); when this
+    process changed one since the last attention call (an A/B test), have it read them again."""
+    cur = tuple(os.environ.get(k) for k in _ATTN_ENV)
+    if cur != _attn_env_seen[0]:
+        call("ltx_attn_reload_switches")
+        _attn_env_seen[0] = cur
+
+
 def attn_fwd(q, k, v, B, H, d, scale, key_bias=None, out=None, kv_shared=False):
     """q [B*Nq, >=H*d] row view, k/v [B*Nk, ...] -> (o [B*Nq, H*d], lse [B,H,Nq] f32 log2).
     kv_shared: k/v/key_bias hold ONE batch ([Nk, ...], [1, Nk]) attended by every query batch."""
     Nq = q.shape[0] // B
     Nk = k.shape[0] if kv_shared else k.shape[0] // B
+    _attn_env_sync()
+    _gemm_workspace(q.device)  # split-query partials / diagnostic stamps use the stream's workspace
     o = torch.empty(B * Nq, H * d, dtype=BF16, device=q.device) if out is None else out
     lse = torch.empty(B, H, Nq, dtype=F32, device=q.device)
     bias = "true" if (key_bias is not None or Nk % 64) else "false"
@@ -391,6 +409,8 @@ def attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=None, dq_f32=False, d
     Nq = q.shape[0] // B
     Nk = k.shape[0] if kv_shared else k.shape[0] // B
     dev = q.device
+    _attn_env_sync()
+    _gemm_workspace(dev)  # split-query / few-key partials live in the stream's workspace
     dq = torch.empty(B * Nq, H * d, dtype=F32 if dq_f32 else BF16, device=dev) if dq is None else dq
     dk = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dk is None else dk
     dv = torch.empty(B * Nk, H * d, dtype=BF16, device=dev) if dv is None else dv
