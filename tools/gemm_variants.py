@@ -48,7 +48,7 @@ for name in names:
     aux1 = None
     if epi in ("gated_residual", "accum", "gelu_bwd"):
         pre = torch.randn(m, n, device="cuda").bfloat16()
-    if epi == "gelu_bwd":  # the factor as the GELU forward keeps it: rint(2^14 gelu_tanh'(F))
+    if epi == "gelu_bwd":  # the factor as the GELU forward keeps it: rint(32767 * gelu_tanh'(F) / 2) (ops.GELU_Q)
         pre = ops.gelu_grad_q(pre)
     if epi == "gated_residual":
         aux1 = torch.randn(m // ROWS, n, device="cuda").bfloat16()
