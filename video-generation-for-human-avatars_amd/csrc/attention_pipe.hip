@@ -1251,9 +1251,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               ls[(2 * u + ss) & 3] = __builtin_amdgcn_fdot2_f32_bf16(
-                  __builtin_bit_cast(bf16x2_t, (unsigned)(unsigned short)pk[u][ss][2 * j] |
-                                                   ((unsigned)(unsigned short)pk[u][ss][2 * j + 1] << 16)),
-                  __builtin_bit_cast(bf16x2_t, 0x3F803F80u), ls[(2 * u + ss) & 3], false);
+                  as_bf16x2((unsigned)(unsigned short)pk[u][ss][2 * j] |
+                            ((unsigned)(unsigned short)pk[u][ss][2 * j + 1] << 16)),
+                  as_bf16x2(0x3F803F80u), ls[(2 * u + ss) & 3], false);
           }
         }
       }

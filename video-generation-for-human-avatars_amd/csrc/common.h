@@ -145,6 +145,16 @@ int fail(int code, const std::string& msg);
 // ltx_gemm_set_stream_workspace); kernels on one stream run in order, so any launcher on that
 // stream may use it between its own launches. bytes = 0 when none was set.
 float* stream_workspace(hipStream_t s, size_t* bytes);
+// a packed bf16 pair as the operand type of v_dot2c_f32_bf16 (__builtin_amdgcn_fdot2_f32_bf16).
+// memcpy, not __builtin_bit_cast: this hipcc miscompiles a bit_cast of an ext-vector element into
+// bf16x2 (in an unrolled loop over a u32x4 every use read element 0)
+typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16x2_v as_bf16x2(uint32_t w) {
+  bf16x2_v r;
+  __builtin_memcpy(&r, &w, 4);
+  return r;
+}
+
 }  // namespace ltx
 
 #define LTX_CHECK_ARG(cond, msg)                                   \

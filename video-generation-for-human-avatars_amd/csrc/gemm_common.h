@@ -96,6 +96,32 @@ __device__ __forceinline__ void epi_load(const GemmParams& p, int m, int n0, Epi
     if (p.aux1) x.g = *(const u32x4*)((const bf16_t*)p.aux1 + (int64_t)(m / p.rows_per_batch) * p.ld1 + n0);
 }
 
+// Row-dot of 8 columns (store + delta epilogue): sum of c_j * o_j over bf16 pairs in packed words,
+// one v_dot2c_f32_bf16 per pair (each bf16 x bf16 product is exact in f32), the pairs in column
+// order; then the head's hd / 8 lanes reduce on DPP lane moves (no LDS round trip per step, as
+// __shfl_xor's ds_bpermute had): quad_perm [1,0,3,2] = xor 1, [2,3,0,1] = xor 2, row_half_mirror
+// pairs quad 0 with quad 1 of each 8 lanes (= xor 4 once both quads hold their sums). Every
+// epilogue site hands a row's 8-column chunks to consecutive lanes, so a head of hd = p.rank (32 /
+// 64) columns is hd/8 lanes aligned at a multiple of hd/8 (N % hd == 0, checked at launch). The
+// lane at the head's first chunk stores delta[b][h][row].
+__device__ __forceinline__ void rowdot8(const GemmParams& p, int m, int n0, const u32x4& c4, const u32x4& o4,
+                                        const EpiAux* pre) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    s = __builtin_amdgcn_fdot2_f32_bf16(as_bf16x2(c4[j]), as_bf16x2(o4[j]), s, false);
+  const int hd = p.rank, lanes = hd >> 3;
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
+  s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
+  if (lanes == 8) s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x141, 0xF, 0xF, false));
+  if (pre && pre->di != -1) {  // index precomputed by the caller (no integer division per row)
+    if (pre->di >= 0) ((float*)p.aux1)[pre->di] = s;
+  } else if (((n0 >> 3) & (lanes - 1)) == 0) {
+    const int rpb = p.rows_per_batch, H = p.N / hd;
+    ((float*)p.aux1)[((int64_t)(m / rpb) * H + n0 / hd) * rpb + m % rpb] = s;
+  }
+}
+
 template <int EPI, int R>
 __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0, const bf16_t* cvals,
                                               float* out8, const EpiAux* pre = nullptr) {
@@ -107,29 +133,15 @@ __device__ __forceinline__ void epilogue_row8(const GemmParams& p, int m, int n0
 #pragma unroll
     for (int j = 0; j < 8; ++j) out8[j] = v[j];
   } else if constexpr (EPI == LTX_EPI_STORE_ROWDOT) {
-    // every epilogue site hands a row's 8-column chunks to consecutive lanes, so a head of
-    // hd = p.rank (32 / 64) columns is hd/8 lanes aligned at a multiple of hd/8 (N % hd == 0,
-    // checked at launch): reduce there
     const u32x4 o4 = pre ? pre->a : *(const u32x4*)((const bf16_t*)p.aux0 + (int64_t)m * p.ld0 + n0);
-    float s = 0.f;
+    u32x4 c4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      out8[j] = v[j];
-      s += v[j] * bf2f((bf16_t)(o4[j >> 1] >> ((j & 1) * 16)));
+    for (int j = 0; j < 4; ++j) {
+      out8[2 * j] = v[2 * j];
+      out8[2 * j + 1] = v[2 * j + 1];
+      c4[j] = (uint32_t)(uint16_t)cvals[2 * j] | ((uint32_t)(uint16_t)cvals[2 * j + 1] << 16);
     }
-    // the butterfly on DPP lane moves (no LDS round trip per step, as __shfl_xor's ds_bpermute
-    // had): quad_perm [1,0,3,2] = xor 1, [2,3,0,1] = xor 2, row_half_mirror pairs quad 0 with quad
-    // 1 of each 8 lanes (= xor 4 once both quads hold their sums); the same sums in the same order
-    const int hd = p.rank, lanes = hd >> 3;
-    s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
-    s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
-    if (lanes == 8) s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x141, 0xF, 0xF, false));
-    if (pre && pre->di != -1) {  // index precomputed by the caller (no integer division per row)
-      if (pre->di >= 0) ((float*)p.aux1)[pre->di] = s;
-    } else if (((n0 >> 3) & (lanes - 1)) == 0) {
-      const int rpb = p.rows_per_batch, H = p.N / hd;
-      ((float*)p.aux1)[((int64_t)(m / rpb) * H + n0 / hd) * rpb + m % rpb] = s;
-    }
+    rowdot8(p, m, n0, c4, o4, pre);
   } else if constexpr (EPI == LTX_EPI_GELU) {
     // aux0 (optional, int16 snorm of d / 2, ld0): the backward's factor d = gelu_tanh'(y) at the bf16
     // pre-activation y, from the GELU's own sigmoid (the backward then multiplies: no transcendental)
