@@ -27,6 +27,9 @@
 
 namespace ltx {
 
+#ifndef LTX_RF_NR
+#define LTX_RF_NR 5
+#endif
 namespace {
 constexpr int DY_G = 7;      // row groups of 32 per block (14336 = 64 x 7 x 32)
 constexpr int DY_NR = 4;     // ring slots per wave
@@ -320,6 +323,164 @@ __global__ __launch_bounds__(256) void lora_dy_finish_kernel(const float* __rest
   }
 }
 
+// u = alpha * x . A^T for token-sized M with the whole contraction inside one block (round 6):
+// block = 8 waves on RG row groups of 32 rows, wave w owns the K / 8 = 64 CH contiguous columns
+// from 64 CH w, so the block's rows are complete after its cross-wave sum and u and the split
+// operand leave the kernel directly (the column-split MODE 1 pass needed lora_dy_finish_kernel
+// for the 4 column partials: one more launch and 3.7 MB of partials per call). The wave's A^T
+// pieces (3 x 16 j x 64 CH columns) stay in registers for its RG x CH slots, which stream through
+// the same private 4-slot LDS-DMA ring as lora_dy_kernel (slot = 32 rows x 64 columns, order
+// (group, chunk)). Same exact bf16 products summed in f32; the sum order is per-slot MFMA
+// accumulation, then the 8 wave partials in wave order.
+template <int R, int RG, int CH, int NR>
+__global__ __launch_bounds__(512) void lora_rows_full_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                             const bf16_t* __restrict__ w3, int64_t ldw,
+                                                             float* __restrict__ out, int64_t ldo, int M, float alpha,
+                                                             bf16_t* __restrict__ split, int64_t lds, int K2) {
+  constexpr int RP = R >= 16 ? R : 16;
+  constexpr int JT = RP / 16;
+  constexpr int NF = 3 * JT;
+  constexpr int NS = RG * CH;  // slots per wave
+  constexpr int RING = 8 * NR * 4096;
+  constexpr int PROW = RG * 32 + 4;  // floats per (wave, j) partial row; +4 spreads the banks
+  static_assert(R == 8 || R == 16, "rank 8 or 16");
+  static_assert(8 * RP * PROW * 4 <= RING, "wave partials fit the ring");
+  __shared__ __attribute__((aligned(16))) char smem[RING];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c0 = wave * 64 * CH;
+  const int mb = blockIdx.x * RG * 32;
+  const int ng = min(RG, (M - mb) / 32);  // M % 32 == 0
+  const int ns = ng * CH;
+
+  uint32_t yo[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 8 * i + (lane >> 3);
+    yo[i] = (uint32_t)(row * ldx + (((lane & 7) ^ swz<64>(row)) * 8)) * 2;
+  }
+  const uint32_t lring = lds_u32(smem + wave * (NR * 4096));
+  auto dma = [&](int s) {  // slot s = (group s / CH, chunk s % CH)
+    const char* sb = (const char*)(x + (int64_t)(mb + 32 * (s / CH)) * ldx + c0 + 64 * (s % CH));
+    const uint32_t l = lring + (s % NR) * 4096;
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %6\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %2, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %3, %5\n\t"
+        "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %4, %5\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(yo[0]), "v"(yo[1]), "v"(yo[2]), "v"(yo[3]), "s"(sb), "s"(l)
+        : "memory", "scc");
+  };
+  // the ring's first slots go out first; the pieces' loads overlap them, then everything retires
+  // (hipcc's own waits for the pieces are counted without the asm DMA)
+  for (int s = 0; s < NR - 1; ++s)
+    if (s < ns) dma(s);
+  s16x8 bp[CH][2][NF];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int t = 0; t < JT; ++t) {
+        const bf16_t* src = w3 + (int64_t)(p * RP + t * 16 + (lane & 15)) * ldw + c0 + 64 * c + (lane >> 4) * 8;
+        bp[c][0][p * JT + t] = *(const s16x8*)src;
+        bp[c][1][p * JT + t] = *(const s16x8*)(src + 32);
+      }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int f = 0; f < NF; ++f) asm volatile("" : "+v"(bp[c][h][f]));
+
+  int roff[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 16 * q + (lane & 15);
+      roff[q][h] = row * 128 + (((4 * h + (lane >> 4)) ^ swz<64>(row)) * 16);
+    }
+  f32x4 acc[RG][2][JT];
+#pragma unroll
+  for (int g = 0; g < RG; ++g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int t = 0; t < JT; ++t) acc[g][q][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (s >= ns) break;
+    const int g = s / CH, c = s % CH;
+    const int younger = min(NR - 2, ns - 1 - s);  // slots issued after s
+    if (younger >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const char* sl = smem + wave * (NR * 4096) + (s % NR) * 4096;
+    s16x8 xf[2][2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) xf[q][h] = *(const s16x8*)(sl + roff[q][h]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot s read: its ring slot may be refilled
+    if (s + NR - 1 < ns) dma(s + NR - 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int t = 0; t < JT; ++t)
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            acc[g][q][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[q][h], bp[c][h][p * JT + t], acc[g][q][t], 0, 0, 0);
+  }
+  // the 8 wave partials [j][rows] through LDS (the ring is free once every wave is past its last
+  // slot), then thread (row m, j quad q) sums them in wave order and writes u[m][4q..] and the
+  // [hi | hi | lo | 0..] split row (as lora_dy_finish_kernel)
+  __syncthreads();
+  float* part = (float*)smem;
+#pragma unroll
+  for (int g = 0; g < RG; ++g)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int t = 0; t < JT; ++t)
+        *(f32x4*)(part + (wave * RP + 16 * t + (lane & 15)) * PROW + 32 * g + 16 * q + 4 * (lane >> 4)) = acc[g][q][t];
+  __syncthreads();
+  constexpr int NQ = R / 4;
+  for (int e = tid; e < RG * 32 * NQ; e += 512) {
+    const int q = e / (RG * 32), rr = e % (RG * 32), m = mb + rr;
+    if (m >= M) continue;
+    f32x4 wv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v = part[(4 * q + k) * PROW + rr];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) v += part[(w * RP + 4 * q + k) * PROW + rr];
+      wv[k] = v * alpha;
+    }
+    *(f32x4*)(out + (int64_t)m * ldo + 4 * q) = wv;
+    if (split == nullptr) continue;
+    uint32_t hi[2], lo[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const bf16_t h0 = f2bf(wv[2 * k]), h1 = f2bf(wv[2 * k + 1]);
+      hi[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      lo[k] = (uint32_t)f2bf(wv[2 * k] - bf2f(h0)) | ((uint32_t)f2bf(wv[2 * k + 1] - bf2f(h1)) << 16);
+    }
+    bf16_t* sr = split + (int64_t)m * lds;
+    *(u32x2*)(sr + 4 * q) = (u32x2){hi[0], hi[1]};
+    *(u32x2*)(sr + R + 4 * q) = (u32x2){hi[0], hi[1]};
+    *(u32x2*)(sr + 2 * R + 4 * q) = (u32x2){lo[0], lo[1]};
+    for (int cc = 3 * R + 4 * q; cc < K2; cc += R) *(u32x2*)(sr + cc) = (u32x2){0u, 0u};
+  }
+}
+
 // ltx_lora_wgrad's token-sized path (called from lora.hip): dw (+)= alpha . Y^T . u through the
 // dB product of lora_dy_kernel (bf16 matrix core, u split into exact hi / mid / lo pieces) and the
 // dB half of the finish kernel. lora_wgrad_kernel spends ~9 us of f32 MFMA issue on the same
@@ -370,6 +531,27 @@ bool lora_rows_dy(const bf16_t* x, int64_t ldx, const bf16_t* w3, int64_t ldw, f
   if (ldw % 8 != 0 || ((uintptr_t)w3 % 16) != 0 || ldw < K) return false;
   if (ldo % 4 != 0 || ((uintptr_t)out % 16) != 0) return false;
   if (split && (ld_split % 4 != 0 || ((uintptr_t)split % 8) != 0 || K2 < 3 * r || (K2 - 3 * r) % 4 != 0)) return false;
+  // K = 512 / 1024 / 2048: the whole contraction per block (lora_rows_full_kernel, no finish);
+  // LTX_LORA_ROWS_FULL=0 at load keeps the column-split pass + finish
+  static const int full = [] {
+    const char* e = getenv("LTX_LORA_ROWS_FULL");
+    return e ? atoi(e) : 1;
+  }();
+  if (full && (K == 512 || K == 1024 || K == 2048)) {
+    constexpr int RG = 2, NRF = LTX_RF_NR;
+    const dim3 gf((unsigned)((M + RG * 32 - 1) / (RG * 32)));
+#define LTX_LORA_RF(RR, CHH)                                                                                  \
+  hipLaunchKernelGGL((lora_rows_full_kernel<RR, RG, CHH, NRF>), gf, dim3(512), 0, s, x, ldx, w3, ldw, out, ldo, (int)M, \
+                     alpha, split, ld_split, (int)K2)
+    const int ch = (int)(K / 512);
+    if (r == 8) {
+      if (ch == 1) LTX_LORA_RF(8, 1); else if (ch == 2) LTX_LORA_RF(8, 2); else LTX_LORA_RF(8, 4);
+    } else {
+      if (ch == 1) LTX_LORA_RF(16, 1); else if (ch == 2) LTX_LORA_RF(16, 2); else LTX_LORA_RF(16, 4);
+    }
+#undef LTX_LORA_RF
+    return true;
+  }
   const int64_t RP = r >= 16 ? r : 16;
   const int CS = (int)(K / DY_COLS), RS = (int)((M + DY_G * 32 - 1) / (DY_G * 32));
   size_t ws = 0;
