@@ -331,6 +331,19 @@ int ltx_lora_dy(const void* y, int64_t ldy, const float* u, int64_t ldu, const v
                 float* workspace, void* stream);
 /* f32 workspace size (in floats) of ltx_lora_dy for an [M, N] dY at rank r */
 int ltx_lora_dy_workspace(int64_t M, int64_t N, int64_t r, int64_t* floats);
+/* ltx_lora_dy plus the same adapter's lora_A gradient (the rest of peft lora.Linear's backward,
+ * training.py:50-68: dA = alpha_a * x^T . w with w the f32 term above, as ltx_lora_wgrad(x, w,
+ * alpha_a) computes it): dwa[k*ona + j*oja] (+)= alpha_a * sum_m X[m,k] * w[m,j] (acc_a != 0 adds),
+ * X bf16 [M,K] (ldx), K % 512 == 0, N <= 2048. Three launches instead of ltx_lora_dy's two plus
+ * ltx_lora_wgrad's two; every output bitwise those calls' (dA where ltx_lora_wgrad takes its
+ * token-sized path, M >= 2048; below, the same products in another f32 order).
+ * workspace: ltx_lora_dy_dA_workspace. */
+int ltx_lora_dy_dA(const void* y, int64_t ldy, const float* u, int64_t ldu, const void* w3, int64_t ldw3,
+                   const void* x, int64_t ldx, int64_t M, int64_t N, int64_t K, int64_t r, float alpha,
+                   float* w, int64_t ldw_out, void* split, int64_t ld_split, int64_t K2, float* dw,
+                   int64_t on, int64_t oj, int accumulate, float alpha_a, float* dwa, int64_t ona,
+                   int64_t oja, int acc_a, float* workspace, void* stream);
+int ltx_lora_dy_dA_workspace(int64_t M, int64_t N, int64_t K, int64_t r, int64_t* floats);
 
 /* ---- small ops -------------------------------------------------------------------------------- */
 /* AdaLayerNormSingle sinusoid: out[b,:] = bf16([cos(s*t*f), sin(s*t*f)]) (256 ch), s = scale */

@@ -725,6 +725,24 @@ def test_lora_dy_one_pass(M, N, r):
     buf2 = torch.zeros(N, r, device=DEV)
     ops.lora_dy(dy, u, pieces, r, 0.5, buf2, accumulate=False)
     assert rel(buf2, ops.lora_wgrad(dy, u, alpha=0.5)) < 1e-6
+    # with the adapter's dA = x^T . w in the same call (ltx_lora_dy_dA: the x pass reads w from the
+    # dY pass's partials, one finish for all): w, split and dB bitwise the call above; dA bitwise
+    # ltx_lora_wgrad(x, w) where that takes its token-sized path (M >= 2048), else to f32 order
+    K = 1024 if N != 1024 else 512
+    x = g(M, K, seed=9)
+    bB1, bA1 = torch.randn(N, r, device=DEV), torch.randn(r, K, device=DEV)
+    bB2, bA2 = bB1.clone(), bA1.clone()
+    w1, sp1 = ops.lora_dy(dy, u, pieces, r, 0.5, bB1)
+    ops.lora_wgrad(x, w1, transpose_out=True, out=bA1, accumulate=True)
+    w2, sp2 = ops.lora_dy(dy, u, pieces, r, 0.5, bB2, x=x, dA_out=bA2)
+    assert torch.equal(w1, w2) and torch.equal(sp1, sp2) and torch.equal(bB1, bB2)
+    if M >= 2048:
+        assert torch.equal(bA1, bA2)
+    else:
+        assert rel(bA2, bA1) < 1e-6
+    bA3 = torch.zeros(r, K, device=DEV)
+    ops.lora_dy(dy, u, pieces, r, 0.5, torch.zeros(N, r, device=DEV), x=x, dA_out=bA3, dA_accumulate=False)
+    assert rel(bA3, w1.t() @ x.float()) < 1e-5
 
 
 @pytest.mark.parametrize("M,K,r", [(14336, 2048, 16), (4480, 1024, 8), (2048, 512, 16)])

@@ -35,17 +35,22 @@ constexpr int DY_G = 7;      // row groups of 32 per block (14336 = 64 x 7 x 32)
 constexpr int DY_NR = 4;     // ring slots per wave
 constexpr int DY_COLS = 512; // columns per block
 constexpr int DY_UPAD = DY_G * 32 + 4;  // u^T row length in LDS (floats; +4 spreads the banks)
+constexpr int DY_MAXCS = 4;  // column splits a MODE-6 pass sums its u from (N <= 2048)
 }  // namespace
 
 // MODE: bit 0 the w product, bit 1 the dB product. MODE 2 is ltx_lora_wgrad's token-sized path
 // (dw = alpha . Y^T . u on the bf16 matrix core with u's exact three-piece split, where
 // lora_wgrad_kernel runs f32 MFMAs); MODE 1 is ltx_lora_rows' (u = x . A^T from A's pieces).
+// Bit 2 (with bit 1, round 6): u is not read but summed from another pass's column-split w partials
+// part_u[c][j][m] (c < CSu, in c order) times alpha_u -- bitwise the w lora_dy_finish_kernel writes
+// from them -- so the dA pass of an adapter (dA = w^T . x) need not wait for that finish launch.
 template <int R, int MODE>
 __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__ y, int64_t ldy,
                                                       const float* __restrict__ u, int64_t ldu,
                                                       const bf16_t* __restrict__ w3, int64_t ldw,
                                                       float* __restrict__ part_w, float* __restrict__ part_b,
-                                                      int M, int N) {
+                                                      int M, int N, const float* __restrict__ part_u, int CSu,
+                                                      float alpha_u) {
   constexpr int RP = R >= 16 ? R : 16;
   constexpr int JT = RP / 16;
   constexpr int NF = 3 * JT;
@@ -112,15 +117,43 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
   // rolled loop waited out one load round trip per element, ~2 us per block)
   constexpr int UPT = (DY_G * 32 * RP + 511) / 512;
   float uv[UPT];
+  if constexpr ((MODE & 4) != 0) {  // u from the w partials: e -> (j, row), rows fastest (coalesced)
+    // every partial load in flight before the first add (CSu <= DY_MAXCS; loads past CSu or past the
+    // block's rows read partial 0 / row 0 and are not added); then the sum in c order from 0
+    float pv[UPT][DY_MAXCS];
 #pragma unroll
-  for (int i = 0; i < UPT; ++i) {
-    const int e = tid + 512 * i, rr = e / RP, j = e % RP, m = mb + rr;
-    uv[i] = ((MODE & 2) && e < DY_G * 32 * RP && m < M && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
-  }
+    for (int i = 0; i < UPT; ++i) {
+      const int e = tid + 512 * i, j = e / (DY_G * 32), rr = e % (DY_G * 32), m = mb + rr;
+      const bool ok = e < DY_G * 32 * RP && m < M && j < R;
 #pragma unroll
-  for (int i = 0; i < UPT; ++i) {
-    const int e = tid + 512 * i;
-    if ((MODE & 2) && e < DY_G * 32 * RP) ut[(e % RP) * DY_UPAD + e / RP] = uv[i];
+      for (int c = 0; c < DY_MAXCS; ++c)
+        pv[i][c] = part_u[((int64_t)(c < CSu ? c : 0) * RP + (ok ? j : 0)) * M + (ok ? m : 0)];
+    }
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int e = tid + 512 * i, j = e / (DY_G * 32), rr = e % (DY_G * 32), m = mb + rr;
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < DY_MAXCS; ++c)
+        if (c < CSu) acc += pv[i][c];
+      uv[i] = (e < DY_G * 32 * RP && m < M && j < R) ? acc * alpha_u : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int e = tid + 512 * i;
+      if (e < DY_G * 32 * RP) ut[(e / (DY_G * 32)) * DY_UPAD + e % (DY_G * 32)] = uv[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int e = tid + 512 * i, rr = e / RP, j = e % RP, m = mb + rr;
+      uv[i] = ((MODE & 2) && e < DY_G * 32 * RP && m < M && j < R) ? u[(int64_t)m * ldu + j] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int e = tid + 512 * i;
+      if ((MODE & 2) && e < DY_G * 32 * RP) ut[(e % RP) * DY_UPAD + e / RP] = uv[i];
+    }
   }
   __syncthreads();  // u^T staged; every ordinary load retired before the counted waits below
 
@@ -255,13 +288,39 @@ __global__ __launch_bounds__(512) void lora_dy_kernel(const bf16_t* __restrict__
 // one thread per split element. Blocks [nwb, ..): dw[n*on + j*oj] (+)= alpha * sum_s part_b[s][n][j]
 // for 64 (n, j) pairs per block, the row splits dealt to 4 thread groups (strided, independent
 // loads in flight) and the 4 group sums added in a fixed order (deterministic).
+// Blocks [nwb + nbb, ..) (round 6): a second row-split sum of the same kind, dwa (+)= alpha_a *
+// sum_s part_a[s][n][j] over Na columns (the adapter's dA from the pass that ran after its dY pass).
+template <int R>
+__device__ __forceinline__ void finish_rows(const float* __restrict__ part, int RS, int N, float alpha,
+                                            float* __restrict__ dw, int64_t on, int64_t oj, int accumulate, int blk,
+                                            float (*red)[64]) {
+  constexpr int RP = R >= 16 ? R : 16;
+  const int pr = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blk * 64 + pr;  // pair (n, j), j fastest
+  const bool ok = e < (int64_t)N * R;
+  const int n = ok ? (int)(e / R) : 0, j = ok ? (int)(e % R) : 0;
+  float sum = 0.f;
+#pragma unroll 8
+  for (int s = grp; s < RS; s += 4) sum += part[((int64_t)s * N + n) * RP + j];
+  red[grp][pr] = sum;
+  __syncthreads();
+  if (grp == 0 && ok) {
+    const float v = (((red[0][pr] + red[1][pr]) + red[2][pr]) + red[3][pr]) * alpha;
+    float* o = dw + (int64_t)n * on + (int64_t)j * oj;
+    *o = accumulate ? *o + v : v;
+  }
+}
+
 template <int R>
 __global__ __launch_bounds__(256) void lora_dy_finish_kernel(const float* __restrict__ part_w, int CS,
                                                              const float* __restrict__ part_b, int RS, int M, int N,
                                                              float alpha, float* __restrict__ w, int64_t ldw_out,
                                                              bf16_t* __restrict__ split, int64_t lds, int K2,
                                                              float* __restrict__ dw, int64_t on, int64_t oj,
-                                                             int accumulate, int nwb) {
+                                                             int accumulate, int nwb, int nbb,
+                                                             const float* __restrict__ part_a, int Na, float alpha_a,
+                                                             float* __restrict__ dwa, int64_t ona, int64_t oja,
+                                                             int acc_a) {
   constexpr int RP = R >= 16 ? R : 16;
   if ((int)blockIdx.x < nwb) {
     // thread (j quad q, row m), m fastest (the partial reads coalesce): w[m][4q..4q+3],
@@ -307,20 +366,9 @@ __global__ __launch_bounds__(256) void lora_dy_finish_kernel(const float* __rest
     return;
   }
   __shared__ float red[4][64];
-  const int pr = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int64_t e = (int64_t)(blockIdx.x - nwb) * 64 + pr;  // pair (n, j), j fastest
-  const bool ok = e < (int64_t)N * R;
-  const int n = ok ? (int)(e / R) : 0, j = ok ? (int)(e % R) : 0;
-  float sum = 0.f;
-#pragma unroll 8
-  for (int s = grp; s < RS; s += 4) sum += part_b[((int64_t)s * N + n) * RP + j];
-  red[grp][pr] = sum;
-  __syncthreads();
-  if (grp == 0 && ok) {
-    const float v = (((red[0][pr] + red[1][pr]) + red[2][pr]) + red[3][pr]) * alpha;
-    float* o = dw + (int64_t)n * on + (int64_t)j * oj;
-    *o = accumulate ? *o + v : v;
-  }
+  const int blk = (int)blockIdx.x - nwb;
+  if (blk < nbb) finish_rows<R>(part_b, RS, N, alpha, dw, on, oj, accumulate, blk, red);
+  else finish_rows<R>(part_a, RS, Na, alpha_a, dwa, ona, oja, acc_a, blk - nbb, red);
 }
 
 // u = alpha * x . A^T for token-sized M with the whole contraction inside one block (round 6):
@@ -503,9 +551,10 @@ bool lora_wgrad_rows(const bf16_t* y, int64_t ldy, const float* u, int64_t ldu, 
   const dim3 g2((unsigned)((N * r + 63) / 64));
 #define LTX_LORA_WG(RR)                                                                                       \
   hipLaunchKernelGGL((lora_dy_kernel<RR, 2>), grid, dim3(512), 0, s, y, ldy, u, ldu, nullptr, (int64_t)0, \
-                     nullptr, pb, (int)M, (int)N);                                                            \
+                     nullptr, pb, (int)M, (int)N, (const float*)nullptr, 0, 1.f);                           \
   hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, nullptr, 0, pb, RS, (int)M, (int)N,    \
-                     alpha, nullptr, (int64_t)0, nullptr, (int64_t)0, 0, dw, on, oj, accumulate, 0);
+                     alpha, nullptr, (int64_t)0, nullptr, (int64_t)0, 0, dw, on, oj, accumulate, 0, 1 << 30,   \
+                     (const float*)nullptr, 0, 1.f, (float*)nullptr, (int64_t)0, (int64_t)0, 0);
   if (r == 8) {
     LTX_LORA_WG(8)
   } else {
@@ -562,9 +611,10 @@ bool lora_rows_dy(const bf16_t* x, int64_t ldx, const bf16_t* w3, int64_t ldw, f
   const int nwb = (int)g2.x;
 #define LTX_LORA_RW(RR)                                                                                      \
   hipLaunchKernelGGL((lora_dy_kernel<RR, 1>), grid, dim3(512), 0, s, x, ldx, nullptr, (int64_t)0, w3, ldw, pw, \
-                     nullptr, (int)M, (int)K);                                                              \
+                     nullptr, (int)M, (int)K, (const float*)nullptr, 0, 1.f);                             \
   hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, pw, CS, nullptr, 0, (int)M, (int)K,    \
-                     alpha, out, ldo, split, ld_split, (int)K2, nullptr, (int64_t)0, (int64_t)0, 0, nwb);
+                     alpha, out, ldo, split, ld_split, (int)K2, nullptr, (int64_t)0, (int64_t)0, 0, nwb, 1 << 30, \
+                     (const float*)nullptr, 0, 1.f, (float*)nullptr, (int64_t)0, (int64_t)0, 0);
   if (r == 8) {
     LTX_LORA_RW(8)
   } else {
@@ -606,16 +656,78 @@ extern "C" int ltx_lora_dy(const void* y, int64_t ldy, const float* u, int64_t l
   const dim3 g2((unsigned)(nwb + (N * r + 63) / 64));
 #define LTX_LORA_DY(RR)                                                                                          \
   hipLaunchKernelGGL((lora_dy_kernel<RR, 3>), grid, dim3(512), 0, s, (const bf16_t*)y, ldy, u, ldu,                \
-                     (const bf16_t*)w3, ldw3, pw, pb, (int)M, (int)N);                                           \
+                     (const bf16_t*)w3, ldw3, pw, pb, (int)M, (int)N, (const float*)nullptr, 0, 1.f);          \
   LTX_LAUNCH_CHECK();                                                                                            \
   hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), g2, dim3(256), 0, s, pw, CS, pb, RS, (int)M, (int)N, alpha, w, \
-                     ldw_out, (bf16_t*)split, ld_split, (int)K2, dw, on, oj, accumulate, nwb);
+                     ldw_out, (bf16_t*)split, ld_split, (int)K2, dw, on, oj, accumulate, nwb, 1 << 30,           \
+                     (const float*)nullptr, 0, 1.f, (float*)nullptr, (int64_t)0, (int64_t)0, 0);
   switch (r) {
     case 8: LTX_LORA_DY(8) break;
     case 16: LTX_LORA_DY(16) break;
     default: return fail(LTX_ERR_BAD_ARG, "lora_dy: rank must be 8 or 16");
   }
 #undef LTX_LORA_DY
+  LTX_LAUNCH_CHECK();
+  return LTX_OK;
+}
+
+extern "C" int ltx_lora_dy_dA_workspace(int64_t M, int64_t N, int64_t K, int64_t r, int64_t* floats) {
+  LTX_CHECK_ARG(floats && M > 0 && N > 0 && K > 0 && (r == 8 || r == 16), "lora_dy_dA_workspace: bad args");
+  const int64_t RP = r >= 16 ? r : 16;
+  const int64_t CS = N / DY_COLS, RS = (M + DY_G * 32 - 1) / (DY_G * 32);
+  *floats = CS * M * RP + RS * N * RP + RS * K * RP;
+  return LTX_OK;
+}
+
+// ltx_lora_dy + the adapter's dA = alpha_a . x^T . w ([K, r] or [r, K]) in three launches instead of
+// four: the dY pass (w and dB partials), the x pass reading w from those partials (lora_dy_kernel
+// MODE 6), and one finish for w / split, dB and dA. Every output is bitwise what ltx_lora_dy followed
+// by ltx_lora_wgrad(x, w, alpha_a) produces (dA: where that takes lora_wgrad_rows, M >= 2048).
+extern "C" int ltx_lora_dy_dA(const void* y, int64_t ldy, const float* u, int64_t ldu, const void* w3, int64_t ldw3,
+                              const void* x, int64_t ldx, int64_t M, int64_t N, int64_t K, int64_t r, float alpha,
+                              float* w, int64_t ldw_out, void* split, int64_t ld_split, int64_t K2, float* dw,
+                              int64_t on, int64_t oj, int accumulate, float alpha_a, float* dwa, int64_t ona,
+                              int64_t oja, int acc_a, float* workspace, void* stream) {
+  LTX_CHECK_ARG(y && u && w3 && x && w && split && dw && dwa && workspace, "lora_dy_dA: null operand");
+  LTX_CHECK_ARG(M >= 32 && M % 32 == 0 && N % DY_COLS == 0 && K % DY_COLS == 0 && (r == 8 || r == 16),
+                "lora_dy_dA: M % 32 == 0, N % 512 == 0, K % 512 == 0, rank 8 or 16");
+  LTX_CHECK_ARG(N <= DY_MAXCS * DY_COLS, "lora_dy_dA: N <= 2048 (the dA pass sums w from <= 4 column splits)");
+  LTX_CHECK_ARG(ldy % 8 == 0 && ((uintptr_t)y % 16) == 0 && ldw3 % 8 == 0 && ((uintptr_t)w3 % 16) == 0 && ldw3 >= N,
+                "lora_dy_dA: 16-B aligned rows of dY and of the pieces");
+  LTX_CHECK_ARG(ldx % 8 == 0 && ((uintptr_t)x % 16) == 0 && ldx >= K, "lora_dy_dA: 16-B aligned rows of x");
+  LTX_CHECK_ARG(ldy * 2 * 32 < ((int64_t)1 << 32) && ldx * 2 * 32 < ((int64_t)1 << 32),
+                "lora_dy_dA: 32-bit DMA offsets");
+  LTX_CHECK_ARG(ldw_out >= r && ldu >= r && K2 >= 3 * r && K2 % 64 == 0 && ld_split >= K2,
+                "lora_dy_dA: output strides");
+  LTX_CHECK_ARG(ldw_out % 4 == 0 && ((uintptr_t)w % 16) == 0 && ld_split % 4 == 0 && ((uintptr_t)split % 8) == 0,
+                "lora_dy_dA: 16-B aligned w rows, 8-B aligned split rows");
+  LTX_CHECK_ARG((on == r && oj == 1) || (on == 1 && oj == N), "lora_dy_dA: dB must be a dense [N,r] or [r,N]");
+  LTX_CHECK_ARG((ona == r && oja == 1) || (ona == 1 && oja == K), "lora_dy_dA: dA must be a dense [K,r] or [r,K]");
+  const int64_t RP = r >= 16 ? r : 16;
+  const int CS = (int)(N / DY_COLS), CSx = (int)(K / DY_COLS), RS = (int)((M + DY_G * 32 - 1) / (DY_G * 32));
+  float* pw = workspace;
+  float* pb = pw + (int64_t)CS * M * RP;
+  float* pa = pb + (int64_t)RS * N * RP;
+  hipStream_t s = (hipStream_t)stream;
+  const int nwb = (int)((M * (r / 4) + 255) / 256);
+  const int nbb = (int)((N * r + 63) / 64), nba = (int)((K * r + 63) / 64);
+#define LTX_LORA_DYA(RR)                                                                                           \
+  hipLaunchKernelGGL((lora_dy_kernel<RR, 3>), dim3((unsigned)CS, (unsigned)RS), dim3(512), 0, s, (const bf16_t*)y, \
+                     ldy, u, ldu, (const bf16_t*)w3, ldw3, pw, pb, (int)M, (int)N, (const float*)nullptr, 0, 1.f);  \
+  LTX_LAUNCH_CHECK();                                                                                              \
+  hipLaunchKernelGGL((lora_dy_kernel<RR, 6>), dim3((unsigned)CSx, (unsigned)RS), dim3(512), 0, s,                 \
+                     (const bf16_t*)x, ldx, (const float*)nullptr, (int64_t)0, (const bf16_t*)nullptr, (int64_t)0, \
+                     (float*)nullptr, pa, (int)M, (int)K, (const float*)pw, CS, alpha);                             \
+  LTX_LAUNCH_CHECK();                                                                                              \
+  hipLaunchKernelGGL((lora_dy_finish_kernel<RR>), dim3((unsigned)(nwb + nbb + nba)), dim3(256), 0, s, pw, CS, pb,  \
+                     RS, (int)M, (int)N, alpha, w, ldw_out, (bf16_t*)split, ld_split, (int)K2, dw, on, oj,         \
+                     accumulate, nwb, nbb, (const float*)pa, (int)K, alpha_a, dwa, ona, oja, acc_a);
+  switch (r) {
+    case 8: LTX_LORA_DYA(8) break;
+    case 16: LTX_LORA_DYA(16) break;
+    default: return fail(LTX_ERR_BAD_ARG, "lora_dy_dA: rank must be 8 or 16");
+  }
+#undef LTX_LORA_DYA
   LTX_LAUNCH_CHECK();
   return LTX_OK;
 }

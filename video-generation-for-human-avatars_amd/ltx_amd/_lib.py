@@ -77,6 +77,9 @@ _SIGNATURES = {
     "ltx_lora_dy": [_p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _f32, _p, _i64, _p, _i64, _i64, _p,
                     _i64, _i64, _i32, _p, _p],
     "ltx_lora_dy_workspace": [_i64, _i64, _i64, ctypes.POINTER(_i64)],
+    "ltx_lora_dy_dA": [_p, _i64, _p, _i64, _p, _i64, _p, _i64, _i64, _i64, _i64, _i64, _f32, _p, _i64,
+                       _p, _i64, _i64, _p, _i64, _i64, _i32, _f32, _p, _i64, _i64, _i32, _p, _p],
+    "ltx_lora_dy_dA_workspace": [_i64, _i64, _i64, _i64, ctypes.POINTER(_i64)],
     "ltx_lora_split_bf16": [_p, _i64, _i64, _f32, _i64, _i64, _i32, _p, _i64, _i64, _p],
     "ltx_lora_down": [_p, _i64, _p, _i64, _i64, _p, _i64, _i64, _i64, _i64, _f32, _p, _i64, _i64,
                       _p],

@@ -753,15 +753,29 @@ def lora_dy_enabled():
     return os.environ.get("LTX_LORA_DY", "1") != "0"
 
 
+def lora_dy_da_enabled():
+    """LTX_LORA_DY_DA=0 (read per call): the adapter's dA stays a separate ltx_lora_wgrad call."""
+    return os.environ.get("LTX_LORA_DY_DA", "1") != "0"
+
+
+def lora_dy_da_fits(y, x, r):
+    """lora_dy(y, ..., x=x) applies (and LTX_LORA_DY_DA is not 0)."""
+    return lora_dy_da_enabled() and lora_dy_fits(x, r) and y.shape[1] <= 2048 and x.shape[0] == y.shape[0]
+
+
 def lora_dy_fits(y, r):
     M, N = y.shape
     return r in (8, 16) and M % 32 == 0 and N % 512 == 0 and y.stride(1) == 1 and y.stride(0) % 8 == 0
 
 
-def lora_dy(y, u, w3, r, alpha, dB_out, accumulate=True, transpose_out=False):
+def lora_dy(y, u, w3, r, alpha, dB_out, accumulate=True, transpose_out=False, x=None, dA_out=None,
+            dA_accumulate=True):
     """One pass over dY (ltx_lora_dy): returns (w, split) as lora_down(y, B, transposed=True,
     split=True) does, and adds alpha * y^T . u into dB_out ([N, r], or [r, N] with transpose_out)
-    as lora_wgrad(y, u, alpha, out=dB_out, accumulate=accumulate) does."""
+    as lora_wgrad(y, u, alpha, out=dB_out, accumulate=accumulate) does. With x ([M, K] bf16,
+    lora_dy_fits; N <= 2048) and dA_out ([r, K] f32): also dA_out (+)= x^T . w as lora_wgrad(x, w,
+    transpose_out=True, out=dA_out, accumulate=dA_accumulate) does, bitwise, with one launch fewer
+    than the two calls (ltx_lora_dy_dA)."""
     M, N = y.shape
     shape = (r, N) if transpose_out else (N, r)
     assert tuple(dB_out.shape) == shape and dB_out.dtype == F32 and dB_out.is_contiguous()
@@ -770,6 +784,17 @@ def lora_dy(y, u, w3, r, alpha, dB_out, accumulate=True, transpose_out=False):
     w = torch.empty(M, r, dtype=F32, device=y.device)
     sp = torch.empty(M, K2, dtype=BF16, device=y.device)
     n = ctypes.c_int64(0)
+    if x is not None:
+        K = x.shape[1]
+        assert x.shape[0] == M and x.dtype == BF16 and lora_dy_fits(x, r) and N <= 2048
+        assert tuple(dA_out.shape) == (r, K) and dA_out.dtype == F32 and dA_out.is_contiguous()
+        call("ltx_lora_dy_dA_workspace", M, N, K, r, ctypes.byref(n))
+        ws = torch.empty(n.value, dtype=F32, device=y.device)
+        call("ltx_lora_dy_dA", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(w3), _rows(w3, "w3"),
+             _p(x), _rows(x, "x"), M, N, K, r, float(alpha), _p(w), _rows(w, "w"), _p(sp),
+             _rows(sp, "split"), K2, _p(dB_out), on, oj, 1 if accumulate else 0, 1.0, _p(dA_out), 1,
+             K, 1 if dA_accumulate else 0, _p(ws), _s())
+        return w, sp
     call("ltx_lora_dy_workspace", M, N, r, ctypes.byref(n))
     ws = torch.empty(n.value, dtype=F32, device=y.device)
     call("ltx_lora_dy", _p(y), _rows(y, "y"), _p(u), _rows(u, "u"), _p(w3), _rows(w3, "w3"), M, N, r,

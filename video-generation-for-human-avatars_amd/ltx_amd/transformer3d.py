@@ -582,13 +582,19 @@ class _BlockFn(torch.autograd.Function):
             if _DELTA_FUSED else {}
         if has_lora:
             lq, lk, lv, lo = lora
-            if ops.lora_dy_enabled() and ops.lora_dy_fits(dh2, r):  # one pass over dY
-                w_o, sw = ops.lora_dy(dh2, u_o, lo.weight_pieces("Bt"), r, s, _grad_buf(lo, "B"))
+            dy_ok = ops.lora_dy_enabled() and ops.lora_dy_fits(dh2, r)
+            if dy_ok and ops.lora_dy_da_fits(dh2, o2, r):
+                # one pass over dY, one over o2 (dA), one finish for w / split, dB and dA
+                w_o, sw = ops.lora_dy(dh2, u_o, lo.weight_pieces("Bt"), r, s, _grad_buf(lo, "B"),
+                                      x=o2, dA_out=_grad_buf(lo, "A"))
             else:
-                ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
-                w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True,
-                                         pieces=lambda: lo.weight_pieces("Bt"))
-            ops.lora_wgrad(o2, w_o, transpose_out=True, out=_grad_buf(lo, "A"), accumulate=True)
+                if dy_ok:  # one pass over dY
+                    w_o, sw = ops.lora_dy(dh2, u_o, lo.weight_pieces("Bt"), r, s, _grad_buf(lo, "B"))
+                else:
+                    ops.lora_wgrad(dh2, u_o, alpha=s, out=_grad_buf(lo, "B"), accumulate=True)
+                    w_o, sw = ops.lora_down(dh2, Bo, alpha=s, transposed=True, split=True,
+                                             pieces=lambda: lo.weight_pieces("Bt"))
+                ops.lora_wgrad(o2, w_o, transpose_out=True, out=_grad_buf(lo, "A"), accumulate=True)
             do2 = ops.gemm(dh2, W["o2_wT"], ext=(sw, lo.weight_split("A")), **rd)
         else:
             do2 = ops.gemm(dh2, W["o2_wT"], **rd)
@@ -661,13 +667,18 @@ class _BlockFn(torch.autograd.Function):
         d_y1 = torch.empty_like(dh2)
         gated = dict(aux1=mods[:, 2], aux2=d_y1, rows_per_batch=rpm)
         if has_lora:
-            if ops.lora_dy_enabled() and ops.lora_dy_fits(dq2raw, r):
-                w_q, sw = ops.lora_dy(dq2raw, u_q, lq.weight_pieces("Bt"), r, s, _grad_buf(lq, "B"))
+            dy_ok = ops.lora_dy_enabled() and ops.lora_dy_fits(dq2raw, r)
+            if dy_ok and ops.lora_dy_da_fits(dq2raw, h1, r):
+                w_q, sw = ops.lora_dy(dq2raw, u_q, lq.weight_pieces("Bt"), r, s, _grad_buf(lq, "B"),
+                                      x=h1, dA_out=_grad_buf(lq, "A"))
             else:
-                ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
-                w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True,
-                                         pieces=lambda: lq.weight_pieces("Bt"))
-            ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
+                if dy_ok:
+                    w_q, sw = ops.lora_dy(dq2raw, u_q, lq.weight_pieces("Bt"), r, s, _grad_buf(lq, "B"))
+                else:
+                    ops.lora_wgrad(dq2raw, u_q, alpha=s, out=_grad_buf(lq, "B"), accumulate=True)
+                    w_q, sw = ops.lora_down(dq2raw, Bq, alpha=s, transposed=True, split=True,
+                                             pieces=lambda: lq.weight_pieces("Bt"))
+                ops.lora_wgrad(h1, w_q, transpose_out=True, out=_grad_buf(lq, "A"), accumulate=True)
             dh1 = ops.gemm(dq2raw, W["q2_wT"], epilogue="accum", aux0=dh2,
                            ext=(sw, lq.weight_split("A")), **gated)
             if tx is None:
