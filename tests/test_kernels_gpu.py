@@ -373,6 +373,10 @@ def test_attention_fwd_one_pass(B, H, Nq, Nk, masked, shared, valid, monkeypatch
     bias = _cross_bias(Nk, Bk, valid) if masked else None
     monkeypatch.setenv("LTX_ATTN_FWD1", "1")
     o1, l1 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)
+    monkeypatch.setenv("LTX_ATTN_FWD1_ROWS", "0")  # O in 32-B pieces instead of LDS-staged rows
+    o2, l2 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)
+    monkeypatch.delenv("LTX_ATTN_FWD1_ROWS")
+    assert torch.equal(o1, o2) and torch.equal(l1, l2)
     monkeypatch.setenv("LTX_ATTN_FWD1", "0")
     monkeypatch.setenv("LTX_ATTN_FWD_PIPE", "0")  # the tiled kernel whose arithmetic fwd1 mirrors
     o0, l0 = ops.attn_fwd(q, k, v, B, H, d, d ** -0.5, key_bias=bias, kv_shared=shared)

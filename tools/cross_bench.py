@@ -25,18 +25,25 @@ D = H * d
 dev = "cuda"
 _lib.ensure_device(dev)
 g = torch.Generator(device="cpu").manual_seed(0)
-q = torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16)
+ap2 = os.environ.get("LTX_CROSS_ROTATE", "0") == "1"  # rotate 4 operand sets (no cache reuse)
+qs = [torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16) for _ in range(4 if ap2 else 1)]
+q = qs[0]
 kv = torch.randn(L, 2 * D, generator=g).to(dev, torch.bfloat16)
 k, v = kv[:, :D], kv[:, D:]
 bias = torch.zeros(1, L)
 bias[:, args.valid:] = -10000.0
 bias = bias.to(dev)
-do = torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16)
+dos = [torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16) for _ in range(4 if ap2 else 1)]
+do = dos[0]
 scale = d ** -0.5
 
 
+rot = iter(range(1 << 30))
+
+
 def run_fwd():
-    return ops.attn_fwd(q, k, v, B, H, d, scale, key_bias=bias, kv_shared=True)
+    qq = qs[next(rot) % len(qs)]
+    return ops.attn_fwd(qq, k, v, B, H, d, scale, key_bias=bias, kv_shared=True)
 
 
 o, lse = run_fwd()
@@ -44,7 +51,8 @@ delta = (do.float() * o.float()).view(B, N, H, d).sum(-1).transpose(1, 2).contig
 
 
 def run_bwd():
-    return ops.attn_bwd(q, k, v, o, do, lse, B, H, d, scale, key_bias=bias, kv_shared=True, delta=delta)
+    i = next(rot) % len(qs)
+    return ops.attn_bwd(qs[i], k, v, o, dos[i], lse, B, H, d, scale, key_bias=bias, kv_shared=True, delta=delta)
 
 
 def timeit(fn, iters):

@@ -493,13 +493,19 @@ constexpr float KEY_MASKED = -10000.0f;
 // 128-query workgroup in 64-key tiles behind two barriers each, which at Nk = 256 is mostly
 // exposed load latency. Arithmetic per slice is attn_q_kernel's MODE 0 loop, bit for bit.
 // =============================================================================================
-template <int HD, bool BIAS>
+// ROWS (round 6): O leaves as whole 128-B rows through a 1-KiB LDS slot per wave, 8 rows per pass
+// and store instruction (store_rows_lds1k; the slot fits beside the K / V images at two workgroups
+// per CU), instead of the 32-B pieces of 32 rows per instruction store_row_swap writes. With
+// HBM-resident operands (tools/cross_bench.py, profiles/r06p_cross_stores.txt) the forward ran 41 us,
+// 24.6 us with no O stores at all, and 34 us with ROWS; a 16-wave workgroup with a 4-KiB slot per
+// wave (one pass) spilled 17 registers and ran 39 us. Bitwise the same O and lse.
+template <int HD, bool BIAS, bool ROWS>
 __global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BIAS ? 4 : 2, 4))) void attn_fwd1_kernel(const AttnParams p) {
   constexpr int KT = 64;
   constexpr int KS = HD / 16;
   constexpr int DS = HD / 32;
   constexpr int IMG = BWD1_KEYS * HD * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG + (ROWS ? 1024 * (BWD1_THREADS / 64) : 0)];
   __shared__ __attribute__((aligned(16))) float kb[BWD1_KEYS];
   char* kimg = smem;
   char* vimg = smem + IMG;
@@ -628,7 +634,11 @@ __global__ __launch_bounds__(BWD1_THREADS) __attribute__((amdgpu_waves_per_eu(BI
     const float inv = 1.0f / l_tot;
     // O rows in 16-B pieces (32 contiguous bytes per row per store instruction; the 8-B pieces of
     // the per-lane layout took half the kernel's time)
-    store_row_swap<HD>(acc, inv, qi < p.Nq ? p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD : nullptr, lane);
+    if constexpr (ROWS)
+      store_rows_lds1k<HD>(smem + 2 * IMG + wave * 1024, acc, inv, p.o_out + (int64_t)b * p.Nq * p.ldo + hh * HD,
+                           p.ldo, sl * 32, min(32, p.Nq - sl * 32), lane);
+    else
+      store_row_swap<HD>(acc, inv, qi < p.Nq ? p.o_out + ((int64_t)b * p.Nq + qi) * p.ldo + hh * HD : nullptr, lane);
     if (qi < p.Nq && h == 0) p.lse[((int64_t)b * p.H + hh) * p.Nq + qi] = m_run + log2f(l_tot);
   }
 }
@@ -669,6 +679,7 @@ constexpr int FK_RING = 8 * 2 * FK_SLOT;          // 8 waves x 2 slots
 constexpr int FK_SIMG = 32 * 64;                  // dS image [32 keys][32 queries] bf16, per wave
 constexpr int FK_KIMG = 32 * 128;                 // K rows of the active block
 constexpr int FK_LDS = FK_RING + 8 * FK_SIMG + FK_KIMG;
+constexpr int FK_NST = 4;  // dQ store instructions per sub-tile (bf16 rows through the dS image)
 static_assert(8 * 4 * 16 * 64 * 4 <= FK_RING, "the dK / dV partials fit the ring");
 }  // namespace
 
@@ -754,11 +765,11 @@ __device__ __forceinline__ void bwd1_few_keys(const AttnParams& p, char* smem, i
   const int sw4 = swz<32>(lane & 31);
   for (int i = 0; i < nmine; ++i) {
     // this sub-tile's 9 DMA instructions landed: younger than them are the next sub-tile's 9 (issued
-    // in iteration i - 1) and iteration i - 1's 8 dQ stores (inline asm, so exactly 8; CDNA4's
+    // in iteration i - 1) and iteration i - 1's dQ stores (inline asm, so exactly FK_NST; CDNA4's
     // vmcnt counts stores too)
-    if (i + 1 < nmine && i >= 1) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+    if (i + 1 < nmine && i >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(9 + FK_NST) : "memory");
     else if (i + 1 < nmine) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else if (i >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (i >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(FK_NST) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int q0 = (wave + 8 * i) * 32;
     char* slot = ring + (i & 1) * FK_SLOT;
@@ -842,9 +853,46 @@ __device__ __forceinline__ void bwd1_few_keys(const AttnParams& p, char* smem, i
       for (int qb = 0; qb < 2; ++qb)
         dqa[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[qb], (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     }
-    // the stores: 8 asm instructions while another sub-tile follows (only the last sub-tile of
+    // the stores: FK_NST asm instructions while another sub-tile follows (only the last sub-tile of
     // the (batch, head) can be ragged, and it is its wave's last)
     const bool last = i + 1 == nmine;
+    if (!p.dq_f32) {
+      // bf16 dQ as whole 128-B rows (round 6): each 16-query half through the wave's dS image (its
+      // reads are done), 16-B chunks XOR row & 7, then 8 rows per store instruction. The lane's
+      // pieces (4 dims of one query per head-dim block) as direct stores were 16 partial lines per
+      // instruction: the kernel ran 57 us against 34 us with no dQ stores at all (HBM-resident
+      // operands, tools/cross_bench.py, profiles/r06p_cross_stores.txt).
+      char* dimg = simg;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the image's previous reads are done
+        const int row = lane & 15;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          u32x2 w;
+          w[0] = pack2(dqa[db][qb][0] * p.scale, dqa[db][qb][1] * p.scale);
+          w[1] = pack2(dqa[db][qb][2] * p.scale, dqa[db][qb][3] * p.scale);
+          const int c = 2 * db + (g4 >> 1);
+          *(u32x2*)(dimg + row * 128 + ((c ^ (row & 7)) << 4) + 8 * (g4 & 1)) = w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        u32x4 rv[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int rr = 8 * h2 + (lane >> 3), c = lane & 7;
+          rv[h2] = *(const u32x4*)(dimg + rr * 128 + ((c ^ (rr & 7)) << 4));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int q = q0 + 16 * qb + 8 * h2 + (lane >> 3);
+          bf16_t* dst = (bf16_t*)p.dq + ((int64_t)b * p.Nq + min(q, p.Nq - 1)) * p.lddq + (int64_t)hh * HD + 8 * (lane & 7);
+          if (!last) asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(dst), "v"(rv[h2]) : "memory");
+          else if (q < p.Nq) *(u32x4*)dst = rv[h2];
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       const int q = q0 + 16 * qb + (lane & 15);
@@ -1327,6 +1375,7 @@ static AttnSwitches read_attn_switches() {
   w.w8 = num("LTX_ATTN_W8", LTX_ATTN_W8_DEFAULT);
   w.skip = off0("LTX_ATTN_SKIP");
   w.fwd1 = off0("LTX_ATTN_FWD1");
+  w.fwd1_rows = off0("LTX_ATTN_FWD1_ROWS");
   {  // off by default: its step A/B was neutral, and with it dK / dV of the unmasked keys are the sum
      // of two partials (f32 rounding away from the 8 x 32-key kernel; dQ stays bitwise)
     const char* e = std::getenv("LTX_ATTN_BWD1_QS");
@@ -1383,10 +1432,14 @@ static int launch_fwd(AttnParams p, hipStream_t s) {
       int z = nsl >= 16 ? 2 : 1;
       if (z == 2 && p.H * p.B < 128) z = std::max(2, std::min(nsl / 8, (256 + p.H * p.B - 1) / (p.H * p.B)));
       const dim3 g1((unsigned)p.H, (unsigned)p.B, (unsigned)z);
-      if (needs_bias(p))
-        hipLaunchKernelGGL((attn_fwd1_kernel<HD, true>), g1, dim3(BWD1_THREADS), 0, s, p);
-      else
-        hipLaunchKernelGGL((attn_fwd1_kernel<HD, false>), g1, dim3(BWD1_THREADS), 0, s, p);
+      const bool rows = attn_switches().fwd1_rows != 0;
+      if (needs_bias(p)) {
+        if (rows) hipLaunchKernelGGL((attn_fwd1_kernel<HD, true, true>), g1, dim3(BWD1_THREADS), 0, s, p);
+        else hipLaunchKernelGGL((attn_fwd1_kernel<HD, true, false>), g1, dim3(BWD1_THREADS), 0, s, p);
+      } else {
+        if (rows) hipLaunchKernelGGL((attn_fwd1_kernel<HD, false, true>), g1, dim3(BWD1_THREADS), 0, s, p);
+        else hipLaunchKernelGGL((attn_fwd1_kernel<HD, false, false>), g1, dim3(BWD1_THREADS), 0, s, p);
+      }
       LTX_LAUNCH_CHECK();
       return LTX_OK;
     }

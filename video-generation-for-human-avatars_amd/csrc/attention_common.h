@@ -150,6 +150,7 @@ struct AttnSwitches {
   int w8 = 1;           // LTX_ATTN_W8: bit 0 8-wave tiled forward, bit 1 8-wave dK/dV
   int skip = 1;         // LTX_ATTN_SKIP=0: one-pass kernels keep all-padding key blocks
   int fwd1 = 1;         // LTX_ATTN_FWD1=0: tiled forward for every key range
+  int fwd1_rows = 1;    // LTX_ATTN_FWD1_ROWS=0: the one-pass forward stores O in 32-B pieces
   int bwd1_qs = 0;      // LTX_ATTN_BWD1_QS=1: query-split one-pass backward for biased ranges
   int bwd1_few = 1;     // LTX_ATTN_BWD1_FEW=0: keep the 8 x 32-key schedule for few unmasked keys
   int qsplit = 1;       // LTX_ATTN_QSPLIT=0: one workgroup per (batch, head) at any H * B
@@ -264,6 +265,34 @@ __device__ __forceinline__ void xcd_block(int xcd_order, int& bx, int& by, int& 
 // different lines per instruction. Staged through a wave-private 4-KiB LDS slot (16-B chunks XOR
 // row & 7: conflict-free both ways), each store instruction then writes 8 whole 128-B rows.
 // `scale` multiplies before the bf16 rounding (the same values as the per-lane path).
+// The same through a 1-KiB slot, 8 rows per pass (4 passes): the lanes holding a pass's rows write
+// them, then every lane reads 16 B and one store instruction writes the pass's 8 whole rows.
+template <int HD>
+__device__ __forceinline__ void store_rows_lds1k(char* stage, const f32x16* acc, float scale, bf16_t* out,
+                                                 int64_t ld, int row0, int nrows, int lane) {
+  static_assert(HD == 64, "128-B rows");
+  const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+    if ((r >> 3) == ps) {  // each lane's row falls in exactly one pass
+      const int rl = r & 7;
+#pragma unroll
+      for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = d * 32 + 8 * g + 4 * h;
+          u32x2 w;
+          w[0] = pack2(acc[d][4 * g] * scale, acc[d][4 * g + 1] * scale);
+          w[1] = pack2(acc[d][4 * g + 2] * scale, acc[d][4 * g + 3] * scale);
+          *(u32x2*)(stage + rl * 128 + ((((col >> 3) ^ rl)) << 4) + ((col >> 2) & 1) * 8) = w;
+        }
+    }
+    const int rr = lane >> 3, c = lane & 7;
+    const u32x4 v = *(const u32x4*)(stage + rr * 128 + ((c ^ rr) << 4));
+    if (8 * ps + rr < nrows) *(u32x4*)(out + (int64_t)(row0 + 8 * ps + rr) * ld + c * 8) = v;
+  }
+}
+
 template <int HD>
 __device__ __forceinline__ void store_rows_lds(char* stage, const f32x16* acc, float scale, bf16_t* out,
                                                int64_t ld, int row0, int nrows, int lane) {

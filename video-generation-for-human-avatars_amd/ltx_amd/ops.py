@@ -359,7 +359,8 @@ def _env_on(var):
 _ATTN_ENV = ("LTX_ATTN_XCD", "LTX_ATTN_BWD1", "LTX_ATTN_W8", "LTX_ATTN_SKIP", "LTX_ATTN_FWD1",
              "LTX_ATTN_BWD1_QS", "LTX_ATTN_BWD1_FEW", "LTX_ATTN_QSPLIT", "LTX_ATTN_DKDV_W1",
              "LTX_ATTN_DQ_W1", "LTX_ATTN_DQ_PIPE", "LTX_ATTN_DQ_NBUF", "LTX_ATTN_FWD_W1",
-             "LTX_ATTN_FWD_PIPE", "LTX_ATTN_FWD_F32SUM", "LTX_ATTN_DKDV_PIPE", "LTX_ATTN_DKDV_NBUF")
+             "LTX_ATTN_FWD_PIPE", "LTX_ATTN_FWD_F32SUM", "LTX_ATTN_DKDV_PIPE", "LTX_ATTN_DKDV_NBUF",
+             "LTX_ATTN_FWD1_ROWS")
 _attn_env_seen = [None]
 
 
