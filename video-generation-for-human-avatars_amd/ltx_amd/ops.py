@@ -760,8 +760,11 @@ def lora_dy_da_enabled():
 
 
 def lora_dy_da_fits(y, x, r):
-    """lora_dy(y, ..., x=x) applies (and LTX_LORA_DY_DA is not 0)."""
-    return lora_dy_da_enabled() and lora_dy_fits(x, r) and y.shape[1] <= 2048 and x.shape[0] == y.shape[0]
+    """lora_dy(y, ..., x=x) applies (and LTX_LORA_DY_DA is not 0). Only at M >= 2048, where
+    ltx_lora_wgrad takes the same token-sized path, so the merged call is bitwise the separate ones
+    (below it ltx_lora_wgrad runs the f32-MFMA kernel: another rounding of dA)."""
+    return (lora_dy_da_enabled() and lora_dy_fits(x, r) and y.shape[1] <= 2048 and x.shape[0] == y.shape[0]
+            and y.shape[0] >= 2048)
 
 
 def lora_dy_fits(y, r):
