@@ -2,7 +2,9 @@
 N = 1792 queries, one shared 256-token prompt with 16 valid tokens: kv_shared, key bias -10000 on the
 padding keys, delta precomputed by the dO GEMM), timed with HIP events; the rocprofv3 target for
 their per-kernel traces and PMC passes (--iters small).
-  --env-ab NAME: time with NAME cycling through --env-vals, interleaved rounds (A/B in one process)."""
+  --env-ab NAME: time with NAME cycling through --env-vals, interleaved rounds (A/B in one process).
+  LTX_CROSS_ROTATE=1: rotate four q / dO sets (operands HBM-resident, as in the training step; the same
+  operands every call stay in the Infinity Cache and hide the store pattern)."""
 import argparse
 import os
 import sys
@@ -25,15 +27,15 @@ D = H * d
 dev = "cuda"
 _lib.ensure_device(dev)
 g = torch.Generator(device="cpu").manual_seed(0)
-ap2 = os.environ.get("LTX_CROSS_ROTATE", "0") == "1"  # rotate 4 operand sets (no cache reuse)
-qs = [torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16) for _ in range(4 if ap2 else 1)]
+rotate = os.environ.get("LTX_CROSS_ROTATE", "0") == "1"  # 4 operand sets: HBM-resident, as in the step
+qs = [torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16) for _ in range(4 if rotate else 1)]
 q = qs[0]
 kv = torch.randn(L, 2 * D, generator=g).to(dev, torch.bfloat16)
 k, v = kv[:, :D], kv[:, D:]
 bias = torch.zeros(1, L)
 bias[:, args.valid:] = -10000.0
 bias = bias.to(dev)
-dos = [torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16) for _ in range(4 if ap2 else 1)]
+dos = [torch.randn(B * N, D, generator=g).to(dev, torch.bfloat16) for _ in range(4 if rotate else 1)]
 do = dos[0]
 scale = d ** -0.5
 
