@@ -47,4 +47,13 @@ qkvs = [g(M, 3 * D) for _ in range(2)]
 qw, kw = g(D, scale=0.1) + 1, g(D, scale=0.1) + 1
 res["qk_rope_fwd_us"] = timeit(lambda: ops.qk_norm_rope_fwd((q := qkvs[next(it) % 2])[:, :D], q[:, D:2 * D], qw, kw,
                                                              rope))
+_, _, rq, rk = ops.qk_norm_rope_fwd(qkvs[0][:, :D], qkvs[0][:, D:2 * D], qw, kw, rope)
+
+
+def qk_bwd():
+    q = qkvs[next(it) % 2]
+    return ops.qk_norm_rope_bwd(xs[next(it) % 4], q[:, :D], qw, rq, xs[1], q[:, D:2 * D], kw, rk, rope)
+
+
+res["qk_rope_bwd_us"] = timeit(qk_bwd)
 print(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in res.items()}), flush=True)
